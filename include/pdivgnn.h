@@ -1,0 +1,219 @@
+/*
+ * pdivgnn.h — C ABI of libpdivgnn_hip.so, the MI355X (gfx950) implementation of
+ * the P-DivGNN hot path: EncodeProcessDecode forward/backward
+ * (gnn_local_stress/models.py:98-326) and the divergence-regularised loss
+ * (scripts/gnn_train.py:41-92).
+ *
+ * The reference is pure Python over PyTorch ATen + torch_geometric; it has no
+ * FFI of its own.  Each entry point below replaces the group of ATen/PyG ops
+ * named in its comment (file:line of the reference call site).  The Python
+ * mirror (p-div-gnn_amd/gnn_local_stress) binds them with ctypes; INTEGRATION.md
+ * shows the binding a maintainer would add to the reference.
+ *
+ * Conventions (all entry points):
+ *   - device pointers to fp32 / int32 arrays; latent tensors are row-major
+ *     (rows x 128) fp32, natural feature order, 16-byte aligned;
+ *   - `stream` is a hipStream_t passed as void* (0 = null stream);
+ *   - kernels never allocate; partial-sum buffers are caller-provided, sized
+ *     by pdg_max_blocks();
+ *   - return 0 on success, otherwise a nonzero code; pdg_last_error() gives
+ *     the message of the last failure on the calling thread;
+ *   - edges are in dst-sorted order (CSR over edge_index[1]); `src`/`dst` are
+ *     the endpoints of each dst-sorted edge, `rowptr` the dst-CSR offsets.
+ */
+#ifndef PDIVGNN_H
+#define PDIVGNN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PDG_LATENT 128
+#define PDG_OK 0
+#define PDG_ERR_ARG 1
+#define PDG_ERR_HIP 2
+
+/* Graph-LayerNorm statistics of one call (torch_geometric LayerNorm, mode="graph", batch=None). */
+typedef struct pdg_ln_stat {
+  float mean;   /* mean over all rows x channels of the call */
+  float den;    /* std_pop + eps (the forward divides by it) */
+  float rstd;   /* 1 / den */
+  float std_;   /* population std */
+  double mean_d, std_d, count; /* fp64 copies and the element count M */
+} pdg_ln_stat;
+
+/* Backward scalars of one graph-LayerNorm call. */
+typedef struct pdg_ln_bwd {
+  float c1, c2;
+  double S1, S2;
+} pdg_ln_bwd;
+
+/* ---------------------------------------------------------------- library */
+const char* pdg_last_error(void);
+int pdg_version(void);
+/* Upper bound on the number of per-block partials any launcher writes. */
+int pdg_max_blocks(void);
+
+/* ---------------------------------------------------------------- forward */
+
+/* models.py:140-152 (format_node_features) + :154-162, :303-307 (format_edge_features):
+ * x_in[n] = [(mean_stress-mu)/s (3), (pos-mu)/s (2), node_type (1)]; e_in[k] = (edge_attr[perm[k]]-mu)/s.
+ * stats8 = {mean_pos, std_pos, mean_mean_stress, std_mean_stress, mean_local_stress,
+ *           std_local_stress, mean_edge_weight, std_edge_weight} (device, fp32). */
+int pdg_format_inputs(int n_nodes, int n_edges, const float* pos, const float* mean_stress,
+                      const int64_t* node_types, const float* edge_attr, const int* perm,
+                      const float* stats8, int scale_input, float* x_in, float* e_in, void* stream);
+
+/* Encoder MLP (models.py:260-274): a1 = relu(W0 x + b0) (K = in_features in {1..8}),
+ * a2 = relu(W2 a1 + b2); writes a1, a2 and per-block LayerNorm partials (sum, sumsq). */
+int pdg_encoder_fwd(int rows, int in_features, const float* x_in, const float* W0, const float* b0,
+                    const float* W2, const float* b2, float* a1, float* a2,
+                    double* partials, int* nparts, void* stream);
+
+/* Reduce LayerNorm partials -> statistics (mean, std_pop + eps). */
+int pdg_ln_finalize(const double* partials, int nparts, double count, pdg_ln_stat* out, void* stream);
+
+/* Processor node pre-pass (models.py:221/236 re-associated): x_t = LN(a2_prev) [+ x_res];
+ * P = W1[:, 0:128] x_t, Q = W1[:, 128:256] x_t  (W1 = processor.edge_net.0.weight, 128 x 384). */
+int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                const float* ln_b, const float* x_res, float* x_out, const float* W1,
+                float* P, float* Q, void* stream);
+
+/* Fused edge pass of one message-passing step (models.py:215-222, :233-238):
+ * e_t = LN(a2_prev) [+ e_res]; C = W1[:, 256:384] e_t + b1;
+ * message:  a1m = relu(C + P[dst] + Q[src]), a2m = relu(W2 a1m + b2)
+ * edge upd: a1e = relu(C + P[src] + Q[dst]), a2e = relu(W2 a1e + b2)
+ * writes e_t, a1m, a2m, a1e, a2e and LayerNorm partials of a2m and a2e. */
+int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                 const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
+                 const float* P, const float* Q, const float* W1, const float* b1,
+                 const float* W2, const float* b2, float* a1m, float* a2m, float* a1e, float* a2e,
+                 double* part_m, double* part_e, int* nparts, void* stream);
+
+/* PyG "add" aggregation (scatter_add_ at edge_index[1]) of LN-normalised rows:
+ * out[v] = sum_{k in rowptr[v]..rowptr[v+1]} LN(rows[k]); st == NULL -> raw rows. */
+int pdg_segment_sum(int n_nodes, const int* rowptr, const float* rows, const pdg_ln_stat* st,
+                    const float* ln_g, const float* ln_b, float* out, void* stream);
+
+/* Processor.update first layer (models.py:240-243, :202-204):
+ * a1n = relu(Wn1[:, 0:128] aggr + Wn1[:, 128:256] x + bn1). */
+int pdg_node_mlp1(int n_nodes, const float* aggr, const float* x, const float* Wn1,
+                  const float* bn1, float* a1n, void* stream);
+
+/* Second MLP layer with LN partials: a2 = relu(W2 a1 + b2). */
+int pdg_mlp2_fwd(int rows, const float* a1, const float* W2, const float* b2, float* a2,
+                 double* partials, int* nparts, void* stream);
+
+/* Decoder (models.py:282-286, :316-321): x_S = LN(a2_prev) + x_res; a1d = relu(Wd1 x_S + bd1);
+ * y = Wd2 a1d + bd2 (3 outputs); if scale_output: y = y * std_local_stress + mean_local_stress. */
+int pdg_decoder_fwd(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                    const float* ln_b, const float* x_res, float* x_out, const float* Wd1,
+                    const float* bd1, float* a1d, const float* Wd2, const float* bd2,
+                    const float* stats8, int scale_output, float* y, void* stream);
+
+/* torch.any(x != 0) into *flag (int, device). models.py:294 */
+int pdg_any_nonzero(const float* x, int64_t n, int* flag, void* stream);
+
+/* ---------------------------------------------------------------- backward */
+
+/* Decoder backward: gz1d = (Wd2^T gy) * [a1d > 0]; gx = Wd1^T gz1d. */
+int pdg_decoder_bwd(int n_nodes, const float* gy, const float* a1d, const float* Wd2,
+                    const float* Wd1T, float* gz1d, float* gx, void* stream);
+
+/* Per-channel LayerNorm backward sums over rows: sum gy, sum gy*xhat (xhat from a2 and st);
+ * gy row k = gy_rows[gidx ? gidx[k] : k]. Writes per-block partials (2 x 128 doubles each). */
+int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, const float* a2,
+                  const pdg_ln_stat* st, double* partials, int* nparts, void* stream);
+
+/* Reduce colsum partials: grad_b += sum gy, grad_g += sum gy*xhat, and the call's
+ * backward scalars (S1 = sum g*gy, S2 = sum g*gy*xhat). */
+int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g,
+                           const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
+                           void* stream);
+
+/* MLP tail backward (LN -> relu -> Linear2 -> relu): ga2 = LNbwd(gy); gz2 = ga2 * [a2 > 0];
+ * gz1 = (W2^T gz2) * [a1 > 0].  gy row k = gy_rows[gidx ? gidx[k] : k]. */
+int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a2, const float* a1,
+                 const pdg_ln_stat* st, const pdg_ln_bwd* lb, const float* ln_g, const float* W2T,
+                 float* gz2, float* gz1, void* stream);
+
+/* out0 = W0T in [+ res0]; out1 = W1T in [+ res1]  (two 128x128 products of one input). */
+int pdg_gemm_dual(int rows, const float* in, const float* W0T, const float* W1T,
+                  const float* res0, const float* res1, float* out0, float* out1, void* stream);
+
+/* out = res + W0T in0 + W1T in1. */
+int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
+                  const float* res, float* out, void* stream);
+
+/* Fused edge backward of one step: both edge_net evaluations' LN/relu/Linear2 backward
+ * (message: gy = gaggr[dst]; edge update: gy = ge_next), gC = gz1m + gz1e,
+ * ge_out = ge_next + WcT gC.  Writes gz2m, gz1m, gz2e, gz1e, gC, ge_out. */
+int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
+                 const float* a2m, const float* a1m, const float* a2e, const float* a1e,
+                 const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
+                 const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, const float* WcT,
+                 float* gz2m, float* gz1m, float* gz2e, float* gz1e, float* gC, float* ge_out,
+                 void* stream);
+
+/* Backward of the P/Q gathers: gP[v] = sum_{dst-seg(v)} gz1m + sum_{src-seg(v)} gz1e,
+ * gQ[v] = sum_{src-seg(v)} gz1m + sum_{dst-seg(v)} gz1e.  src-seg uses rowptr_src and
+ * perm_src (positions of the dst-sorted edges grouped by src). */
+int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int* rowptr_src,
+                       const int* perm_src, const float* gz1m, const float* gz1e,
+                       float* gP, float* gQ, void* stream);
+
+/* Weight gradient of a 128x128 Linear: per-block partial of sum_k G[k]^T X[k] (+ a second
+ * pair G2/X2) and of sum_k G[k] (+G2); accumulated (+=) into slab[block] (128*128 + 128 floats),
+ * so repeated calls over message-passing steps sum in a fixed order. */
+int pdg_wgrad_accum(int rows, const float* G, const float* X, const float* G2, const float* X2,
+                    float* slabs, int nslabs, void* stream);
+/* grad_W[o*ld + col0 + i] += sum over slabs; grad_b[o] += (if grad_b) sum over slabs. */
+int pdg_wgrad_reduce(const float* slabs, int nslabs, float* grad_W, int ld, int col0,
+                     float* grad_b, void* stream);
+/* Narrow weight gradient: T[c][i] = sum_k Wide[k][c] Narrow[k][i] (c < 128, i < k_narrow <= 8),
+ * sums sum_k Wide[k][c] and sum_k Narrow[k][i]; added into grad arrays:
+ * transpose == 0: grad_W[c*k_narrow + i] (shape 128 x k), else grad_W[i*128 + c] (k x 128);
+ * grad_b_wide[c] += ..., grad_b_narrow[i] += ... (each nullable). */
+int pdg_wgrad_narrow(int rows, const float* wide, const float* narrow, int k_narrow, int transpose,
+                     double* partials, float* grad_W, float* grad_b_wide, float* grad_b_narrow,
+                     void* stream);
+
+/* ---------------------------------------------------------------- losses */
+
+/* Per-graph normalised MSE (gnn_train.py:41-57) over node segments ptr[0..B]:
+ * loss_g = mean_c sum_n (gt-pred)^2 / sum_n (gt - mean gt)^2.  Writes loss[g] and den[g*3+c]. */
+int pdg_nmse_fwd(int n_graphs, const int* ptr, const float* gt, const float* pred,
+                 float* loss, float* den, void* stream);
+/* g_pred[n][c] (+)= scale * (-2/3) (gt-pred)/den_c. */
+int pdg_nmse_bwd(int n_graphs, const int* ptr, int n_nodes, const float* gt, const float* pred,
+                 const float* den, const float* scale, int accumulate, float* g_pred, void* stream);
+
+/* Divergence penalty (gnn_train.py:60-92) with the operator in CSR over global rows and
+ * graph-local columns (col < n_i: x-derivative, else y-derivative), ptr = node offsets:
+ * div[v] = A_v . [[sxx;sxy],[sxy;syy]], rows with node_type +-1 zeroed, loss_g = mean_v |div|^2. */
+int pdg_div_fwd(int n_graphs, const int* ptr, const int* a_rowptr, const int* a_col,
+                const float* a_val, const int64_t* node_types, const float* sigma, int reduce_abs,
+                float* div, float* loss, void* stream);
+/* g_sigma (+)= A^T-weighted grads: uses A^T in CSR (at_rowptr over global nodes, at_row = source
+ * row v, at_comp = 0/1 (x/y column block), at_val).  d loss_g / d div = 2 div / n_g ("square")
+ * or sign(div) / n_g ("abs"), times *scale. */
+int pdg_div_bwd(int n_graphs, const int* ptr, int n_nodes, const int* at_rowptr, const int* at_row,
+                const int* at_comp, const float* at_val, const float* div, const float* scale,
+                int reduce_abs, int accumulate, float* g_sigma, void* stream);
+
+/* ---------------------------------------------------------------- utilities */
+/* out (cols x rows, contiguous) = in^T for a (rows x cols) row-major matrix with row stride ld. */
+int pdg_transpose(int rows, int cols, int ld, const float* in, float* out, void* stream);
+/* *flag = 1 if any grad element is inf/NaN (GradScaler's skip test, gnn_train.py:205-207). */
+int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream);
+/* Adam (torch.optim.Adam, amsgrad=False, weight_decay=0) on a flat parameter buffer; a no-op
+ * when skip_flag (nullable, device) is set. */
+int pdg_adam(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+             float lr, float beta1, float beta2, float eps, int step, const int* skip_flag, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PDIVGNN_H */

@@ -1,0 +1,72 @@
+"""Build libpdivgnn_hip.so (all HIP kernels + the C ABI of include/pdivgnn.h) for gfx950.
+
+    python p-div-gnn_amd/build.py [--force] [--report]
+
+Compiles each csrc/*.hip with hipcc in parallel and links one shared library into
+pdg/ (in-tree, so it travels to the GPU box with the repo snapshot)."""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+OUT = HERE / "pdg" / "libpdivgnn_hip.so"
+BUILD = HERE / "build"
+ARCH = os.environ.get("PDG_OFFLOAD_ARCH", "gfx950")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and Path(c).exists():
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _compile(src: Path, report: bool) -> Path:
+    obj = BUILD / (src.stem + ".o")
+    deps = [src] + list(CSRC.glob("*.hpp")) + [HERE.parent / "include" / "pdivgnn.h"]
+    if obj.exists() and all(obj.stat().st_mtime >= d.stat().st_mtime for d in deps) and not report:
+        return obj
+    cmd = [hipcc(), *FLAGS, "-c", str(src), "-o", str(obj)]
+    if report:
+        cmd.append("-Rpass-analysis=kernel-resource-usage")
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stderr}")
+    if report:
+        (BUILD / (src.stem + ".res")).write_text(r.stderr)
+    return obj
+
+
+def build(force: bool = False, report: bool = False) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    srcs = sorted(CSRC.glob("*.hip"))
+    if force:
+        for o in BUILD.glob("*.o"):
+            o.unlink()
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
+        objs = list(ex.map(lambda s: _compile(s, report), srcs))
+    if force or not OUT.exists() or any(o.stat().st_mtime > OUT.stat().st_mtime for o in objs):
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr}")
+    return OUT
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--report", action="store_true", help="write per-kernel register/spill report")
+    a = ap.parse_args()
+    out = build(force=a.force, report=a.report)
+    print(out)
+    if a.report:
+        subprocess.run([sys.executable, str(HERE / "tools" / "regs.py"), *map(str, sorted(BUILD.glob("*.res")))])

@@ -1,0 +1,448 @@
+// Backward kernels of the P-DivGNN hot path (autograd of gnn_local_stress/models.py:288-326).
+//
+// Conventions: pdg_common.hpp.  Transposed weights (W^T) are passed explicitly
+// (pdg_transpose), so every LDS image is built with contiguous 16-byte loads.
+//
+// graph-LayerNorm backward (PyG LayerNorm mode="graph", y = g*xhat + b,
+// xhat = (a - mean)/(std + eps)), over all M = rows*128 elements of a call:
+//   ga = rstd * (g*gy - S1/M) - xhat * S2 / (M*std),  S1 = sum g*gy,  S2 = sum g*gy*xhat
+// S1/S2 come from the per-channel sums (pdg_ln_colsum*), which are also the
+// LayerNorm parameter gradients.
+#include "pdg_common.hpp"
+#include "pdg_runtime.hpp"
+
+using namespace pdg;
+
+// ga2 -> gz2 for one fragment (in place on gy): LN backward and relu mask.
+__device__ __forceinline__ void ln_relu_bwd(float (&gy)[64], const float (&a2)[64], const LNStat& st,
+                                            const pdg_ln_bwd& lb, const float* __restrict__ g) {
+  const f32x4* gp = reinterpret_cast<const f32x4*>(g + half_off());
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const f32x4 gg = gp[t];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = 4 * t + j;
+      const float xhat = div_den(a2[s] - st.mean, st.den, st.rstd);
+      const float ga = st.rstd * (gg[j] * gy[s] - lb.c1) - xhat * lb.c2;
+      gy[s] = a2[s] > 0.f ? ga : 0.f;
+    }
+    if ((t & 3) == 3) PDG_FENCE();
+  }
+}
+
+__device__ __forceinline__ void relu_mask_acc(float (&v)[64], const f32x16 (&acc)[4], const float (&a)[64]) {
+  PDG_FOR_FRAG(s) v[s] = a[s] > 0.f ? ACC(acc, s) : 0.f;
+}
+
+// ============================================================================ decoder backward
+__global__ __launch_bounds__(256, 2) void decoder_bwd_kernel(int N, const float* __restrict__ gy,
+                                                              const float* __restrict__ a1d,
+                                                              const float* __restrict__ Wd2,
+                                                              const float* __restrict__ Wd1T,
+                                                              float* __restrict__ gz1d,
+                                                              float* __restrict__ gx) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* w2l = lds + WBLK;   // Wd2 (3 x 128)
+  load_wblock(lds, Wd1T, L, 0);
+  for (int i = threadIdx.x; i < 3 * L; i += blockDim.x) w2l[i] = Wd2[i];
+  __syncthreads();
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(N);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < N;
+    const int rc = valid ? row : N - 1;
+    const float g0 = gy[(size_t)rc * 3], g1 = gy[(size_t)rc * 3 + 1], g2 = gy[(size_t)rc * 3 + 2];
+    float v[64];
+    const int ho = half_off();
+    const float* w0 = w2l + ho;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 a[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[t] = reinterpret_cast<const f32x4*>(a1d + (size_t)rc * L + ho + 16 * q)[t];
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int s = 16 * q + 4 * t + j;
+          const float ga = fmaf(g2, w0[2 * L + s], fmaf(g1, w0[L + s], g0 * w0[s]));
+          v[s] = a[t][j] > 0.f ? ga : 0.f;
+        }
+      PDG_FENCE();
+    }
+    if (valid) store_frag(gz1d + (size_t)row * L, v);
+    f32x16 acc[4];
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    if (valid) store_acc(gx + (size_t)row * L, acc);
+  }
+}
+
+extern "C" int pdg_decoder_bwd(int n_nodes, const float* gy, const float* a1d, const float* Wd2,
+                               const float* Wd1T, float* gz1d, float* gx, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_decoder_bwd: n_nodes must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(a1d) && PDG_ALIGNED(gz1d) && PDG_ALIGNED(gx) && PDG_ALIGNED(Wd1T),
+                "pdg_decoder_bwd: misaligned pointer");
+  const int grid = persistent_grid(n_nodes, 4, 2);
+  hipLaunchKernelGGL(decoder_bwd_kernel, dim3(grid), dim3(256), (WBLK + 3 * L) * sizeof(float), (hipStream_t)stream,
+                     n_nodes, gy, a1d, Wd2, Wd1T, gz1d, gx);
+  PDG_CHECK_LAUNCH("pdg_decoder_bwd");
+  return PDG_OK;
+}
+
+// ============================================================================ LN column sums
+// Half-wave per row (lane j: channels 4j..4j+3); fp64 accumulation; block partial
+// = [sum gy (128) | sum gy*xhat (128)].
+__global__ __launch_bounds__(256) void ln_colsum_kernel(int M, const float* __restrict__ gyr,
+                                                        const int* __restrict__ gidx,
+                                                        const float* __restrict__ a2,
+                                                        const pdg_ln_stat* __restrict__ stp,
+                                                        double* __restrict__ part) {
+  __shared__ double red[8][256];
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const int nhw = blockDim.x >> 5;
+  const float mean = stp->mean, den = stp->den, rstd = stp->rstd;
+  double sg[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
+  for (int k = blockIdx.x * nhw + hw; k < M; k += gridDim.x * nhw) {
+    const int gr = gidx ? gidx[k] : k;
+    const f32x4 g = reinterpret_cast<const f32x4*>(gyr + (size_t)gr * L)[j];
+    const f32x4 a = reinterpret_cast<const f32x4*>(a2 + (size_t)k * L)[j];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float xhat = div_den(a[c] - mean, den, rstd);
+      sg[c] += (double)g[c];
+      sx[c] += (double)(g[c] * xhat);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    red[hw][4 * j + c] = sg[c];
+    red[hw][128 + 4 * j + c] = sx[c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    double s = 0;
+    for (int w = 0; w < nhw; ++w) s += red[w][i];
+    part[(size_t)blockIdx.x * 256 + i] = s;
+  }
+}
+
+extern "C" int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, const float* a2,
+                             const pdg_ln_stat* st, double* partials, int* nparts, void* stream) {
+  PDG_CHECK_ARG(rows > 0, "pdg_ln_colsum: rows must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(gy_rows) && PDG_ALIGNED(a2), "pdg_ln_colsum: misaligned pointer");
+  long want = (rows + 7) / 8;
+  long cap = (long)device_cus() * 2;
+  if (cap > MAX_BLOCKS) cap = MAX_BLOCKS;
+  const int grid = (int)(want < cap ? want : cap);
+  hipLaunchKernelGGL(ln_colsum_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, gy_rows, gidx, a2, st,
+                     partials);
+  PDG_CHECK_LAUNCH("pdg_ln_colsum");
+  if (nparts) *nparts = grid;
+  return PDG_OK;
+}
+
+__global__ void ln_colsum_finalize_kernel(const double* __restrict__ part, int n, const float* __restrict__ g,
+                                          const pdg_ln_stat* __restrict__ stp, float* __restrict__ grad_g,
+                                          float* __restrict__ grad_b, pdg_ln_bwd* __restrict__ out) {
+  __shared__ double red[2 * 16];
+  const int c = threadIdx.x;  // 128 threads, one channel each
+  double sg = 0, sx = 0;
+  for (int b = 0; b < n; ++b) {
+    sg += part[(size_t)b * 256 + c];
+    sx += part[(size_t)b * 256 + 128 + c];
+  }
+  if (grad_b) grad_b[c] += (float)sg;
+  if (grad_g) grad_g[c] += (float)sx;
+  double s1 = (double)g[c] * sg, s2 = (double)g[c] * sx;
+  block_sum2(s1, s2, red);
+  if (threadIdx.x == 0) {
+    const double M = stp->count;
+    const double sd = stp->std_d;
+    pdg_ln_bwd r;
+    r.S1 = s1;
+    r.S2 = s2;
+    r.c1 = (float)(s1 / M);
+    r.c2 = sd > 0 ? (float)(s2 / (M * sd)) : 0.f;
+    *out = r;
+  }
+}
+
+extern "C" int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g,
+                                      const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
+                                      void* stream) {
+  PDG_CHECK_ARG(nparts > 0, "pdg_ln_colsum_finalize: no partials");
+  hipLaunchKernelGGL(ln_colsum_finalize_kernel, dim3(1), dim3(128), 0, (hipStream_t)stream, partials, nparts, ln_g,
+                     st, grad_g, grad_b, out);
+  PDG_CHECK_LAUNCH("pdg_ln_colsum_finalize");
+  return PDG_OK;
+}
+
+// ============================================================================ MLP tail backward
+__global__ __launch_bounds__(256, 2) void mlp2_bwd_kernel(int M, const float* __restrict__ gyr,
+                                                           const int* __restrict__ gidx,
+                                                           const float* __restrict__ a2,
+                                                           const float* __restrict__ a1,
+                                                           const pdg_ln_stat* __restrict__ stp,
+                                                           const pdg_ln_bwd* __restrict__ lbp,
+                                                           const float* __restrict__ lg,
+                                                           const float* __restrict__ W2T,
+                                                           float* __restrict__ gz2, float* __restrict__ gz1) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  load_wblock(lds, W2T, L, 0);
+  __syncthreads();
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const pdg_ln_bwd lb = *lbp;
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(M);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < M;
+    const int rc = valid ? row : M - 1;
+    const int gr = gidx ? gidx[rc] : rc;
+    float v[64], a[64];
+    load_frag(v, gyr + (size_t)gr * L);
+    load_frag(a, a2 + (size_t)rc * L);
+    ln_relu_bwd(v, a, st, lb, lg);
+    if (valid) store_frag(gz2 + (size_t)row * L, v);
+    f32x16 acc[4];
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    load_frag(a, a1 + (size_t)rc * L);
+    relu_mask_acc(v, acc, a);
+    if (valid) store_frag(gz1 + (size_t)row * L, v);
+  }
+}
+
+extern "C" int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a2, const float* a1,
+                            const pdg_ln_stat* st, const pdg_ln_bwd* lb, const float* ln_g, const float* W2T,
+                            float* gz2, float* gz1, void* stream) {
+  PDG_CHECK_ARG(rows > 0, "pdg_mlp2_bwd: rows must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(gy_rows) && PDG_ALIGNED(a2) && PDG_ALIGNED(a1) && PDG_ALIGNED(gz2) &&
+                    PDG_ALIGNED(gz1) && PDG_ALIGNED(W2T),
+                "pdg_mlp2_bwd: misaligned pointer");
+  const int grid = persistent_grid(rows, 4, 2);
+  hipLaunchKernelGGL(mlp2_bwd_kernel, dim3(grid), dim3(256), WBLK * sizeof(float), (hipStream_t)stream, rows,
+                     gy_rows, gidx, a2, a1, st, lb, ln_g, W2T, gz2, gz1);
+  PDG_CHECK_LAUNCH("pdg_mlp2_bwd");
+  return PDG_OK;
+}
+
+// ============================================================================ dual / summed GEMMs
+__global__ __launch_bounds__(512, 2) void gemm_dual_kernel(int M, const float* __restrict__ in,
+                                                            const float* __restrict__ W0T,
+                                                            const float* __restrict__ W1T,
+                                                            const float* __restrict__ res0,
+                                                            const float* __restrict__ res1,
+                                                            float* __restrict__ out0, float* __restrict__ out1) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  load_wblock(lds, W0T, L, 0);
+  load_wblock(lds + WBLK, W1T, L, 0);
+  __syncthreads();
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(M);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < M;
+    const int rc = valid ? row : M - 1;
+    float v[64], r[64];
+    load_frag(v, in + (size_t)rc * L);
+    f32x16 acc[4];
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    if (res0) {
+      load_frag(r, res0 + (size_t)rc * L);
+      PDG_FOR_FRAG(s) ACC(acc, s) += r[s];
+    }
+    if (valid) store_acc(out0 + (size_t)row * L, acc);
+    zero_acc(acc);
+    gemm128(acc, lds + WBLK, v);
+    if (res1) {
+      load_frag(r, res1 + (size_t)rc * L);
+      PDG_FOR_FRAG(s) ACC(acc, s) += r[s];
+    }
+    if (valid) store_acc(out1 + (size_t)row * L, acc);
+  }
+}
+
+extern "C" int pdg_gemm_dual(int rows, const float* in, const float* W0T, const float* W1T, const float* res0,
+                             const float* res1, float* out0, float* out1, void* stream) {
+  PDG_CHECK_ARG(rows > 0, "pdg_gemm_dual: rows must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(in) && PDG_ALIGNED(out0) && PDG_ALIGNED(out1) && PDG_ALIGNED(W0T) &&
+                    PDG_ALIGNED(W1T) && (!res0 || PDG_ALIGNED(res0)) && (!res1 || PDG_ALIGNED(res1)),
+                "pdg_gemm_dual: misaligned pointer");
+  const int grid = persistent_grid(rows, 8, 1);
+  hipLaunchKernelGGL(gemm_dual_kernel, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream, rows,
+                     in, W0T, W1T, res0, res1, out0, out1);
+  PDG_CHECK_LAUNCH("pdg_gemm_dual");
+  return PDG_OK;
+}
+
+__global__ __launch_bounds__(512, 2) void gemm_sum2_kernel(int M, const float* __restrict__ in0,
+                                                            const float* __restrict__ in1,
+                                                            const float* __restrict__ W0T,
+                                                            const float* __restrict__ W1T,
+                                                            const float* __restrict__ res,
+                                                            float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  load_wblock(lds, W0T, L, 0);
+  load_wblock(lds + WBLK, W1T, L, 0);
+  __syncthreads();
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(M);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < M;
+    const int rc = valid ? row : M - 1;
+    float v[64];
+    f32x16 acc[4];
+    zero_acc(acc);
+    load_frag(v, in0 + (size_t)rc * L);
+    gemm128(acc, lds, v);
+    load_frag(v, in1 + (size_t)rc * L);
+    gemm128(acc, lds + WBLK, v);
+    if (res) {
+      load_frag(v, res + (size_t)rc * L);
+      PDG_FOR_FRAG(s) ACC(acc, s) += v[s];
+    }
+    if (valid) store_acc(out + (size_t)row * L, acc);
+  }
+}
+
+extern "C" int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
+                             const float* res, float* out, void* stream) {
+  PDG_CHECK_ARG(rows > 0, "pdg_gemm_sum2: rows must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(in0) && PDG_ALIGNED(in1) && PDG_ALIGNED(out) && PDG_ALIGNED(W0T) &&
+                    PDG_ALIGNED(W1T) && (!res || PDG_ALIGNED(res)),
+                "pdg_gemm_sum2: misaligned pointer");
+  const int grid = persistent_grid(rows, 8, 1);
+  hipLaunchKernelGGL(gemm_sum2_kernel, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream, rows,
+                     in0, in1, W0T, W1T, res, out);
+  PDG_CHECK_LAUNCH("pdg_gemm_sum2");
+  return PDG_OK;
+}
+
+// ============================================================================ fused edge backward
+__global__ __launch_bounds__(512, 2) void edge_bwd_kernel(
+    int E, const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
+    const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
+    const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ stm_p, const pdg_ln_stat* __restrict__ ste_p,
+    const pdg_ln_bwd* __restrict__ lbm_p, const pdg_ln_bwd* __restrict__ lbe_p, const float* __restrict__ lg,
+    const float* __restrict__ W2T, const float* __restrict__ WcT, float* __restrict__ gz2m,
+    float* __restrict__ gz1m, float* __restrict__ gz2e, float* __restrict__ gz1e, float* __restrict__ gC,
+    float* __restrict__ ge_out) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  load_wblock(lds, W2T, L, 0);
+  load_wblock(lds + WBLK, WcT, L, 0);
+  __syncthreads();
+  const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
+  const LNStat ste = *reinterpret_cast<const LNStat*>(ste_p);
+  const pdg_ln_bwd lbm = *lbm_p, lbe = *lbe_p;
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(E);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < E;
+    const int rc = valid ? row : E - 1;
+    const int d_node = dst[rc];
+    float v[64], a[64];
+    f32x16 acc[4];
+    // ---- message path: gy = gaggr[dst]   (scatter_add_ backward = gather)
+    load_frag(v, gaggr + (size_t)d_node * L);
+    load_frag(a, a2m + (size_t)rc * L);
+    ln_relu_bwd(v, a, stm, lbm, lg);
+    if (valid) store_frag(gz2m + (size_t)row * L, v);
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    load_frag(a, a1m + (size_t)rc * L);
+    relu_mask_acc(v, acc, a);
+    if (valid) store_frag(gz1m + (size_t)row * L, v);
+    // ---- edge-update path: gy = ge_next
+    load_frag(v, ge_next + (size_t)rc * L);
+    load_frag(a, a2e + (size_t)rc * L);
+    ln_relu_bwd(v, a, ste, lbe, lg);
+    if (valid) store_frag(gz2e + (size_t)row * L, v);
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    load_frag(a, a1e + (size_t)rc * L);
+    relu_mask_acc(v, acc, a);
+    if (valid) store_frag(gz1e + (size_t)row * L, v);
+    // ---- gC = gz1m + gz1e (gz1m re-read from this lane's own store);  ge_out = ge_next + Wc^T gC
+    load_frag(a, gz1m + (size_t)(valid ? row : rc) * L);
+    PDG_FOR_FRAG(s) v[s] += a[s];
+    if (valid) store_frag(gC + (size_t)row * L, v);
+    zero_acc(acc);
+    gemm128(acc, lds + WBLK, v);
+    load_frag(a, ge_next + (size_t)rc * L);
+    PDG_FOR_FRAG(s) ACC(acc, s) += a[s];
+    if (valid) store_acc(ge_out + (size_t)row * L, acc);
+  }
+}
+
+extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
+                            const float* a2m, const float* a1m, const float* a2e, const float* a1e,
+                            const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
+                            const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, const float* WcT,
+                            float* gz2m, float* gz1m, float* gz2e, float* gz1e, float* gC, float* ge_out,
+                            void* stream) {
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd: n_edges must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(ge_next) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) &&
+                    PDG_ALIGNED(a2e) && PDG_ALIGNED(a1e) && PDG_ALIGNED(gz2m) && PDG_ALIGNED(gz1m) &&
+                    PDG_ALIGNED(gz2e) && PDG_ALIGNED(gz1e) && PDG_ALIGNED(gC) && PDG_ALIGNED(ge_out),
+                "pdg_edge_bwd: misaligned pointer");
+  PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd: ge_out must not alias ge_next");
+  const int grid = persistent_grid(n_edges, 8, 1);
+  hipLaunchKernelGGL(edge_bwd_kernel, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+                     n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
+                     gz1m, gz2e, gz1e, gC, ge_out);
+  PDG_CHECK_LAUNCH("pdg_edge_bwd");
+  return PDG_OK;
+}
+
+// ============================================================================ P/Q gather backward
+__global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* __restrict__ rpd,
+                                                             const int* __restrict__ rps,
+                                                             const int* __restrict__ perm_s,
+                                                             const float* __restrict__ gz1m,
+                                                             const float* __restrict__ gz1e,
+                                                             float* __restrict__ gP, float* __restrict__ gQ) {
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const int nhw = blockDim.x >> 5;
+  for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
+    f32x4 p = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
+    const int d0 = rpd[v], d1 = rpd[v + 1];
+    for (int k = d0; k < d1; ++k) {   // edges whose target is v: message x_i, edge-update x[col]
+      p += reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
+      q += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+    }
+    const int s0 = rps[v], s1 = rps[v + 1];
+    for (int i = s0; i < s1; ++i) {   // edges whose source is v: message x_j, edge-update x[row]
+      const int k = perm_s[i];
+      q += reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
+      p += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+    }
+    reinterpret_cast<f32x4*>(gP + (size_t)v * L)[j] = p;
+    reinterpret_cast<f32x4*>(gQ + (size_t)v * L)[j] = q;
+  }
+}
+
+extern "C" int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int* rowptr_src, const int* perm_src,
+                                  const float* gz1m, const float* gz1e, float* gP, float* gQ, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_pq_scatter_bwd: n_nodes must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(gz1m) && PDG_ALIGNED(gz1e) && PDG_ALIGNED(gP) && PDG_ALIGNED(gQ),
+                "pdg_pq_scatter_bwd: misaligned pointer");
+  long want = (n_nodes + 7) / 8;
+  long cap = (long)device_cus() * 8;
+  const int grid = (int)(want < cap ? want : cap);
+  hipLaunchKernelGGL(pq_scatter_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, rowptr_dst,
+                     rowptr_src, perm_src, gz1m, gz1e, gP, gQ);
+  PDG_CHECK_LAUNCH("pdg_pq_scatter_bwd");
+  return PDG_OK;
+}

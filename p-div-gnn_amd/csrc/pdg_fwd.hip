@@ -1,0 +1,676 @@
+// Forward kernels of the P-DivGNN hot path (EncodeProcessDecode.forward,
+// gnn_local_stress/models.py:288-326) for gfx950.
+//
+// Layout and wave-tile conventions: pdg_common.hpp.  Every kernel that ends in a
+// graph-LayerNorm writes per-block (sum, sum of squares) partials in fp64; the
+// statistics are reduced by pdg_ln_finalize and applied by the *consumer* of the
+// normalised tensor (LN is graph-global, so it cannot be applied in the producer).
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "pdg_common.hpp"
+#include "pdg_runtime.hpp"
+
+using namespace pdg;
+
+namespace pdg {
+
+static thread_local char g_err[512];
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (!cached[dev]) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    cached[dev] = cus;
+  }
+  return cached[dev];
+}
+
+}  // namespace pdg
+
+// ============================================================================ input formatting
+__global__ void format_inputs_kernel(int N, int E, const float* __restrict__ pos,
+                                     const float* __restrict__ ms, const int64_t* __restrict__ types,
+                                     const float* __restrict__ ea, const int* __restrict__ perm,
+                                     const float* __restrict__ st8, int scale, float* __restrict__ x_in,
+                                     float* __restrict__ e_in) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  float mp = 0.f, sp = 1.f, mm = 0.f, sm = 1.f, me = 0.f, se = 1.f;
+  if (scale) { mp = st8[0]; sp = st8[1]; mm = st8[2]; sm = st8[3]; me = st8[6]; se = st8[7]; }
+  if (i < N) {
+    float* o = x_in + i * 6;
+    // models.py:147-151: hstack[(mean_stress - mu)/s, (pos - mu)/s, node_type]
+    for (int c = 0; c < 3; ++c) { float v = ms[i * 3 + c]; o[c] = scale ? (v - mm) / sm : v; }
+    for (int c = 0; c < 2; ++c) { float v = pos[i * 2 + c]; o[3 + c] = scale ? (v - mp) / sp : v; }
+    o[5] = (float)types[i];
+  }
+  if (i < E) {
+    const float v = ea[perm[i]];
+    e_in[i] = scale ? (v - me) / se : v;
+  }
+}
+
+extern "C" int pdg_format_inputs(int n_nodes, int n_edges, const float* pos, const float* mean_stress,
+                                 const int64_t* node_types, const float* edge_attr, const int* perm,
+                                 const float* stats8, int scale_input, float* x_in, float* e_in,
+                                 void* stream) {
+  PDG_CHECK_ARG(n_nodes >= 0 && n_edges >= 0, "pdg_format_inputs: negative size");
+  const long n = n_nodes > n_edges ? n_nodes : n_edges;
+  if (n == 0) return PDG_OK;
+  PDG_CHECK_ARG(stats8 != nullptr || !scale_input, "pdg_format_inputs: stats8 is NULL");
+  const int threads = 256;
+  const long blocks = (n + threads - 1) / threads;
+  hipLaunchKernelGGL(format_inputs_kernel, dim3((unsigned)blocks), dim3(threads), 0, (hipStream_t)stream,
+                     n_nodes, n_edges, pos, mean_stress, node_types, edge_attr, perm, stats8, scale_input,
+                     x_in, e_in);
+  PDG_CHECK_LAUNCH("pdg_format_inputs");
+  return PDG_OK;
+}
+
+// ============================================================================ stats helpers
+__device__ __forceinline__ void accum_stats(const float (&v)[64], bool valid, double& s1, double& s2) {
+  if (!valid) return;
+  // 64 values of one row half: fp32 partial per 16, fp64 across
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { const float x = v[16 * q + j]; a += x; b += x * x; }
+    s1 += (double)a;
+    s2 += (double)b;
+  }
+}
+
+__device__ __forceinline__ void write_partials(double s1, double s2, double* part) {
+  __shared__ double red[2 * 16];
+  block_sum2(s1, s2, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s1;
+    part[2 * blockIdx.x + 1] = s2;
+  }
+}
+
+// v = LN(a2 row) [+ residual row], four fenced chunks of 16 floats.
+template <bool RES>
+__device__ __forceinline__ void ln_res_frag(float (&v)[64], const float* __restrict__ a2row,
+                                            const float* __restrict__ resrow, const LNStat& st,
+                                            const float* __restrict__ g, const float* __restrict__ b) {
+  const int ho = half_off();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 x[4], r[4], gg[4], bb[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      x[t] = reinterpret_cast<const f32x4*>(a2row + ho + 16 * q)[t];
+      if (RES) r[t] = reinterpret_cast<const f32x4*>(resrow + ho + 16 * q)[t];
+      gg[t] = reinterpret_cast<const f32x4*>(g + ho + 16 * q)[t];
+      bb[t] = reinterpret_cast<const f32x4*>(b + ho + 16 * q)[t];
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float y = div_den(x[t][j] - st.mean, st.den, st.rstd) * gg[t][j] + bb[t][j];
+        if (RES) y += r[t][j];
+        v[16 * q + 4 * t + j] = y;
+      }
+    PDG_FENCE();
+  }
+}
+
+// v[s] = relu(acc[s] + bias[64h + s]), two fenced chunks.
+__device__ __forceinline__ void bias_relu(float (&v)[64], const f32x16 (&acc)[4], const float* __restrict__ bias) {
+  const f32x4* bp = reinterpret_cast<const f32x4*>(bias + half_off());
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const f32x4 bb = bp[t];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * t + j] = fmaxf(ACC(acc, 4 * t + j) + bb[j], 0.f);
+    if (t == 7) PDG_FENCE();
+  }
+}
+
+// ============================================================================ encoder
+// models.py:260-274.  W2 in LDS (A-image); W0 (128 x IN) and b0 appended.
+template <int IN>
+__global__ __launch_bounds__(256, 2) void encoder_kernel(int M, const float* __restrict__ x_in,
+                                                          const float* __restrict__ W0,
+                                                          const float* __restrict__ b0,
+                                                          const float* __restrict__ W2,
+                                                          const float* __restrict__ b2,
+                                                          float* __restrict__ a1, float* __restrict__ a2,
+                                                          double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* w0l = lds + WBLK;           // [128][IN]
+  float* b0l = w0l + 128 * IN;       // [128]
+  load_wblock(lds, W2, 128, 0);
+  for (int i = threadIdx.x; i < 128 * IN; i += blockDim.x) w0l[i] = W0[i];
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) b0l[i] = b0[i];
+  __syncthreads();
+  const int l = lane_id(), h = l >> 5;
+  const int nw = blockDim.x >> 6;
+  double s1 = 0, s2 = 0;
+  const int ntiles = tiles_of(M);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < M;
+    const int rc = valid ? row : M - 1;
+    float xi[IN];
+#pragma unroll
+    for (int i = 0; i < IN; ++i) xi[i] = x_in[(size_t)rc * IN + i];
+    float v[64];
+    const int ho = half_off();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int s = 16 * q; s < 16 * q + 16; ++s) {
+        const int o = ho + s;
+        float d = 0.f;
+#pragma unroll
+        for (int i = 0; i < IN; ++i) d = fmaf(w0l[o * IN + i], xi[i], d);
+        v[s] = fmaxf(d + b0l[o], 0.f);
+      }
+      PDG_FENCE();
+    }
+    if (valid) store_frag(a1 + (size_t)row * L, v);
+    f32x16 acc[4];
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    bias_relu(v, acc, b2);
+    if (valid) store_frag(a2 + (size_t)row * L, v);
+    accum_stats(v, valid, s1, s2);
+  }
+  write_partials(s1, s2, part);
+}
+
+extern "C" int pdg_encoder_fwd(int rows, int in_features, const float* x_in, const float* W0,
+                               const float* b0, const float* W2, const float* b2, float* a1, float* a2,
+                               double* partials, int* nparts, void* stream) {
+  PDG_CHECK_ARG(rows > 0, "pdg_encoder_fwd: rows must be > 0");
+  PDG_CHECK_ARG(in_features == 1 || in_features == 6, "pdg_encoder_fwd: in_features must be 1 or 6");
+  PDG_CHECK_ARG(PDG_ALIGNED(a1) && PDG_ALIGNED(a2) && PDG_ALIGNED(W2) && PDG_ALIGNED(b2),
+                "pdg_encoder_fwd: misaligned pointer");
+  const int grid = persistent_grid(rows, 4, 2);
+  const size_t shm = (size_t)(WBLK + 128 * in_features + 128) * sizeof(float);
+  if (in_features == 6)
+    hipLaunchKernelGGL(encoder_kernel<6>, dim3(grid), dim3(256), shm, (hipStream_t)stream, rows, x_in, W0,
+                       b0, W2, b2, a1, a2, partials);
+  else
+    hipLaunchKernelGGL(encoder_kernel<1>, dim3(grid), dim3(256), shm, (hipStream_t)stream, rows, x_in, W0,
+                       b0, W2, b2, a1, a2, partials);
+  PDG_CHECK_LAUNCH("pdg_encoder_fwd");
+  if (nparts) *nparts = grid;
+  return PDG_OK;
+}
+
+// ============================================================================ LN finalize
+__global__ void ln_finalize_kernel(const double* __restrict__ part, int n, double count,
+                                   pdg_ln_stat* __restrict__ out) {
+  __shared__ double red[2 * 16];
+  double a = 0, b = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) { a += part[2 * i]; b += part[2 * i + 1]; }
+  block_sum2(a, b, red);
+  if (threadIdx.x == 0) {
+    const double mean = a / count;
+    double var = b / count - mean * mean;
+    if (var < 0) var = 0;
+    const double sd = sqrt(var);
+    pdg_ln_stat s;
+    s.mean = (float)mean;
+    s.std_ = (float)sd;
+    s.den = s.std_ + LN_EPS;
+    s.rstd = 1.0f / s.den;
+    s.mean_d = mean;
+    s.std_d = sd;
+    s.count = count;
+    *out = s;
+  }
+}
+
+extern "C" int pdg_ln_finalize(const double* partials, int nparts, double count, pdg_ln_stat* out,
+                               void* stream) {
+  PDG_CHECK_ARG(nparts > 0 && count > 0, "pdg_ln_finalize: empty");
+  hipLaunchKernelGGL(ln_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partials, nparts, count,
+                     out);
+  PDG_CHECK_LAUNCH("pdg_ln_finalize");
+  return PDG_OK;
+}
+
+// ============================================================================ node P/Q pre-pass
+template <bool RES>
+__global__ __launch_bounds__(512, 2) void node_pq_kernel(int N, const float* __restrict__ a2p,
+                                                          const pdg_ln_stat* __restrict__ stp,
+                                                          const float* __restrict__ lg,
+                                                          const float* __restrict__ lb,
+                                                          const float* __restrict__ xres,
+                                                          float* __restrict__ xout,
+                                                          const float* __restrict__ W1,
+                                                          float* __restrict__ P, float* __restrict__ Q) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  load_wblock(lds, W1, 3 * L, 0);           // W_a: input block x_i (target)
+  load_wblock(lds + WBLK, W1, 3 * L, L);    // W_b: input block x_j (source)
+  __syncthreads();
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(N);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < N;
+    const int rc = valid ? row : N - 1;
+    float v[64];
+    ln_res_frag<RES>(v, a2p + (size_t)rc * L, RES ? xres + (size_t)rc * L : nullptr, st, lg, lb);
+    if (valid) store_frag(xout + (size_t)row * L, v);
+    f32x16 acc[4];
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    if (valid) store_acc(P + (size_t)row * L, acc);
+    zero_acc(acc);
+    gemm128(acc, lds + WBLK, v);
+    if (valid) store_acc(Q + (size_t)row * L, acc);
+  }
+}
+
+extern "C" int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                           const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
+                           float* Q, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_node_pq: n_nodes must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(x_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
+                    PDG_ALIGNED(W1) && (!x_res || PDG_ALIGNED(x_res)),
+                "pdg_node_pq: misaligned pointer");
+  const int grid = persistent_grid(n_nodes, 8, 1);
+  if (x_res)
+    hipLaunchKernelGGL(node_pq_kernel<true>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+                       n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q);
+  else
+    hipLaunchKernelGGL(node_pq_kernel<false>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+                       n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q);
+  PDG_CHECK_LAUNCH("pdg_node_pq");
+  return PDG_OK;
+}
+
+// ============================================================================ fused edge pass
+// First layer of both edge_net evaluations from the shared C = W_c e + b1, in
+// four fenced 16-float chunks aligned with the accumulator tuples C[q] (each
+// tuple dies as its chunk is consumed):
+//   edge update: relu(C + P[src] + Q[dst]) -> stored to a1e
+//   message:     relu(C + P[dst] + Q[src]) -> v (and stored to a1m by the caller)
+__device__ __forceinline__ void first_layers(float (&v)[64], const f32x16 (&C)[4], const float* __restrict__ ps,
+                                             const float* __restrict__ qd, const float* __restrict__ pd,
+                                             const float* __restrict__ qs, float* __restrict__ a1e_row,
+                                             bool valid) {
+  const int ho = half_off();
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    f32x4 xs[2], yd[2], xd[2], ys[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      xs[t] = reinterpret_cast<const f32x4*>(ps + ho + 8 * q)[t];
+      yd[t] = reinterpret_cast<const f32x4*>(qd + ho + 8 * q)[t];
+      xd[t] = reinterpret_cast<const f32x4*>(pd + ho + 8 * q)[t];
+      ys[t] = reinterpret_cast<const f32x4*>(qs + ho + 8 * q)[t];
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      f32x4 e;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int s = 8 * q + 4 * t + j;
+        const float c = ACC(C, s);
+        e[j] = fmaxf((c + xs[t][j]) + yd[t][j], 0.f);
+        v[s] = fmaxf((c + xd[t][j]) + ys[t][j], 0.f);
+      }
+      if (valid) reinterpret_cast<f32x4*>(a1e_row + ho + 8 * q)[t] = e;
+    }
+    PDG_FENCE();
+  }
+}
+
+template <bool RES>
+__global__ __launch_bounds__(512, 2) void edge_fwd_kernel(
+    int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
+    const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
+    const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ P,
+    const float* __restrict__ Q, const float* __restrict__ W1, const float* __restrict__ b1,
+    const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ a1m,
+    float* __restrict__ a2m, float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m,
+    double* __restrict__ part_e) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  load_wblock(lds, W1, 3 * L, 2 * L);   // W_c: edge-feature block
+  load_wblock(lds + WBLK, W2, L, 0);
+  __syncthreads();
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(E);
+  double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < E;
+    const int rc = valid ? row : E - 1;
+    const int s_node = src[rc], d_node = dst[rc];
+    float v[64];
+    // e_t = LN(a2_prev) + e_res   (models.py:225 residual of the previous step)
+    ln_res_frag<RES>(v, a2p + (size_t)rc * L, RES ? eres + (size_t)rc * L : nullptr, st, lg, lb);
+    if (valid) store_frag(eout + (size_t)row * L, v);
+    // C = W_c e_t + b1 (shared by both edge_net evaluations)
+    f32x16 C[4];
+    zero_acc(C);
+    gemm128(C, lds, v);
+    {
+      const f32x4* bp = reinterpret_cast<const f32x4*>(b1 + half_off());
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const f32x4 bb = bp[t];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ACC(C, 4 * t + j) += bb[j];
+      }
+    }
+    // layer 1 of the edge update (models.py:219-222, x[row] = x[src], x[col] = x[dst]; stored,
+    // re-read below) and of the message (models.py:233-238, x_i = x[dst], x_j = x[src])
+    first_layers(v, C, P + (size_t)s_node * L, Q + (size_t)d_node * L, P + (size_t)d_node * L,
+                 Q + (size_t)s_node * L, a1e + (size_t)row * L, valid);
+    if (valid) store_frag(a1m + (size_t)row * L, v);
+    f32x16 Z[4];
+    zero_acc(Z);
+    gemm128(Z, lds + WBLK, v);
+    bias_relu(v, Z, b2);
+    if (valid) store_frag(a2m + (size_t)row * L, v);
+    accum_stats(v, valid, sm1, sm2);
+    // edge-update layer 2
+    load_frag(v, a1e + (size_t)(valid ? row : rc) * L);
+    zero_acc(Z);
+    gemm128(Z, lds + WBLK, v);
+    bias_relu(v, Z, b2);
+    if (valid) store_frag(a2e + (size_t)row * L, v);
+    accum_stats(v, valid, se1, se2);
+  }
+  write_partials(sm1, sm2, part_m);
+  write_partials(se1, se2, part_e);
+}
+
+extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                            const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
+                            const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
+                            const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
+                            double* part_e, int* nparts, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd: n_edges must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
+                    PDG_ALIGNED(a1m) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e) &&
+                    (!e_res || PDG_ALIGNED(e_res)),
+                "pdg_edge_fwd: misaligned pointer");
+  const int grid = persistent_grid(n_edges, 8, 1);
+  if (e_res)
+    hipLaunchKernelGGL(edge_fwd_kernel<true>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+                       n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m,
+                       a1e, a2e, part_m, part_e);
+  else
+    hipLaunchKernelGGL(edge_fwd_kernel<false>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+                       n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m,
+                       a1e, a2e, part_m, part_e);
+  PDG_CHECK_LAUNCH("pdg_edge_fwd");
+  if (nparts) *nparts = grid;
+  return PDG_OK;
+}
+
+// ============================================================================ segment sum
+// Half-wave (32 lanes x 16 B) per destination node; rows of a segment are
+// contiguous in the dst-sorted edge order, summed sequentially from zero in
+// segment order (= PyG scatter_add_ order for a coalesced edge_index).
+__global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __restrict__ rowptr,
+                                                          const float* __restrict__ rows,
+                                                          const pdg_ln_stat* __restrict__ stp,
+                                                          const float* __restrict__ lg,
+                                                          const float* __restrict__ lb,
+                                                          float* __restrict__ out) {
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const int nhw = blockDim.x >> 5;
+  float mean = 0.f, den = 1.f, rstd = 1.f;
+  f32x4 g = {1.f, 1.f, 1.f, 1.f}, b = {0.f, 0.f, 0.f, 0.f};
+  const bool ln = stp != nullptr;
+  if (ln) {
+    mean = stp->mean;
+    den = stp->den;
+    rstd = stp->rstd;
+    g = reinterpret_cast<const f32x4*>(lg)[j];
+    b = reinterpret_cast<const f32x4*>(lb)[j];
+  }
+  for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
+    const int k0 = rowptr[v], k1 = rowptr[v + 1];
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    int k = k0;
+    for (; k + 1 < k1; k += 2) {
+      f32x4 x0 = reinterpret_cast<const f32x4*>(rows + (size_t)k * L)[j];
+      f32x4 x1 = reinterpret_cast<const f32x4*>(rows + (size_t)(k + 1) * L)[j];
+      if (ln) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          x0[c] = div_den(x0[c] - mean, den, rstd) * g[c] + b[c];
+          x1[c] = div_den(x1[c] - mean, den, rstd) * g[c] + b[c];
+        }
+      }
+      acc += x0;
+      acc += x1;
+    }
+    if (k < k1) {
+      f32x4 x0 = reinterpret_cast<const f32x4*>(rows + (size_t)k * L)[j];
+      if (ln) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x0[c] = div_den(x0[c] - mean, den, rstd) * g[c] + b[c];
+      }
+      acc += x0;
+    }
+    reinterpret_cast<f32x4*>(out + (size_t)v * L)[j] = acc;
+  }
+}
+
+extern "C" int pdg_segment_sum(int n_nodes, const int* rowptr, const float* rows, const pdg_ln_stat* st,
+                               const float* ln_g, const float* ln_b, float* out, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_segment_sum: n_nodes must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(rows) && PDG_ALIGNED(out), "pdg_segment_sum: misaligned pointer");
+  long want = (n_nodes + 7) / 8;
+  long cap = (long)device_cus() * 8;
+  const int grid = (int)(want < cap ? want : cap);
+  hipLaunchKernelGGL(segment_sum_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, rowptr, rows,
+                     st, ln_g, ln_b, out);
+  PDG_CHECK_LAUNCH("pdg_segment_sum");
+  return PDG_OK;
+}
+
+// ============================================================================ node MLP layer 1
+__global__ __launch_bounds__(512, 2) void node_mlp1_kernel(int N, const float* __restrict__ aggr,
+                                                            const float* __restrict__ x,
+                                                            const float* __restrict__ Wn1,
+                                                            const float* __restrict__ bn1,
+                                                            float* __restrict__ a1n) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  load_wblock(lds, Wn1, 2 * L, 0);          // aggr block (models.py:241 cat order)
+  load_wblock(lds + WBLK, Wn1, 2 * L, L);   // x block
+  __syncthreads();
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(N);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < N;
+    const int rc = valid ? row : N - 1;
+    float v[64];
+    f32x16 acc[4];
+    zero_acc(acc);
+    load_frag(v, aggr + (size_t)rc * L);
+    gemm128(acc, lds, v);
+    load_frag(v, x + (size_t)rc * L);
+    gemm128(acc, lds + WBLK, v);
+    bias_relu(v, acc, bn1);
+    if (valid) store_frag(a1n + (size_t)row * L, v);
+  }
+}
+
+extern "C" int pdg_node_mlp1(int n_nodes, const float* aggr, const float* x, const float* Wn1,
+                             const float* bn1, float* a1n, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_node_mlp1: n_nodes must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(aggr) && PDG_ALIGNED(x) && PDG_ALIGNED(a1n) && PDG_ALIGNED(Wn1),
+                "pdg_node_mlp1: misaligned pointer");
+  const int grid = persistent_grid(n_nodes, 8, 1);
+  hipLaunchKernelGGL(node_mlp1_kernel, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+                     n_nodes, aggr, x, Wn1, bn1, a1n);
+  PDG_CHECK_LAUNCH("pdg_node_mlp1");
+  return PDG_OK;
+}
+
+// ============================================================================ MLP layer 2 (+ LN partials)
+__global__ __launch_bounds__(256, 2) void mlp2_fwd_kernel(int M, const float* __restrict__ a1,
+                                                           const float* __restrict__ W2,
+                                                           const float* __restrict__ b2,
+                                                           float* __restrict__ a2, double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  load_wblock(lds, W2, L, 0);
+  __syncthreads();
+  const int l = lane_id();
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(M);
+  double s1 = 0, s2 = 0;
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < M;
+    const int rc = valid ? row : M - 1;
+    float v[64];
+    load_frag(v, a1 + (size_t)rc * L);
+    f32x16 acc[4];
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    bias_relu(v, acc, b2);
+    if (valid) store_frag(a2 + (size_t)row * L, v);
+    accum_stats(v, valid, s1, s2);
+  }
+  write_partials(s1, s2, part);
+}
+
+extern "C" int pdg_mlp2_fwd(int rows, const float* a1, const float* W2, const float* b2, float* a2,
+                            double* partials, int* nparts, void* stream) {
+  PDG_CHECK_ARG(rows > 0, "pdg_mlp2_fwd: rows must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(a1) && PDG_ALIGNED(a2) && PDG_ALIGNED(W2), "pdg_mlp2_fwd: misaligned pointer");
+  const int grid = persistent_grid(rows, 4, 2);
+  hipLaunchKernelGGL(mlp2_fwd_kernel, dim3(grid), dim3(256), WBLK * sizeof(float), (hipStream_t)stream, rows,
+                     a1, W2, b2, a2, partials);
+  PDG_CHECK_LAUNCH("pdg_mlp2_fwd");
+  if (nparts) *nparts = grid;
+  return PDG_OK;
+}
+
+// ============================================================================ decoder
+__global__ __launch_bounds__(256, 2) void decoder_kernel(int N, const float* __restrict__ a2p,
+                                                          const pdg_ln_stat* __restrict__ stp,
+                                                          const float* __restrict__ lg,
+                                                          const float* __restrict__ lb,
+                                                          const float* __restrict__ xres,
+                                                          float* __restrict__ xout,
+                                                          const float* __restrict__ Wd1,
+                                                          const float* __restrict__ bd1,
+                                                          float* __restrict__ a1d,
+                                                          const float* __restrict__ Wd2,
+                                                          const float* __restrict__ bd2,
+                                                          const float* __restrict__ st8, int scale,
+                                                          float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* w2l = lds + WBLK;   // Wd2 (3 x 128)
+  load_wblock(lds, Wd1, L, 0);
+  for (int i = threadIdx.x; i < 3 * L; i += blockDim.x) w2l[i] = Wd2[i];
+  __syncthreads();
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const int l = lane_id(), h = l >> 5;
+  const int nw = blockDim.x >> 6;
+  const int ntiles = tiles_of(N);
+  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
+    const int row = tile * 32 + (l & 31);
+    const bool valid = row < N;
+    const int rc = valid ? row : N - 1;
+    float v[64];
+    ln_res_frag<true>(v, a2p + (size_t)rc * L, xres + (size_t)rc * L, st, lg, lb);
+    if (valid) store_frag(xout + (size_t)row * L, v);
+    f32x16 acc[4];
+    zero_acc(acc);
+    gemm128(acc, lds, v);
+    bias_relu(v, acc, bd1);
+    if (valid) store_frag(a1d + (size_t)row * L, v);
+    // Linear(128 -> 3): half-row partial dots, combined across the two lane halves
+    float o3[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      const float* wp = w2l + o * L + half_off();
+      float d = 0.f;
+#pragma unroll
+      for (int s = 0; s < 64; ++s) d = fmaf(wp[s], v[s], d);
+      o3[o] = d;
+      PDG_FENCE();
+    }
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      const float other = __shfl_xor(o3[o], 32);
+      o3[o] = (h == 0 ? o3[o] + other : other + o3[o]) + bd2[o];
+      if (scale) o3[o] = o3[o] * st8[5] + st8[4];
+    }
+    if (valid && h == 0) {
+      y[(size_t)row * 3 + 0] = o3[0];
+      y[(size_t)row * 3 + 1] = o3[1];
+      y[(size_t)row * 3 + 2] = o3[2];
+    }
+  }
+}
+
+extern "C" int pdg_decoder_fwd(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                               const float* ln_b, const float* x_res, float* x_out, const float* Wd1,
+                               const float* bd1, float* a1d, const float* Wd2, const float* bd2,
+                               const float* stats8, int scale_output, float* y, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_decoder_fwd: n_nodes must be > 0");
+  PDG_CHECK_ARG(x_res != nullptr, "pdg_decoder_fwd: x_res is NULL");
+  PDG_CHECK_ARG(!scale_output || stats8 != nullptr, "pdg_decoder_fwd: stats8 is NULL");
+  PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(x_res) && PDG_ALIGNED(x_out) && PDG_ALIGNED(a1d) &&
+                    PDG_ALIGNED(Wd1) && PDG_ALIGNED(Wd2),
+                "pdg_decoder_fwd: misaligned pointer");
+  const int grid = persistent_grid(n_nodes, 4, 2);
+  hipLaunchKernelGGL(decoder_kernel, dim3(grid), dim3(256), (WBLK + 3 * L) * sizeof(float), (hipStream_t)stream, n_nodes,
+                     a2_prev, st, ln_g, ln_b, x_res, x_out, Wd1, bd1, a1d, Wd2, bd2, stats8, scale_output, y);
+  PDG_CHECK_LAUNCH("pdg_decoder_fwd");
+  return PDG_OK;
+}
+
+// ============================================================================ any-nonzero guard
+__global__ void any_nonzero_kernel(const float* __restrict__ x, long n, int* __restrict__ flag) {
+  int found = 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    found |= (x[i] != 0.f);
+  if (__any(found) && lane_id() == 0) atomicOr(flag, 1);
+}
+
+extern "C" int pdg_any_nonzero(const float* x, int64_t n, int* flag, void* stream) {
+  PDG_CHECK_ARG(n >= 0 && flag != nullptr, "pdg_any_nonzero: bad args");
+  if (hipMemsetAsync(flag, 0, sizeof(int), (hipStream_t)stream) != hipSuccess) {
+    set_error("pdg_any_nonzero: memset failed");
+    return PDG_ERR_HIP;
+  }
+  if (n == 0) return PDG_OK;
+  long blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(any_nonzero_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, (long)n,
+                     flag);
+  PDG_CHECK_LAUNCH("pdg_any_nonzero");
+  return PDG_OK;
+}
+
+// ============================================================================ library info
+extern "C" const char* pdg_last_error(void) { return pdg::g_err; }
+extern "C" int pdg_version(void) { return 1; }
+extern "C" int pdg_max_blocks(void) { return MAX_BLOCKS; }

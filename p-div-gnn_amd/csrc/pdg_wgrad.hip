@@ -1,0 +1,209 @@
+// Weight gradients of the shared 128x128 Linears (autograd of addmm in
+// gnn_local_stress/models.py:194-208, :260-286), deterministic split-K.
+//
+// dW[o][i] = sum_k G[k][o] X[k][i] is a K = rows reduction (rows = edges, up
+// to ~10^6).  Each block owns a contiguous row range and accumulates into its
+// own fp32 slab (128x128 + 128 bias sums) with += (no atomics), so the shared
+// weights of the 10 weight-tied message-passing steps accumulate across calls
+// in a fixed order; pdg_wgrad_reduce sums the slabs in block order.
+//
+// MFMA mapping (v_mfma_f32_32x32x2_f32): A = G^T (o on the lane, k = lane half),
+// B = X (i on the lane, k = lane half): both operands are plain 128-byte
+// row segments, read straight from global memory.  4 waves per block, wave w
+// owns outputs o in [32w, 32w+32) and all 128 inputs (4 accumulators).
+#include "pdg_common.hpp"
+#include "pdg_runtime.hpp"
+
+using namespace pdg;
+
+constexpr int SLAB = L * L + L;   // floats per slab
+
+__device__ __forceinline__ void wgrad_pass(int M, int r0, int r1, const float* __restrict__ G,
+                                           const float* __restrict__ X, f32x16 (&acc)[4], double& bsum) {
+  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
+  const float* gcol = G + 32 * w + c;
+  const float* xcol = X + c;
+  int k = r0;
+  for (; k + 8 <= r1; k += 8) {
+    float ga[4], xb[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t kk = (size_t)(k + 2 * u + h) * L;
+      ga[u] = gcol[kk];
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib) xb[u][ib] = xcol[kk + 32 * ib];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      bsum += (double)ga[u];
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)
+        acc[ib] = __builtin_amdgcn_mfma_f32_32x32x2f32(ga[u], xb[u][ib], acc[ib], 0, 0, 0);
+    }
+  }
+  for (; k < r1; k += 2) {
+    const int kr = k + h;
+    const bool ok = kr < r1;
+    const size_t kk = (size_t)(ok ? kr : r0) * L;
+    const float ga = ok ? gcol[kk] : 0.f;
+    bsum += (double)ga;
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib) {
+      const float xb = ok ? xcol[kk + 32 * ib] : 0.f;
+      acc[ib] = __builtin_amdgcn_mfma_f32_32x32x2f32(ga, xb, acc[ib], 0, 0, 0);
+    }
+  }
+  (void)M;
+}
+
+__global__ __launch_bounds__(256) void wgrad_accum_kernel(int M, const float* __restrict__ G,
+                                                          const float* __restrict__ X,
+                                                          const float* __restrict__ G2,
+                                                          const float* __restrict__ X2,
+                                                          float* __restrict__ slabs) {
+  const int nb = gridDim.x;
+  const long chunk = (((long)M + nb - 1) / nb + 1) & ~1L;
+  const int r0 = (int)min((long)M, chunk * blockIdx.x);
+  const int r1 = (int)min((long)M, chunk * (blockIdx.x + 1));
+  f32x16 acc[4];
+  zero_acc(acc);
+  double bsum = 0;
+  wgrad_pass(M, r0, r1, G, X, acc, bsum);
+  if (G2) wgrad_pass(M, r0, r1, G2, X2, acc, bsum);
+  const int l = lane_id(), h = l >> 5, w = wave_id();
+  float* slab = slabs + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = 32 * w + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int i = 32 * ib + (l & 31);
+      slab[o * L + i] += acc[ib][r];
+    }
+  const double other = __shfl_xor(bsum, 32);
+  if (h == 0) slab[L * L + 32 * w + (l & 31)] += (float)(bsum + other);
+}
+
+extern "C" int pdg_wgrad_accum(int rows, const float* G, const float* X, const float* G2, const float* X2,
+                               float* slabs, int nslabs, void* stream) {
+  PDG_CHECK_ARG(rows > 0 && nslabs > 0 && nslabs <= MAX_BLOCKS, "pdg_wgrad_accum: bad sizes");
+  PDG_CHECK_ARG((G2 == nullptr) == (X2 == nullptr), "pdg_wgrad_accum: G2/X2 must both be set or NULL");
+  hipLaunchKernelGGL(wgrad_accum_kernel, dim3(nslabs), dim3(256), 0, (hipStream_t)stream, rows, G, X, G2, X2,
+                     slabs);
+  PDG_CHECK_LAUNCH("pdg_wgrad_accum");
+  return PDG_OK;
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int n, float* __restrict__ gW, int ld,
+                                    int col0, float* __restrict__ gb) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= SLAB) return;
+  float s = 0.f;
+  for (int b = 0; b < n; ++b) s += slabs[(size_t)b * SLAB + e];
+  if (e < L * L) {
+    const int o = e / L, i = e % L;
+    gW[(size_t)o * ld + col0 + i] += s;
+  } else if (gb) {
+    gb[e - L * L] += s;
+  }
+}
+
+extern "C" int pdg_wgrad_reduce(const float* slabs, int nslabs, float* grad_W, int ld, int col0, float* grad_b,
+                                void* stream) {
+  PDG_CHECK_ARG(nslabs > 0 && grad_W != nullptr, "pdg_wgrad_reduce: bad args");
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((SLAB + 255) / 256), dim3(256), 0, (hipStream_t)stream, slabs,
+                     nslabs, grad_W, ld, col0, grad_b);
+  PDG_CHECK_LAUNCH("pdg_wgrad_reduce");
+  return PDG_OK;
+}
+
+// ============================================================================ narrow weight gradient
+// T[c][i] = sum_k Wide[k][c] * Narrow[k][i], c < 128, i < K <= 8.  Half-wave per row.
+template <int K>
+__global__ __launch_bounds__(256) void wgrad_narrow_kernel(int M, const float* __restrict__ wide,
+                                                           const float* __restrict__ narrow,
+                                                           double* __restrict__ part) {
+  constexpr int NP = 4 * K + 4 + K;   // per-lane partials: 4 channels x K, 4 wide sums, K narrow sums
+  __shared__ double red[8][32][NP];
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const int nhw = blockDim.x >> 5;
+  double acc[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) acc[p] = 0;
+  for (int k = blockIdx.x * nhw + hw; k < M; k += gridDim.x * nhw) {
+    const f32x4 w = reinterpret_cast<const f32x4*>(wide + (size_t)k * L)[j];
+    float nv[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) nv[i] = narrow[(size_t)k * K + i];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int i = 0; i < K; ++i) acc[c * K + i] += (double)(w[c] * nv[i]);
+      acc[4 * K + c] += (double)w[c];
+    }
+#pragma unroll
+    for (int i = 0; i < K; ++i) acc[4 * K + 4 + i] += (double)nv[i];
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) red[hw][j][p] = acc[p];
+  __syncthreads();
+  // block partial layout: [T (128*K) | wide sums (128) | narrow sums (K)]
+  double* out = part + (size_t)blockIdx.x * (L * K + L + K);
+  for (int e = threadIdx.x; e < L * K + L + K; e += blockDim.x) {
+    double s = 0;
+    if (e < L * K) {
+      const int c = e / K, i = e % K;
+      for (int w = 0; w < nhw; ++w) s += red[w][c >> 2][(c & 3) * K + i];
+    } else if (e < L * K + L) {
+      const int c = e - L * K;
+      for (int w = 0; w < nhw; ++w) s += red[w][c >> 2][4 * K + (c & 3)];
+    } else {
+      const int i = e - L * K - L;
+      for (int w = 0; w < nhw; ++w) s += red[w][0][4 * K + 4 + i];   // same in every lane
+    }
+    out[e] = s;
+  }
+}
+
+__global__ void wgrad_narrow_finalize_kernel(const double* __restrict__ part, int n, int K, int transpose,
+                                             float* __restrict__ gW, float* __restrict__ gbw,
+                                             float* __restrict__ gbn) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int tot = L * K + L + K;
+  if (e >= tot) return;
+  double s = 0;
+  for (int b = 0; b < n; ++b) s += part[(size_t)b * tot + e];
+  if (e < L * K) {
+    const int c = e / K, i = e % K;
+    if (transpose) gW[i * L + c] += (float)s;
+    else gW[c * K + i] += (float)s;
+  } else if (e < L * K + L) {
+    if (gbw) gbw[e - L * K] += (float)s;
+  } else {
+    if (gbn) gbn[e - L * K - L] += (float)s;
+  }
+}
+
+extern "C" int pdg_wgrad_narrow(int rows, const float* wide, const float* narrow, int k_narrow, int transpose,
+                                double* partials, float* grad_W, float* grad_b_wide, float* grad_b_narrow,
+                                void* stream) {
+  PDG_CHECK_ARG(rows > 0, "pdg_wgrad_narrow: rows must be > 0");
+  PDG_CHECK_ARG(k_narrow == 1 || k_narrow == 3 || k_narrow == 6, "pdg_wgrad_narrow: k_narrow must be 1, 3 or 6");
+  PDG_CHECK_ARG(PDG_ALIGNED(wide), "pdg_wgrad_narrow: misaligned pointer");
+  long want = (rows + 7) / 8;
+  long cap = (long)device_cus();
+  const int grid = (int)(want < cap ? want : cap);
+  hipStream_t s = (hipStream_t)stream;
+  if (k_narrow == 1)
+    hipLaunchKernelGGL(wgrad_narrow_kernel<1>, dim3(grid), dim3(256), 0, s, rows, wide, narrow, partials);
+  else if (k_narrow == 3)
+    hipLaunchKernelGGL(wgrad_narrow_kernel<3>, dim3(grid), dim3(256), 0, s, rows, wide, narrow, partials);
+  else
+    hipLaunchKernelGGL(wgrad_narrow_kernel<6>, dim3(grid), dim3(256), 0, s, rows, wide, narrow, partials);
+  PDG_CHECK_LAUNCH("pdg_wgrad_narrow");
+  const int tot = L * k_narrow + L + k_narrow;
+  hipLaunchKernelGGL(wgrad_narrow_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, partials, grid,
+                     k_narrow, transpose, grad_W, grad_b_wide, grad_b_narrow);
+  PDG_CHECK_LAUNCH("pdg_wgrad_narrow(finalize)");
+  return PDG_OK;
+}

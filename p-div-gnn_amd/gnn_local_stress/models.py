@@ -1,0 +1,234 @@
+"""Drop-in ``gnn_local_stress.models`` backed by the MI355X HIP kernels.
+
+Mirrors the reference module's public surface (gnn_local_stress/models.py):
+
+* ``StressFieldBaseModel`` (:98-179): same constructor keywords, the 8 scalar
+  standardisation statistics as plain attributes moved by ``.to()`` (:164-179),
+  ``format_node_features`` / ``format_edge_features`` (:140-162);
+* ``Processor`` (:182-243): ``edge_net`` / ``node_net`` Sequentials with the
+  same parameter names, so ``state_dict`` keys match and reference ``.pth``
+  checkpoints load unchanged;
+* ``EncodeProcessDecode`` (:246-326): same constructor and
+  ``forward(mesh_graph, scale_output=True, scale_input=True) -> Data`` with
+  ``local_stress``, ``edge_index``, ``pos``;
+* checkpoint helpers (:44-95) with the same dict keys.
+
+``forward`` on a HIP device runs the whole stack through libpdivgnn_hip.so
+(pdg.engine); autograd is wired with one ``torch.autograd.Function`` whose
+backward is the HIP backward.  There is no silent fallback: on a CPU tensor
+the call raises (the CPU path of this repo is the test oracle, not product).
+"""
+from __future__ import annotations
+
+from abc import ABC
+from typing import Optional
+
+import torch
+from torch.nn import Linear, Sequential
+
+from pdg.engine import PARAM_NAMES, EPDEngine
+from pdg.graph import Data
+from pdg.plan import plan_for
+
+_STAT_ORDER = ("mean_pos", "std_pos", "mean_mean_stress", "std_mean_stress", "mean_local_stress",
+               "std_local_stress", "mean_edge_weight", "std_edge_weight")
+
+
+class GraphLayerNorm(torch.nn.Module):
+    """torch_geometric ``LayerNorm(C)`` in its default ``mode="graph"`` with ``batch=None``:
+    ``(x - x.mean()) / (x.std(unbiased=False) + eps) * weight + bias`` over the whole input.
+    Parameters ``weight`` (ones) and ``bias`` (zeros) as in PyG, so state_dict keys match."""
+
+    def __init__(self, in_channels: int, eps: float = 1e-5) -> None:
+        super().__init__()
+        self.in_channels = in_channels
+        self.eps = eps
+        self.weight = torch.nn.Parameter(torch.ones(in_channels))
+        self.bias = torch.nn.Parameter(torch.zeros(in_channels))
+
+    def forward(self, x: torch.Tensor, batch: Optional[torch.Tensor] = None) -> torch.Tensor:
+        if batch is not None:
+            raise NotImplementedError("per-graph LayerNorm (batch=...) is not used by the reference model")
+        x = x - x.mean()
+        out = x / (x.std(unbiased=False) + self.eps)
+        return out * self.weight + self.bias
+
+    def extra_repr(self) -> str:
+        return f"{self.in_channels}, mode=graph"
+
+
+def print_model(model: torch.nn.Module, data_loader, device: str) -> str:
+    """models.py:33-41 (PyG ``summary`` is unavailable): a parameter table."""
+    lines = [f"{type(model).__name__}  (parameters: {sum(p.numel() for p in model.parameters()):,})"]
+    for name, p in model.named_parameters():
+        lines.append(f"  {name:40s} {tuple(p.shape)}")
+    return "\n".join(lines)
+
+
+def save_model_checkpoint(model: torch.nn.Module, optimizer: torch.optim.Optimizer, epoch: int,
+                          filename: str) -> None:
+    """models.py:44-63 — identical checkpoint dict."""
+    ckpt = {"model_state_dict": model.state_dict(), "optimizer_state_dict": optimizer.state_dict(),
+            "epoch": epoch}
+    for k in ("mean_pos", "mean_mean_stress", "std_mean_stress", "mean_local_stress", "std_pos",
+              "std_local_stress", "mean_edge_weight", "std_edge_weight"):
+        ckpt[k] = getattr(model, k)
+    torch.save(ckpt, filename)
+
+
+def load_model_checkpoint(model: torch.nn.Module, filename: str,
+                          optimizer: Optional[torch.optim.Optimizer] = None) -> int:
+    """models.py:66-87.  Loads with ``weights_only=True`` (the checkpoint holds only
+    tensors, ints and optimizer state)."""
+    map_location = None if torch.cuda.is_available() else torch.device("cpu")
+    ckpt = torch.load(filename, map_location=map_location, weights_only=True)
+    model.load_state_dict(ckpt["model_state_dict"])
+    if optimizer:
+        optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+    for k in _STAT_ORDER:
+        setattr(model, k, ckpt[k])
+    return ckpt["epoch"]
+
+
+def load_optimizer_checkpoint(optimizer: torch.optim.Optimizer, filename: str) -> torch.optim.Optimizer:
+    """models.py:90-95."""
+    ckpt = torch.load(filename, weights_only=True)
+    optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+    return optimizer
+
+
+class StressFieldBaseModel(torch.nn.Module, ABC):
+    """models.py:98-179."""
+
+    def __init__(self, latent_size: int, input_nodes_features_size: int, output_nodes_features_size: int,
+                 mean_pos=torch.Tensor(1), std_pos=torch.Tensor(1), mean_mean_stress=torch.Tensor(1),
+                 std_mean_stress=torch.Tensor(1), mean_local_stress=torch.Tensor(1),
+                 std_local_stress=torch.Tensor(1), mean_edge_weight=torch.Tensor(1),
+                 std_edge_weight=torch.Tensor(1)):
+        super().__init__()
+        self.latent_size = latent_size
+        self.input_nodes_features_size = input_nodes_features_size
+        self.output_nodes_features_size = output_nodes_features_size
+        self.mean_pos = mean_pos
+        self.std_pos = std_pos
+        self.mean_mean_stress = mean_mean_stress
+        self.std_mean_stress = std_mean_stress
+        self.mean_local_stress = mean_local_stress
+        self.std_local_stress = std_local_stress
+        self.mean_edge_weight = mean_edge_weight
+        self.std_edge_weight = std_edge_weight
+
+    def format_node_features(self, mesh_graph, scale_data: bool) -> torch.Tensor:
+        pos, mean_stress, nodes_types = mesh_graph.pos, mesh_graph.mean_stress, mesh_graph.nodes_types
+        if scale_data:
+            mean_stress = (mean_stress - self.mean_mean_stress) / self.std_mean_stress
+            pos = (pos - self.mean_pos) / self.std_pos
+        return torch.hstack([mean_stress, pos, nodes_types])
+
+    def format_edge_features(self, mesh_graph, scale_data: bool) -> torch.Tensor:
+        edge_attr = mesh_graph.edge_attr
+        if scale_data:
+            edge_attr = (edge_attr - self.mean_edge_weight) / self.std_edge_weight
+        return edge_attr
+
+    def to(self, device, *args, **kwargs) -> torch.nn.Module:
+        for attr in _STAT_ORDER:
+            value = getattr(self, attr)
+            if value is not None:
+                setattr(self, attr, value.to(device))
+        return super().to(device, *args, **kwargs)
+
+
+class Processor(torch.nn.Module):
+    """models.py:182-243: the weight-shared message-passing block (parameters only;
+    the fused HIP step in pdg.engine executes it)."""
+
+    def __init__(self, latent_size: int, input_nodes_features_size: int, input_edges_features_size: int):
+        super().__init__()
+        self.latent_size = latent_size
+        self.edge_net = Sequential(Linear(input_edges_features_size, latent_size), torch.nn.ReLU(),
+                                   Linear(latent_size, latent_size), torch.nn.ReLU(), GraphLayerNorm(latent_size))
+        self.node_net = Sequential(Linear(input_nodes_features_size, latent_size), torch.nn.ReLU(),
+                                   Linear(latent_size, latent_size), torch.nn.ReLU(), GraphLayerNorm(latent_size))
+
+
+class _EPDFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, plan, stats8, scale_output, scale_input, pos, mean_stress, nodes_types, edge_attr,
+                *params):
+        P = dict(zip(PARAM_NAMES, params))
+        need_grad = any(p.requires_grad for p in params)
+        y, fctx = model._engine_for(pos.device).forward(
+            P, stats8, plan, pos, mean_stress, nodes_types, edge_attr, model.message_passing_steps,
+            scale_input, scale_output, need_grad)
+        ctx.fctx = fctx
+        ctx.model = model
+        ctx.save_for_backward(*params)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        params = ctx.saved_tensors
+        P = dict(zip(PARAM_NAMES, params))
+        if ctx.fctx.scale_output:
+            P["_std_local_stress"] = ctx.model.std_local_stress
+        G = {n: torch.zeros_like(p) for n, p in zip(PARAM_NAMES, params)}
+        ctx.model._engine_for(gy.device).backward(P, ctx.fctx, gy, G)
+        ctx.fctx = None
+        return (None,) * 9 + tuple(G[n] for n in PARAM_NAMES)
+
+
+class EncodeProcessDecode(StressFieldBaseModel):
+    """models.py:246-326."""
+
+    def __init__(self, input_edges_features_size: int, message_passing_steps: int, *args, **kwargs):
+        super().__init__(*args, **kwargs)
+        if self.latent_size != 128:
+            raise ValueError("the HIP kernels are specialised for latent_size=128 (all reference configs)")
+        self.message_passing_steps = message_passing_steps
+        self.input_edges_features_size = input_edges_features_size
+        L = self.latent_size
+        self.node_encoder = Sequential(Linear(self.input_nodes_features_size, L), torch.nn.ReLU(), Linear(L, L),
+                                       torch.nn.ReLU(), GraphLayerNorm(L))
+        self.edge_encoder = Sequential(Linear(self.input_edges_features_size, L), torch.nn.ReLU(), Linear(L, L),
+                                       torch.nn.ReLU(), GraphLayerNorm(L))
+        self.processor = Processor(L, input_nodes_features_size=L * 2, input_edges_features_size=L * 3)
+        self.node_decoder = Sequential(Linear(L, L), torch.nn.ReLU(), Linear(L, self.output_nodes_features_size))
+        self._engines: dict = {}
+
+    def _engine_for(self, device) -> EPDEngine:
+        key = str(device)
+        if key not in self._engines:
+            self._engines[key] = EPDEngine(device)
+        return self._engines[key]
+
+    def stats_tensor(self, device) -> torch.Tensor:
+        vals = []
+        for k in _STAT_ORDER:
+            v = getattr(self, k)
+            vals.append(torch.as_tensor(v, dtype=torch.float32).reshape(-1)[:1].to(device))
+        return torch.cat(vals).contiguous()
+
+    def forward(self, mesh_graph, scale_output: bool = True, scale_input: bool = True):
+        dev = mesh_graph.pos.device
+        if dev.type != "cuda":
+            raise RuntimeError("EncodeProcessDecode runs on the MI355X HIP path only; move the batch to a HIP "
+                               "device (the CPU restatement lives in oracle/ and is test-only)")
+        if self.input_nodes_features_size != 6 or self.input_edges_features_size != 1 \
+                or self.output_nodes_features_size != 3:
+            raise ValueError("HIP path supports the reference feature sizes (6 node, 1 edge, 3 outputs)")
+        ms = mesh_graph.mean_stress
+        flag = torch.zeros(1, dtype=torch.int32, device=dev)
+        from pdg.lib import lib, stream_handle
+        lib.pdg_any_nonzero(ms.data_ptr(), ms.numel(), flag.data_ptr(), stream_handle(dev))
+        if not bool(flag.item()):   # models.py:294-299 (same host sync as the reference's torch.any)
+            return Data(local_stress=torch.zeros_like(ms), edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)
+        plan = plan_for(mesh_graph)
+        params = [self.get_parameter(n) for n in PARAM_NAMES]
+        pos = mesh_graph.pos.float().contiguous()
+        ms = ms.float().contiguous()
+        types = mesh_graph.nodes_types.reshape(-1).to(torch.int64).contiguous()
+        ea = mesh_graph.edge_attr.reshape(-1).float().contiguous()
+        y = _EPDFunction.apply(self, plan, self.stats_tensor(dev), bool(scale_output), bool(scale_input), pos, ms,
+                               types, ea, *params)
+        return Data(local_stress=y, edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)

@@ -1,0 +1,322 @@
+"""Forward/backward orchestration of EncodeProcessDecode on the HIP kernels.
+
+One call of :meth:`EPDEngine.forward` runs the whole encode-process-decode
+stack of ``gnn_local_stress/models.py:288-326`` as a fixed sequence of HIP
+launches on the current stream (no host sync, no torch compute ops); with
+``need_grad`` it keeps the activations the backward needs.
+:meth:`EPDEngine.backward` runs the reverse sequence and accumulates every
+parameter gradient into caller-provided fp32 buffers.
+
+Per message-passing step t (weights shared across steps, models.py:313-314):
+
+  forward                                   kernels
+  x_t = LN_n(a2n_{t-1}) + x_{t-1}           pdg_node_pq      (also P = Wa x_t, Q = Wb x_t)
+  e_t = LN_e(a2e_{t-1}) + e_{t-1}           pdg_edge_fwd     (C = Wc e_t + b1, both edge_net
+  a1m,a2m (message), a1e,a2e (edge upd.)                      evaluations, LN partials)
+  aggr = sum_dst LN_m(a2m)                  pdg_segment_sum
+  a1n = relu(Wn1 [aggr, x_t] + bn1)         pdg_node_mlp1
+  a2n = relu(Wn2 a1n + bn2)                 pdg_mlp2_fwd
+
+Graph-global LayerNorm statistics are reduced by pdg_ln_finalize between the
+producer and the consumer of each normalised tensor.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import torch
+
+from .lib import LN_BWD_BYTES, LN_STAT_BYTES, lib, stream_handle
+from .plan import GraphPlan
+
+L = 128
+
+PARAM_SHAPES = [  # state_dict order of gnn_local_stress/models.py:246-286
+    ("node_encoder.0.weight", (L, 6)), ("node_encoder.0.bias", (L,)),
+    ("node_encoder.2.weight", (L, L)), ("node_encoder.2.bias", (L,)),
+    ("node_encoder.4.weight", (L,)), ("node_encoder.4.bias", (L,)),
+    ("edge_encoder.0.weight", (L, 1)), ("edge_encoder.0.bias", (L,)),
+    ("edge_encoder.2.weight", (L, L)), ("edge_encoder.2.bias", (L,)),
+    ("edge_encoder.4.weight", (L,)), ("edge_encoder.4.bias", (L,)),
+    ("processor.edge_net.0.weight", (L, 3 * L)), ("processor.edge_net.0.bias", (L,)),
+    ("processor.edge_net.2.weight", (L, L)), ("processor.edge_net.2.bias", (L,)),
+    ("processor.edge_net.4.weight", (L,)), ("processor.edge_net.4.bias", (L,)),
+    ("processor.node_net.0.weight", (L, 2 * L)), ("processor.node_net.0.bias", (L,)),
+    ("processor.node_net.2.weight", (L, L)), ("processor.node_net.2.bias", (L,)),
+    ("processor.node_net.4.weight", (L,)), ("processor.node_net.4.bias", (L,)),
+    ("node_decoder.0.weight", (L, L)), ("node_decoder.0.bias", (L,)),
+    ("node_decoder.2.weight", (3, L)), ("node_decoder.2.bias", (3,)),
+]
+PARAM_NAMES = [n for n, _ in PARAM_SHAPES]
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+class _StatBuf:
+    """A device array of pdg_ln_stat (or pdg_ln_bwd) structs."""
+
+    def __init__(self, n: int, nbytes: int, device) -> None:
+        self.buf = torch.zeros(max(n, 1) * nbytes, dtype=torch.uint8, device=device)
+        self.nbytes = nbytes
+
+    def __getitem__(self, i: int) -> int:
+        return self.buf.data_ptr() + i * self.nbytes
+
+
+@dataclass
+class FwdCtx:
+    plan: GraphPlan
+    steps: int
+    scale_output: bool
+    x_in: torch.Tensor = None
+    e_in: torch.Tensor = None
+    a1_ne: torch.Tensor = None
+    a2_ne: torch.Tensor = None
+    a1_ee: torch.Tensor = None
+    a2_ee: torch.Tensor = None
+    per_step: list = field(default_factory=list)
+    x_S: torch.Tensor = None
+    a1d: torch.Tensor = None
+    stats: _StatBuf = None
+
+
+class EPDEngine:
+    """Stateless executor; parameters are passed per call as a name->tensor dict."""
+
+    def __init__(self, device: torch.device) -> None:
+        self.device = torch.device(device)
+        self.max_blocks = lib.pdg_max_blocks()
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self._part_a = torch.empty(self.max_blocks * 2, **f64)
+        self._part_b = torch.empty(self.max_blocks * 2, **f64)
+        self._part_col = torch.empty(self.max_blocks * 256, **f64)
+        self._part_narrow = torch.empty(self.max_blocks * (L * 6 + L + 6), **f64)
+        self._nparts = ctypes.c_int(0)
+        self._nslabs = 256
+        # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
+        self.timed: dict | None = None
+
+    def _t(self, name: str, fn, *args):
+        """Launch fn(*args); when timing is enabled for `name`, bracket it with HIP events
+        on the current stream (the stream every launch of this engine uses)."""
+        if self.timed is None or name not in self.timed:
+            return fn(*args)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        r = fn(*args)
+        b.record()
+        self.timed[name].append((a, b))
+        return r
+
+    # ------------------------------------------------------------------ helpers
+    def _empty(self, *shape):
+        return torch.empty(*shape, dtype=torch.float32, device=self.device)
+
+    def _finalize(self, part, count: int, out_ptr: int, s) -> None:
+        lib.pdg_ln_finalize(part.data_ptr(), self._nparts.value, float(count), out_ptr, s)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, P: dict, stats8: torch.Tensor, plan: GraphPlan, pos, mean_stress, nodes_types,
+                edge_attr, steps: int, scale_input: bool, scale_output: bool, need_grad: bool):
+        s = stream_handle(self.device)
+        N, E = plan.n_nodes, plan.n_edges
+        if N == 0:
+            raise ValueError("empty graph")
+        if E == 0:
+            raise ValueError("graphs without edges are not supported by the fused edge kernels")
+        np_ = ctypes.byref(self._nparts)
+        ctx = FwdCtx(plan=plan, steps=steps, scale_output=scale_output)
+        ctx.stats = _StatBuf(2 + 3 * steps, LN_STAT_BYTES, self.device)
+        st = ctx.stats
+        x_in = self._empty(N, 6)
+        e_in = self._empty(E)
+        lib.pdg_format_inputs(N, E, _p(pos), _p(mean_stress), _p(nodes_types), _p(edge_attr), _p(plan.perm),
+                              _p(stats8), int(scale_input), _p(x_in), _p(e_in), s)
+        # encoders (models.py:308-309)
+        a1_ne, a2_ne = self._empty(N, L), self._empty(N, L)
+        lib.pdg_encoder_fwd(N, 6, _p(x_in), _p(P["node_encoder.0.weight"]), _p(P["node_encoder.0.bias"]),
+                            _p(P["node_encoder.2.weight"]), _p(P["node_encoder.2.bias"]), _p(a1_ne), _p(a2_ne),
+                            _p(self._part_a), np_, s)
+        self._finalize(self._part_a, N * L, st[0], s)
+        a1_ee, a2_ee = self._empty(E, L), self._empty(E, L)
+        lib.pdg_encoder_fwd(E, 1, _p(e_in), _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]),
+                            _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]), _p(a1_ee), _p(a2_ee),
+                            _p(self._part_a), np_, s)
+        self._finalize(self._part_a, E * L, st[1], s)
+        if need_grad:
+            ctx.x_in, ctx.e_in, ctx.a1_ne, ctx.a2_ne, ctx.a1_ee, ctx.a2_ee = x_in, e_in, a1_ne, a2_ne, a1_ee, a2_ee
+
+        W1, b1 = P["processor.edge_net.0.weight"], P["processor.edge_net.0.bias"]
+        W2, b2 = P["processor.edge_net.2.weight"], P["processor.edge_net.2.bias"]
+        ge, be = P["processor.edge_net.4.weight"], P["processor.edge_net.4.bias"]
+        Wn1, bn1 = P["processor.node_net.0.weight"], P["processor.node_net.0.bias"]
+        Wn2, bn2 = P["processor.node_net.2.weight"], P["processor.node_net.2.bias"]
+        gn, bnn = P["processor.node_net.4.weight"], P["processor.node_net.4.bias"]
+
+        a2n_prev, stn_prev, gn_prev, bn_prev = a2_ne, st[0], P["node_encoder.4.weight"], P["node_encoder.4.bias"]
+        a2e_prev, ste_prev, ge_prev, be_prev = a2_ee, st[1], P["edge_encoder.4.weight"], P["edge_encoder.4.bias"]
+        x_prev = e_prev = None
+        Pm, Qm = self._empty(N, L), self._empty(N, L)
+        for t in range(steps):
+            i_m, i_e, i_n = 2 + 3 * t, 3 + 3 * t, 4 + 3 * t
+            x_t = self._empty(N, L)
+            lib.pdg_node_pq(N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_t), _p(W1),
+                            _p(Pm), _p(Qm), s)
+            e_t = self._empty(E, L)
+            a1m, a2m, a1e, a2e = (self._empty(E, L) for _ in range(4))
+            self._t("edge_fwd", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t),
+                             _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
+                             _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), np_, s)
+            self._finalize(self._part_a, E * L, st[i_m], s)
+            self._finalize(self._part_b, E * L, st[i_e], s)
+            aggr = self._empty(N, L)
+            self._t("segment_sum", lib.pdg_segment_sum, N, _p(plan.rowptr_dst), _p(a2m), st[i_m], _p(ge), _p(be),
+                    _p(aggr), s)
+            a1n, a2n = self._empty(N, L), self._empty(N, L)
+            lib.pdg_node_mlp1(N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(a1n), s)
+            lib.pdg_mlp2_fwd(N, _p(a1n), _p(Wn2), _p(bn2), _p(a2n), _p(self._part_a), np_, s)
+            self._finalize(self._part_a, N * L, st[i_n], s)
+            if need_grad:
+                ctx.per_step.append(dict(x=x_t, e=e_t, a1m=a1m, a2m=a2m, a1e=a1e, a2e=a2e, aggr=aggr,
+                                         a1n=a1n, a2n=a2n, i_m=i_m, i_e=i_e, i_n=i_n))
+            a2n_prev, stn_prev, gn_prev, bn_prev = a2n, st[i_n], gn, bnn
+            a2e_prev, ste_prev, ge_prev, be_prev = a2e, st[i_e], ge, be
+            x_prev, e_prev = x_t, e_t
+        # decoder (models.py:316-321)
+        x_S, a1d, y = self._empty(N, L), self._empty(N, L), self._empty(N, 3)
+        if x_prev is None:
+            raise ValueError("message_passing_steps must be >= 1")
+        lib.pdg_decoder_fwd(N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_S),
+                            _p(P["node_decoder.0.weight"]), _p(P["node_decoder.0.bias"]), _p(a1d),
+                            _p(P["node_decoder.2.weight"]), _p(P["node_decoder.2.bias"]), _p(stats8),
+                            int(scale_output), _p(y), s)
+        if need_grad:
+            ctx.x_S, ctx.a1d = x_S, a1d
+        return y, ctx
+
+    # ------------------------------------------------------------------ backward
+    def transposed(self, P: dict) -> dict:
+        """W^T copies of every weight block the backward GEMMs read."""
+        s = stream_handle(self.device)
+        out = {}
+
+        def tr(name, key, col0, ld):
+            W = P[name]
+            T = self._empty(L, L)
+            lib.pdg_transpose(L, L, ld, W.data_ptr() + 4 * col0, T.data_ptr(), s)
+            out[key] = T
+
+        tr("node_decoder.0.weight", "Wd1T", 0, L)
+        tr("processor.edge_net.2.weight", "W2T", 0, L)
+        tr("processor.edge_net.0.weight", "WaT", 0, 3 * L)
+        tr("processor.edge_net.0.weight", "WbT", L, 3 * L)
+        tr("processor.edge_net.0.weight", "WcT", 2 * L, 3 * L)
+        tr("processor.node_net.2.weight", "Wn2T", 0, L)
+        tr("processor.node_net.0.weight", "Wn1aT", 0, 2 * L)
+        tr("processor.node_net.0.weight", "Wn1bT", L, 2 * L)
+        tr("node_encoder.2.weight", "Wne2T", 0, L)
+        tr("edge_encoder.2.weight", "Wee2T", 0, L)
+        return out
+
+    def backward(self, P: dict, ctx: FwdCtx, gy: torch.Tensor, G: dict) -> None:
+        """Accumulate d(loss)/d(param) into G[name] (fp32, same shapes as P)."""
+        s = stream_handle(self.device)
+        plan = ctx.plan
+        N, E = plan.n_nodes, plan.n_edges
+        np_ = ctypes.byref(self._nparts)
+        T = self.transposed(P)
+        st = ctx.stats
+        lb = _StatBuf(4, LN_BWD_BYTES, self.device)
+        ns = self._nslabs
+        slab_names = ["W2", "Wc", "Wa", "Wb", "Wn2", "Wn1a", "Wn1b", "d1", "ne2", "ee2"]
+        slabs_all = torch.zeros(len(slab_names), ns, L * L + L, dtype=torch.float32, device=self.device)
+        slabs = {k: slabs_all[i] for i, k in enumerate(slab_names)}
+
+        def wacc(rows, Gt, X, key, G2=None, X2=None):
+            lib.pdg_wgrad_accum(rows, _p(Gt), _p(X), _p(G2), _p(X2), _p(slabs[key]), ns, s)
+
+        def colsum(rows, gy_rows, gidx, a2, st_ptr, gname, bname, lb_ptr):
+            lib.pdg_ln_colsum(rows, _p(gy_rows), _p(gidx), _p(a2), st_ptr, _p(self._part_col), np_, s)
+            lib.pdg_ln_colsum_finalize(_p(self._part_col), self._nparts.value, _p(P[gname]), st_ptr,
+                                       _p(G[gname]), _p(G[bname]), lb_ptr, s)
+
+        gy = gy.contiguous()
+        if ctx.scale_output:
+            gy = gy * P["_std_local_stress"]
+        # decoder
+        gz1d, gx = self._empty(N, L), self._empty(N, L)
+        lib.pdg_decoder_bwd(N, _p(gy), _p(ctx.a1d), _p(P["node_decoder.2.weight"]), _p(T["Wd1T"]), _p(gz1d),
+                            _p(gx), s)
+        lib.pdg_wgrad_narrow(N, _p(ctx.a1d), _p(gy), 3, 1, _p(self._part_narrow), _p(G["node_decoder.2.weight"]),
+                             None, _p(G["node_decoder.2.bias"]), s)
+        wacc(N, gz1d, ctx.x_S, "d1")
+
+        ge_next = torch.zeros(E, L, dtype=torch.float32, device=self.device)
+        gz2n, gz1n, gaggr, gx_part = (self._empty(N, L) for _ in range(4))
+        gP, gQ, gx_t = (self._empty(N, L) for _ in range(3))
+        gz2m, gz1m, gz2e, gz1e, gC, ge_out = (self._empty(E, L) for _ in range(6))
+        gx_next = gx
+        for t in reversed(range(ctx.steps)):
+            d = ctx.per_step[t]
+            # node_net tail: n_t = LN_n(a2n_t), gy = gx_next   (x_{t+1} = n_t + x_t)
+            colsum(N, gx_next, None, d["a2n"], st[d["i_n"]], "processor.node_net.4.weight",
+                   "processor.node_net.4.bias", lb[0])
+            lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], lb[0],
+                             _p(P["processor.node_net.4.weight"]), _p(T["Wn2T"]), _p(gz2n), _p(gz1n), s)
+            wacc(N, gz2n, d["a1n"], "Wn2")
+            wacc(N, gz1n, d["aggr"], "Wn1a")
+            wacc(N, gz1n, d["x"], "Wn1b")
+            lib.pdg_gemm_dual(N, _p(gz1n), _p(T["Wn1aT"]), _p(T["Wn1bT"]), None, _p(gx_next), _p(gaggr),
+                              _p(gx_part), s)
+            # edge_net LayerNorm sums: message (gy = gaggr[dst]) and edge update (gy = ge_next)
+            colsum(E, gaggr, plan.dst, d["a2m"], st[d["i_m"]], "processor.edge_net.4.weight",
+                   "processor.edge_net.4.bias", lb[1])
+            colsum(E, ge_next, None, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
+                   "processor.edge_net.4.bias", lb[2])
+            self._t("edge_bwd", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr), _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]),
+                             _p(d["a1e"]), st[d["i_m"]], st[d["i_e"]], lb[1], lb[2],
+                             _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]), _p(gz2m), _p(gz1m),
+                             _p(gz2e), _p(gz1e), _p(gC), _p(ge_out), s)
+            self._t("wgrad_W2", wacc, E, gz2m, d["a1m"], "W2", gz2e, d["a1e"])
+            wacc(E, gC, d["e"], "Wc")
+            self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src), _p(plan.perm_src), _p(gz1m),
+                                   _p(gz1e), _p(gP), _p(gQ), s)
+            wacc(N, gP, d["x"], "Wa")
+            wacc(N, gQ, d["x"], "Wb")
+            lib.pdg_gemm_sum2(N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part), _p(gx_t), s)
+            gx_next, gx_t = gx_t, gx_next
+            ge_next, ge_out = ge_out, ge_next
+        # encoders
+        gz2, gz1 = self._empty(N, L), self._empty(N, L)
+        colsum(N, gx_next, None, ctx.a2_ne, st[0], "node_encoder.4.weight", "node_encoder.4.bias", lb[3])
+        lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], lb[3],
+                         _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), s)
+        wacc(N, gz2, ctx.a1_ne, "ne2")
+        lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
+                             _p(G["node_encoder.0.bias"]), None, s)
+        gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
+        colsum(E, ge_next, None, ctx.a2_ee, st[1], "edge_encoder.4.weight", "edge_encoder.4.bias", lb[3])
+        lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], lb[3],
+                         _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), s)
+        wacc(E, gz2e_, ctx.a1_ee, "ee2")
+        lib.pdg_wgrad_narrow(E, _p(gz1e_), _p(ctx.e_in), 1, 0, _p(self._part_narrow), _p(G["edge_encoder.0.weight"]),
+                             _p(G["edge_encoder.0.bias"]), None, s)
+        # slab reductions into the parameter gradients
+        red = [
+            ("W2", "processor.edge_net.2.weight", L, 0, "processor.edge_net.2.bias"),
+            ("Wc", "processor.edge_net.0.weight", 3 * L, 2 * L, "processor.edge_net.0.bias"),
+            ("Wa", "processor.edge_net.0.weight", 3 * L, 0, None),
+            ("Wb", "processor.edge_net.0.weight", 3 * L, L, None),
+            ("Wn2", "processor.node_net.2.weight", L, 0, "processor.node_net.2.bias"),
+            ("Wn1a", "processor.node_net.0.weight", 2 * L, 0, "processor.node_net.0.bias"),
+            ("Wn1b", "processor.node_net.0.weight", 2 * L, L, None),
+            ("d1", "node_decoder.0.weight", L, 0, "node_decoder.0.bias"),
+            ("ne2", "node_encoder.2.weight", L, 0, "node_encoder.2.bias"),
+            ("ee2", "edge_encoder.2.weight", L, 0, "edge_encoder.2.bias"),
+        ]
+        for key, wname, ld, col0, bname in red:
+            lib.pdg_wgrad_reduce(_p(slabs[key]), ns, _p(G[wname]), ld, col0, _p(G[bname]) if bname else None, s)

@@ -1,0 +1,112 @@
+"""ctypes binding of libpdivgnn_hip.so (C ABI declared in include/pdivgnn.h).
+
+The library is loaded once, after torch (torch ships the HIP runtime whose
+SONAME, libamdhip64.so.7, the library links against, so both share one runtime).
+There is no fallback: if the library is missing or fails to load, every
+hot-path call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_int64, c_void_p
+from pathlib import Path
+
+import torch  # noqa: F401  (must be loaded before the HIP library)
+
+LIB_PATH = Path(os.environ.get("PDG_LIB", Path(__file__).resolve().parent / "libpdivgnn_hip.so"))
+
+P = c_void_p
+I = c_int
+
+# name -> argtypes (restype is int status unless listed in _RESTYPES)
+SIGNATURES: dict[str, list] = {
+    "pdg_last_error": [],
+    "pdg_version": [],
+    "pdg_max_blocks": [],
+    "pdg_format_inputs": [I, I, P, P, P, P, P, P, I, P, P, P],
+    "pdg_encoder_fwd": [I, I, P, P, P, P, P, P, P, P, P, P],
+    "pdg_ln_finalize": [P, I, c_double, P, P],
+    "pdg_node_pq": [I, P, P, P, P, P, P, P, P, P, P],
+    "pdg_edge_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdg_segment_sum": [I, P, P, P, P, P, P, P],
+    "pdg_node_mlp1": [I, P, P, P, P, P, P],
+    "pdg_mlp2_fwd": [I, P, P, P, P, P, P, P],
+    "pdg_decoder_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
+    "pdg_any_nonzero": [P, c_int64, P, P],
+    "pdg_decoder_bwd": [I, P, P, P, P, P, P, P],
+    "pdg_ln_colsum": [I, P, P, P, P, P, P, P],
+    "pdg_ln_colsum_finalize": [P, I, P, P, P, P, P, P],
+    "pdg_mlp2_bwd": [I, P, P, P, P, P, P, P, P, P, P, P],
+    "pdg_gemm_dual": [I, P, P, P, P, P, P, P, P],
+    "pdg_gemm_sum2": [I, P, P, P, P, P, P, P],
+    "pdg_edge_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdg_pq_scatter_bwd": [I, P, P, P, P, P, P, P, P],
+    "pdg_wgrad_accum": [I, P, P, P, P, P, I, P],
+    "pdg_wgrad_reduce": [P, I, P, I, I, P, P],
+    "pdg_wgrad_narrow": [I, P, P, I, I, P, P, P, P, P],
+    "pdg_nmse_fwd": [I, P, P, P, P, P, P],
+    "pdg_nmse_bwd": [I, P, I, P, P, P, P, I, P, P],
+    "pdg_div_fwd": [I, P, P, P, P, P, P, I, P, P, P],
+    "pdg_div_bwd": [I, P, I, P, P, P, P, P, P, I, I, P, P],
+    "pdg_transpose": [I, I, I, P, P, P],
+    "pdg_nonfinite": [P, c_int64, P, P],
+    "pdg_adam": [c_int64, P, P, P, P, c_float, c_float, c_float, c_float, I, P, P],
+}
+_RESTYPES = {"pdg_last_error": ctypes.c_char_p}
+
+LN_STAT_BYTES = 40   # sizeof(pdg_ln_stat)
+LN_BWD_BYTES = 24    # sizeof(pdg_ln_bwd)
+
+
+class PdgError(RuntimeError):
+    pass
+
+
+class _Lib:
+    def __init__(self) -> None:
+        self._dll = None
+
+    def load(self) -> ctypes.CDLL:
+        if self._dll is None:
+            if not LIB_PATH.exists():
+                raise PdgError(f"{LIB_PATH} not built: run `python p-div-gnn_amd/build.py` "
+                               "(the HIP path has no CPU fallback)")
+            dll = ctypes.CDLL(str(LIB_PATH))
+            for name, args in SIGNATURES.items():
+                fn = getattr(dll, name)
+                fn.argtypes = args
+                fn.restype = _RESTYPES.get(name, c_int)
+            self._dll = dll
+        return self._dll
+
+    def __getattr__(self, name: str):
+        if not name.startswith("pdg_"):
+            raise AttributeError(name)
+        fn = getattr(self.load(), name)
+        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks"):
+            return fn
+
+        def call(*args):
+            rc = fn(*args)
+            if rc != 0:
+                msg = self.load().pdg_last_error().decode(errors="replace")
+                raise PdgError(f"{name} failed ({rc}): {msg}")
+            return rc
+
+        call.__name__ = name
+        return call
+
+
+lib = _Lib()
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

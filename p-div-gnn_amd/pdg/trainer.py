@@ -1,0 +1,117 @@
+"""Native training step: the hot loop of scripts/gnn_train.py:154-207 on the HIP path.
+
+Per step (one minibatch already resident in HBM):
+  forward  model.forward(batch, scale_output=False, scale_input=True)      (gnn_train.py:159-161)
+  target   standardize(local_stress, mean/std_local_stress)                (:162-167)
+  loss     sum_g NMSE_g / B  [+ lambda * sum_g div_g / B]                  (:168-197)
+  backward                                                                 (:205)
+  DP       one all-reduce (mean) of the flat fp32 gradient bucket over RCCL (graph-batch data
+           parallelism across GPUs; new in this build)
+  update   Adam(lr, betas=(0.9, 0.999), eps=1e-8) on the flat parameter buffer (:118, :206)
+
+Parameters and gradients live in one flat buffer each (the model's Parameters
+are views into it), so the all-reduce is a single 669 KB collective and Adam a
+single kernel.  GradScaler (gnn_train.py:111) is an fp32 power-of-two rescale,
+numerically the identity except that it skips the update when a gradient is
+non-finite; the same skip is applied here.
+"""
+from __future__ import annotations
+
+import torch
+
+from .engine import PARAM_NAMES, PARAM_SHAPES, EPDEngine
+from .lib import lib, stream_handle
+from .plan import plan_for
+
+
+class Trainer:
+    def __init__(self, model, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 divergence: bool = False, divergence_penalty: float = 1.0, process_group=None) -> None:
+        dev = next(model.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("Trainer needs the model on a HIP device")
+        self.model = model
+        self.device = dev
+        self.engine: EPDEngine = model._engine_for(dev)
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.divergence = divergence
+        self.penalty = float(divergence_penalty)
+        self.pg = process_group
+        sizes = [int(torch.Size(s).numel()) for _, s in PARAM_SHAPES]
+        total = sum(sizes)
+        self.flat_p = torch.empty(total, dtype=torch.float32, device=dev)
+        self.flat_g = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.P, self.G = {}, {}
+        off = 0
+        with torch.no_grad():
+            for (name, shape), n in zip(PARAM_SHAPES, sizes):
+                p = model.get_parameter(name)
+                view = self.flat_p[off:off + n].view(shape)
+                view.copy_(p.detach())
+                p.data = view                       # the model now shares the flat storage
+                self.P[name] = view
+                self.G[name] = self.flat_g[off:off + n].view(shape)
+                off += n
+        self.step_count = 0
+        self._gt_cache: dict = {}
+        self._skip = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def _gt(self, batch) -> torch.Tensor:
+        key = id(batch)
+        if key not in self._gt_cache:
+            m = self.model
+            self._gt_cache = {key: ((batch.local_stress - m.mean_local_stress) / m.std_local_stress).float().contiguous()}
+        return self._gt_cache[key]
+
+    def step(self, batch) -> dict:
+        """One optimisation step; returns device scalars (no host sync)."""
+        m = self.model
+        s = stream_handle(self.device)
+        plan = plan_for(batch)
+        stats8 = m.stats_tensor(self.device)
+        y, ctx = self.engine.forward(self.P, stats8, plan, batch.pos, batch.mean_stress,
+                                     batch.nodes_types.reshape(-1).contiguous(), batch.edge_attr.reshape(-1),
+                                     m.message_passing_steps, True, False, True)
+        gt = self._gt(batch)
+        B, N = plan.n_graphs, plan.n_nodes
+        f32 = dict(dtype=torch.float32, device=self.device)
+        loss_g, den = torch.empty(B, **f32), torch.empty(B, 3, **f32)
+        lib.pdg_nmse_fwd(B, plan.ptr.data_ptr(), gt.data_ptr(), y.data_ptr(), loss_g.data_ptr(), den.data_ptr(), s)
+        scale = torch.full((1,), 1.0 / B, **f32)
+        gy = torch.empty(N, 3, **f32)
+        lib.pdg_nmse_bwd(B, plan.ptr.data_ptr(), N, gt.data_ptr(), y.data_ptr(), den.data_ptr(), scale.data_ptr(), 0,
+                         gy.data_ptr(), s)
+        out = {"nmse": loss_g.sum() / B}
+        if self.divergence:
+            types = batch.surfaces_nodes_for_div if batch.surfaces_nodes_for_div is not None else batch.nodes_types
+            types = types.reshape(-1).to(torch.int64).contiguous()
+            div = torch.empty(N, 2, **f32)
+            loss_d = torch.empty(B, **f32)
+            lib.pdg_div_fwd(B, plan.ptr.data_ptr(), plan.a_rowptr.data_ptr(), plan.a_col.data_ptr(),
+                            plan.a_val.data_ptr(), types.data_ptr(), y.data_ptr(), 0, div.data_ptr(),
+                            loss_d.data_ptr(), s)
+            sd = torch.full((1,), self.penalty / B, **f32)
+            lib.pdg_div_bwd(B, plan.ptr.data_ptr(), N, plan.at_rowptr.data_ptr(), plan.at_row.data_ptr(),
+                            plan.at_comp.data_ptr(), plan.at_val.data_ptr(), div.data_ptr(), sd.data_ptr(), 0, 1,
+                            gy.data_ptr(), s)
+            out["div"] = loss_d.sum() * (self.penalty / B)
+        self.flat_g.zero_()
+        self.engine.backward(self.P, ctx, gy, self.G)
+        del ctx
+        if self.pg is not None:
+            torch.distributed.all_reduce(self.flat_g, group=self.pg)
+            self.flat_g.mul_(1.0 / torch.distributed.get_world_size(self.pg))
+        self.step_count += 1
+        lib.pdg_nonfinite(self.flat_g.data_ptr(), self.flat_g.numel(), self._skip.data_ptr(), s)
+        lib.pdg_adam(self.flat_p.numel(), self.flat_p.data_ptr(), self.flat_g.data_ptr(), self.exp_avg.data_ptr(),
+                     self.exp_avg_sq.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps, self.step_count,
+                     self._skip.data_ptr(), s)
+        out["skipped"] = self._skip
+        out["total"] = out["nmse"] + out.get("div", 0.0)
+        return out
+
+
+def param_names() -> list:
+    return list(PARAM_NAMES)

@@ -1,0 +1,173 @@
+"""End-to-end parity of the HIP EncodeProcessDecode + losses (SURVEY §4 tiers T2):
+
+* against the reference-generated golden fixtures (tests/golden, the reference's
+  own models.py / gnn_train.py run under the PyG stand-in);
+* against the CPU oracle (oracle/epd_oracle.py) at larger sizes, in fp32 and
+  fp64, so the GPU error is judged against the fp32 noise floor of the
+  reference's own CPU path.
+
+Tolerance (north_star: "within 1e-5 rel fp32"): relative L2 error of the
+output field and of the losses <= 1e-5.  Gradients: each parameter's gradient
+must be as close to the float64 restatement as the reference's own fp32 CPU
+result is, within a factor 2, and never worse than 1e-4 relative L2 (they
+aggregate 10^5-10^7 fp32 products through the tied steps and graph-global
+LayerNorms; DESIGN.md "Parity").
+"""
+import pytest
+import torch
+
+from golden_io import CASES
+from gpu_common import dataset_stats, golden_batch, make_batch, rel
+
+pytestmark = pytest.mark.gpu
+
+OUT_TOL = 1e-5
+GRAD_TOL = 1e-4
+
+
+def _model(steps, stats, params=None):
+    from gnn_local_stress.models import EncodeProcessDecode
+    torch.manual_seed(69)
+    m = EncodeProcessDecode(input_edges_features_size=1, message_passing_steps=steps, latent_size=128,
+                            input_nodes_features_size=6, output_nodes_features_size=3,
+                            **{k: torch.as_tensor(v).float() for k, v in stats.items()})
+    if params is not None:
+        m.load_state_dict(params)
+    return m.to("cuda")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_forward_and_grads_match_golden(case):
+    from gnn_local_stress import losses
+    g, batch = golden_batch(case)
+    steps = int(g["steps"])
+    model = _model(steps, g["stats"], g["params"])
+    with torch.no_grad():
+        out = model(batch, scale_output=True).local_stress
+    assert rel(out, g["out_scaled"]) < OUT_TOL, rel(out, g["out_scaled"])
+    pred = model(batch, scale_output=False).local_stress
+    assert rel(pred.detach(), g["pred"]) < OUT_TOL
+    gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
+    total, nmse, div = losses.batch_loss(pred, batch, gt, divergence=bool(g["divergence"]),
+                                         divergence_penalty=float(g["penalty"]))
+    assert abs(float(nmse) - float(g["loss_nmse"])) <= OUT_TOL * abs(float(g["loss_nmse"]))
+    assert abs(float(total.detach()) - float(g["loss_total"])) <= OUT_TOL * abs(float(g["loss_total"]))
+    model.zero_grad()
+    total.backward()
+    # float64 restatement of the same step: the noise floor of the fp32 reference
+    _, _, g64 = _oracle_grads(g["params"], {k: float(v) for k, v in g["stats"].items()}, batch, steps,
+                              torch.float64, bool(g["divergence"]), float(g["penalty"]))
+    for name, p in model.named_parameters():
+        ref32 = rel(g["grads"][name], g64[name])
+        assert rel(p.grad, g64[name]) <= max(GRAD_TOL, 2 * ref32), (name, rel(p.grad, g64[name]), ref32)
+        # direct check against the reference's fp32 gradient: bounded by the two errors to fp64
+        d = rel(p.grad, g["grads"][name])
+        assert d <= max(GRAD_TOL, 1.5 * (rel(p.grad, g64[name]) + ref32)), (name, d)
+
+
+def test_per_graph_losses_match_oracle():
+    from gnn_local_stress import losses
+    from oracle import epd_oracle as O
+    g, batch = golden_batch("batch3_div")
+    pred = torch.from_numpy(g["pred"]).cuda().requires_grad_(True)
+    gt = torch.from_numpy(g["gt_std"]).cuda()
+    ptr = g["ptr"]
+    for i in range(len(ptr) - 1):
+        s, t = int(ptr[i]), int(ptr[i + 1])
+        p_cpu = pred.detach().cpu()[s:t].clone().requires_grad_(True)
+        ref = O.normalized_mse_loss_single(gt.cpu()[s:t], p_cpu)
+        got = losses.normalized_mse_loss_single(ground_truth_local_stress=gt[s:t], predicted_local_stress=pred[s:t])
+        assert abs(float(got) - float(ref)) <= 1e-6 * abs(float(ref))
+        types = batch.nodes_types[s:t]
+        for strat in ("square", "abs"):
+            ref_d = O.compute_divergence(p_cpu, g["op_divs"][i], types.cpu(), strat)
+            got_d = losses.compute_divergence(pred[s:t], g["op_divs"][i].cuda(), types, reduce_strategy=strat)
+            assert abs(float(got_d) - float(ref_d)) <= 1e-5 * abs(float(ref_d)), strat
+            gref, = torch.autograd.grad(ref_d, p_cpu)
+            ggot, = torch.autograd.grad(got_d, pred)
+            assert rel(ggot[s:t], gref) < 1e-5
+    with pytest.raises(AttributeError):
+        losses.compute_divergence(pred[:5], g["op_divs"][0].cuda(), batch.nodes_types[:5], reduce_strategy="cube")
+
+
+def _oracle_grads(model_params, stats, batch, steps, dtype, divergence, penalty):
+    from oracle import epd_oracle as O
+    P = {k: v.detach().cpu().to(dtype).clone().requires_grad_(True) for k, v in model_params.items()}
+    st = {k: torch.as_tensor(v).cpu().to(dtype) for k, v in stats.items()}
+    b = batch
+    args = (b.pos.cpu().to(dtype), b.mean_stress.cpu().to(dtype), b.nodes_types.cpu(), b.edge_index.cpu(),
+            b.edge_attr.cpu().to(dtype))
+    pred = O.epd_forward(P, st, *args, steps, scale_output=False)
+    gt = (b.local_stress.cpu().to(dtype) - st["mean_local_stress"]) / st["std_local_stress"]
+    ops = [d.op_div_matrix.to(dtype) for d in b._data_list]
+    total, nmse, div = O.batch_loss(pred, gt, b.ptr, ops, b.nodes_types.cpu(), divergence, penalty)
+    total.backward()
+    return pred.detach(), float(total), {k: v.grad for k, v in P.items()}
+
+
+@pytest.mark.parametrize("nmesh,ngraph,steps,divergence", [(21, 2, 10, True), (31, 1, 4, False)])
+def test_training_step_matches_oracle_fp32_and_fp64(nmesh, ngraph, steps, divergence):
+    from gnn_local_stress import losses
+    from pdg import meshgen
+    samples = meshgen.make_dataset(ngraph, n=nmesh, hole_radius=(0.15, 0.3), seed=5)
+    batch = make_batch(samples)
+    stats = {k: float(v) for k, v in dataset_stats(batch).items()}
+    model = _model(steps, stats)
+    params = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    pred = model(batch, scale_output=False).local_stress
+    gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
+    total, _, _ = losses.batch_loss(pred, batch, gt, divergence=divergence, divergence_penalty=10.0)
+    model.zero_grad()
+    total.backward()
+    p32, t32, g32 = _oracle_grads(params, stats, batch, steps, torch.float32, divergence, 10.0)
+    p64, t64, g64 = _oracle_grads(params, stats, batch, steps, torch.float64, divergence, 10.0)
+    floor = rel(p32, p64)
+    assert rel(pred.detach(), p32) < OUT_TOL, (rel(pred.detach(), p32), floor)
+    assert rel(pred.detach(), p64) < OUT_TOL
+    assert abs(float(total) - t64) <= OUT_TOL * abs(t64)
+    for name, p in model.named_parameters():
+        ref32 = rel(g32[name], g64[name])
+        assert rel(p.grad, g64[name]) <= max(GRAD_TOL, 2 * ref32), (name, rel(p.grad, g64[name]), ref32)
+
+
+def test_zero_mean_stress_guard_returns_zeros():
+    from pdg import meshgen
+    batch = make_batch([meshgen.hole_plate(9, seed=2)])
+    batch.mean_stress = torch.zeros_like(batch.mean_stress)
+    model = _model(2, {k: 1.0 for k in ("mean_pos", "std_pos", "mean_mean_stress", "std_mean_stress",
+                                        "mean_local_stress", "std_local_stress", "mean_edge_weight",
+                                        "std_edge_weight")})
+    out = model(batch)
+    assert out.local_stress.shape == batch.mean_stress.shape
+    assert float(out.local_stress.abs().max()) == 0.0 and not out.local_stress.requires_grad
+
+
+def test_isolated_node_and_ragged_batch():
+    """A node with no incident edge (in-degree 0) and graphs of unequal sizes."""
+    from pdg import graph, meshgen
+    from oracle import epd_oracle as O
+    s1 = meshgen.hole_plate(7, seed=4)
+    s2 = meshgen.hole_plate(12, hole_radius=0.25, seed=6)
+    d1 = graph.sample_to_data(s1)
+    # append an isolated node to graph 1
+    d1.pos = torch.cat([d1.pos, torch.tensor([[50.0, 50.0]])])
+    d1.mean_stress = torch.cat([d1.mean_stress, d1.mean_stress[:1]])
+    d1.local_stress = torch.cat([d1.local_stress, d1.local_stress[:1]])
+    d1.nodes_types = torch.cat([d1.nodes_types, torch.zeros(1, 1, dtype=torch.int64)])
+    d1.surfaces_nodes_for_div = d1.nodes_types
+    b = graph.Batch.from_data_list([d1, graph.sample_to_data(s2)]).to("cuda")
+    stats = {k: float(v) for k, v in dataset_stats(b).items()}
+    model = _model(3, stats)
+    with torch.no_grad():
+        out = model(b, scale_output=True).local_stress
+    P = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    st = {k: torch.tensor(v) for k, v in stats.items()}
+    ref = O.epd_forward(P, st, b.pos.cpu(), b.mean_stress.cpu(), b.nodes_types.cpu(), b.edge_index.cpu(),
+                        b.edge_attr.cpu(), 3, scale_output=True)
+    assert rel(out, ref) < OUT_TOL

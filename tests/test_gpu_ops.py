@@ -1,0 +1,236 @@
+"""Op-level parity of every HIP kernel against a float64 torch restatement of the
+same op (SURVEY §4 tier T1).  Inputs are seeded; sizes include ragged tails
+(rows not a multiple of the 32-row wave tile), zero in-degree nodes and
+repeated indices."""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+L = 128
+TOL = 2e-6   # relative L2 vs float64 for a single fp32 op
+
+
+@pytest.fixture(scope="module")
+def env():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from pdg.lib import lib, stream_handle
+    from pdg import engine
+    torch.manual_seed(0)
+    return lib, stream_handle, engine
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def rnd(*shape, scale=1.0):
+    return (torch.randn(*shape, dtype=torch.float64) * scale).float().cuda()
+
+
+def lin(out, inp):
+    m = torch.nn.Linear(inp, out)
+    return m.weight.detach().float().cuda().contiguous(), (m.bias.detach().float().cuda() + 0.1).contiguous()
+
+
+def stat_from(buf):
+    raw = buf.cpu().numpy().tobytes()
+    import struct
+    mean, den, rstd, sd, mean_d, std_d, count = struct.unpack("ffffddd", raw[:40])
+    return dict(mean=mean, den=den, rstd=rstd, std=sd, mean_d=mean_d, std_d=std_d, count=count)
+
+
+def finalize(lib, s, part, nparts, count):
+    st = torch.zeros(40, dtype=torch.uint8, device="cuda")
+    lib.pdg_ln_finalize(part.data_ptr(), nparts, float(count), st.data_ptr(), s)
+    return st
+
+
+def ln_ref(a, g, b, eps=1e-5):
+    a = a.double()
+    x = a - a.mean()
+    return x / (x.std(unbiased=False) + eps) * g.double() + b.double()
+
+
+@pytest.mark.parametrize("M", [1, 33, 1000, 4099])
+def test_mlp2_fwd_and_ln_stats(env, M):
+    lib, sh, _ = env
+    s = sh()
+    a1 = torch.relu(rnd(M, L))
+    W, b = lin(L, L)
+    a2 = torch.empty(M, L, device="cuda")
+    part = torch.empty(4096, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    lib.pdg_mlp2_fwd(M, a1.data_ptr(), W.data_ptr(), b.data_ptr(), a2.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
+    ref = torch.relu(a1.double() @ W.double().T + b.double())
+    assert rel(a2, ref) < TOL
+    st = stat_from(finalize(lib, s, part, n.value, M * L))
+    assert abs(st["mean_d"] - float(ref.mean())) <= 1e-6 * abs(float(ref.mean())) + 1e-9
+    assert abs(st["std_d"] - float(ref.std(unbiased=False))) <= 1e-6 * float(ref.std(unbiased=False))
+
+
+@pytest.mark.parametrize("M,IN", [(77, 6), (1025, 1)])
+def test_encoder_fwd(env, M, IN):
+    lib, sh, _ = env
+    s = sh()
+    x = rnd(M, IN)
+    W0, b0 = lin(L, IN)
+    W2, b2 = lin(L, L)
+    a1, a2 = torch.empty(M, L, device="cuda"), torch.empty(M, L, device="cuda")
+    part = torch.empty(4096, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    lib.pdg_encoder_fwd(M, IN, x.data_ptr(), W0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                        a1.data_ptr(), a2.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
+    r1 = torch.relu(x.double() @ W0.double().T + b0.double())
+    r2 = torch.relu(r1 @ W2.double().T + b2.double())
+    assert rel(a1, r1) < TOL and rel(a2, r2) < TOL
+
+
+def _csr(N, E, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    dst = torch.randint(0, N, (E,), generator=g)
+    dst[: N // 7] = 0            # one heavy node
+    src = torch.randint(0, N, (E,), generator=g)
+    key = dst * N + src
+    order = torch.sort(key, stable=True).indices
+    src, dst = src[order], dst[order]
+    rp = torch.zeros(N + 1, dtype=torch.int64)
+    rp[1:] = torch.cumsum(torch.bincount(dst, minlength=N), 0)
+    return src, dst, rp
+
+
+@pytest.mark.parametrize("N,E", [(50, 300), (1031, 6000)])
+def test_segment_sum_with_layernorm(env, N, E):
+    lib, sh, _ = env
+    s = sh()
+    src, dst, rp = _csr(N, E)
+    rows = torch.relu(rnd(E, L))
+    g, b = rnd(L) + 1.0, rnd(L)
+    part = torch.empty(4096, dtype=torch.float64, device="cuda")
+    # stats via the library (pdg_mlp2_fwd path is tested above); use torch values packed as a struct
+    st = torch.zeros(40, dtype=torch.uint8, device="cuda")
+    import struct
+    r64 = rows.double()
+    mean, sd = float(r64.mean()), float(r64.std(unbiased=False))
+    den = float(torch.tensor(sd, dtype=torch.float32) + 1e-5)
+    st.copy_(torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, E * L)),
+                              dtype=torch.uint8).cuda())
+    out = torch.empty(N, L, device="cuda")
+    rp_d = rp.int().cuda()
+    lib.pdg_segment_sum(N, rp_d.data_ptr(), rows.data_ptr(), st.data_ptr(), g.data_ptr(), b.data_ptr(),
+                        out.data_ptr(), s)
+    normed = (r64.cpu() - mean) / den * g.double().cpu() + b.double().cpu()
+    ref = torch.zeros(N, L, dtype=torch.float64).index_add_(0, dst, normed)
+    assert rel(out, ref) < TOL
+    # zero in-degree nodes are exactly zero
+    deg0 = (rp[1:] - rp[:-1]) == 0
+    if deg0.any():
+        assert float(out.cpu()[deg0].abs().max()) == 0.0
+    raw = torch.empty(N, L, device="cuda")
+    lib.pdg_segment_sum(N, rp_d.data_ptr(), rows.data_ptr(), None, None, None, raw.data_ptr(), s)
+    assert rel(raw, torch.zeros(N, L, dtype=torch.float64).index_add_(0, dst, r64.cpu())) < TOL
+
+
+@pytest.mark.parametrize("M", [64, 1000, 3001])
+def test_wgrad_accum_reduce(env, M):
+    lib, sh, _ = env
+    s = sh()
+    G, X, G2, X2 = rnd(M, L), rnd(M, L), rnd(M, L), rnd(M, L)
+    ns = 37
+    slabs = torch.zeros(ns, L * L + L, device="cuda")
+    lib.pdg_wgrad_accum(M, G.data_ptr(), X.data_ptr(), G2.data_ptr(), X2.data_ptr(), slabs.data_ptr(), ns, s)
+    lib.pdg_wgrad_accum(M, G.data_ptr(), X.data_ptr(), None, None, slabs.data_ptr(), ns, s)   # accumulates
+    gW = torch.zeros(L, 3 * L, device="cuda")
+    gb = torch.zeros(L, device="cuda")
+    lib.pdg_wgrad_reduce(slabs.data_ptr(), ns, gW.data_ptr(), 3 * L, L, gb.data_ptr(), s)
+    ref = 2 * G.double().T @ X.double() + G2.double().T @ X2.double()
+    assert rel(gW[:, L:2 * L], ref) < 1e-5
+    assert float(gW[:, :L].abs().max()) == 0 and float(gW[:, 2 * L:].abs().max()) == 0
+    assert rel(gb, 2 * G.double().sum(0) + G2.double().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("K,transpose", [(1, 0), (3, 1), (6, 0)])
+def test_wgrad_narrow(env, K, transpose):
+    lib, sh, _ = env
+    s = sh()
+    M = 2049
+    wide, narrow = rnd(M, L), rnd(M, K)
+    part = torch.empty(4096 * (L * 6 + L + 6), dtype=torch.float64, device="cuda")
+    gW = torch.zeros(L * K, device="cuda")
+    gbw, gbn = torch.zeros(L, device="cuda"), torch.zeros(K, device="cuda")
+    lib.pdg_wgrad_narrow(M, wide.data_ptr(), narrow.data_ptr(), K, transpose, part.data_ptr(), gW.data_ptr(),
+                         gbw.data_ptr(), gbn.data_ptr(), s)
+    T = wide.double().T @ narrow.double()   # (128, K)
+    ref = T.T.reshape(-1) if transpose else T.reshape(-1)
+    assert rel(gW, ref) < 1e-6
+    assert rel(gbw, wide.double().sum(0)) < 1e-6 and rel(gbn, narrow.double().sum(0)) < 1e-6
+
+
+def test_transpose_strided(env):
+    lib, sh, _ = env
+    W = rnd(L, 3 * L)
+    out = torch.empty(L, L, device="cuda")
+    lib.pdg_transpose(L, L, 3 * L, W.data_ptr() + 4 * 2 * L, out.data_ptr(), sh())
+    assert torch.equal(out.cpu(), W[:, 2 * L:].T.contiguous().cpu())
+
+
+def test_pq_scatter_bwd(env):
+    lib, sh, _ = env
+    s = sh()
+    N, E = 300, 2500
+    src, dst, rp = _csr(N, E, seed=3)
+    key2 = src * N + dst
+    perm_src = torch.sort(key2, stable=True).indices
+    rps = torch.zeros(N + 1, dtype=torch.int64)
+    rps[1:] = torch.cumsum(torch.bincount(src, minlength=N), 0)
+    gm, ge = rnd(E, L), rnd(E, L)
+    gP, gQ = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
+    # keep every device array referenced until the kernel has run (no temporaries)
+    rp_d, rps_d, perm_d = rp.int().cuda(), rps.int().cuda(), perm_src.int().cuda()
+    lib.pdg_pq_scatter_bwd(N, rp_d.data_ptr(), rps_d.data_ptr(), perm_d.data_ptr(), gm.data_ptr(), ge.data_ptr(),
+                           gP.data_ptr(), gQ.data_ptr(), s)
+    z = lambda: torch.zeros(N, L, dtype=torch.float64)
+    refP = z().index_add_(0, dst, gm.double().cpu()).index_add_(0, src, ge.double().cpu())
+    refQ = z().index_add_(0, src, gm.double().cpu()).index_add_(0, dst, ge.double().cpu())
+    assert rel(gP, refP) < TOL and rel(gQ, refQ) < TOL
+
+
+def test_ln_colsum_and_mlp2_bwd_vs_autograd(env):
+    """LayerNorm(graph) -> relu -> Linear backward of one MLP tail, against torch autograd in fp64."""
+    lib, sh, _ = env
+    s = sh()
+    M = 1500
+    a1 = torch.relu(rnd(M, L))
+    W, b = lin(L, L)
+    g, beta = (rnd(L) * 0.3 + 1.0), rnd(L) * 0.1
+    a2 = torch.empty(M, L, device="cuda")
+    part = torch.empty(4096 * 256, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    lib.pdg_mlp2_fwd(M, a1.data_ptr(), W.data_ptr(), b.data_ptr(), a2.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
+    st = finalize(lib, s, part, n.value, M * L)
+    gy = rnd(M, L)
+    lib.pdg_ln_colsum(M, gy.data_ptr(), None, a2.data_ptr(), st.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
+    gg, gb = torch.zeros(L, device="cuda"), torch.zeros(L, device="cuda")
+    lb = torch.zeros(24, dtype=torch.uint8, device="cuda")
+    lib.pdg_ln_colsum_finalize(part.data_ptr(), n.value, g.data_ptr(), st.data_ptr(), gg.data_ptr(), gb.data_ptr(),
+                               lb.data_ptr(), s)
+    WT = W.T.contiguous()
+    gz2, gz1 = torch.empty(M, L, device="cuda"), torch.empty(M, L, device="cuda")
+    lib.pdg_mlp2_bwd(M, gy.data_ptr(), None, a2.data_ptr(), a1.data_ptr(), st.data_ptr(), lb.data_ptr(),
+                     g.data_ptr(), WT.data_ptr(), gz2.data_ptr(), gz1.data_ptr(), s)
+    # reference
+    a1d = a1.double().cpu().requires_grad_(True)
+    Wd, bd = W.double().cpu(), b.double().cpu()
+    gd, betad = g.double().cpu().requires_grad_(True), beta.double().cpu().requires_grad_(True)
+    z2 = (a1d @ Wd.T + bd)
+    z2.retain_grad()
+    out = ln_ref(torch.relu(z2), gd, betad)
+    out.backward(gy.double().cpu())
+    assert rel(gg, gd.grad) < 1e-5 and rel(gb, betad.grad) < 1e-5
+    assert rel(gz2, z2.grad) < 1e-5
+    assert rel(gz1, (z2.grad @ Wd) * (a1d.detach() > 0)) < 1e-5
