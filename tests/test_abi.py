@@ -1,0 +1,75 @@
+"""CPU-side checks of the drop-in boundary: the C ABI library loads, exports every
+entry point include/pdivgnn.h declares, and the ctypes signatures match the header."""
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HEADER = ROOT / "include" / "pdivgnn.h"
+
+
+def _decls():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(?:int|const char\*)\s+(pdg_\w+)\s*\(([^)]*)\)\s*;", text, re.S):
+        args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        out[m.group(1)] = args
+    return out
+
+
+def test_header_declares_entry_points():
+    d = _decls()
+    assert len(d) >= 30
+    for name in ("pdg_edge_fwd", "pdg_edge_bwd", "pdg_segment_sum", "pdg_div_fwd", "pdg_nmse_fwd", "pdg_adam"):
+        assert name in d
+
+
+def test_library_exports_every_declared_symbol():
+    from pdg.lib import lib
+    dll = lib.load()
+    for name in _decls():
+        assert hasattr(dll, name), name
+
+
+def test_ctypes_signatures_match_header():
+    from pdg.lib import SIGNATURES
+    d = _decls()
+    assert set(SIGNATURES) == set(d), set(SIGNATURES) ^ set(d)
+    for name, args in d.items():
+        assert len(SIGNATURES[name]) == len(args), (name, len(SIGNATURES[name]), len(args))
+
+
+def test_library_reports_errors_without_gpu():
+    """Argument validation happens before any HIP call, so it runs on a CPU-only host."""
+    from pdg.lib import PdgError, lib
+    with pytest.raises(PdgError, match="rows must be > 0"):
+        lib.pdg_mlp2_fwd(0, None, None, None, None, None, None, None)
+    assert lib.pdg_max_blocks() >= 256
+
+
+def test_struct_sizes_match_header():
+    import ctypes
+    from pdg.lib import LN_BWD_BYTES, LN_STAT_BYTES
+
+    class Stat(ctypes.Structure):
+        _fields_ = [("mean", ctypes.c_float), ("den", ctypes.c_float), ("rstd", ctypes.c_float),
+                    ("std_", ctypes.c_float), ("mean_d", ctypes.c_double), ("std_d", ctypes.c_double),
+                    ("count", ctypes.c_double)]
+
+    class Bwd(ctypes.Structure):
+        _fields_ = [("c1", ctypes.c_float), ("c2", ctypes.c_float), ("S1", ctypes.c_double), ("S2", ctypes.c_double)]
+
+    assert ctypes.sizeof(Stat) == LN_STAT_BYTES and ctypes.sizeof(Bwd) == LN_BWD_BYTES
+
+
+def test_model_refuses_cpu_tensors():
+    import torch
+    from gnn_local_stress.models import EncodeProcessDecode
+    from pdg import graph, meshgen
+    m = EncodeProcessDecode(1, 2, latent_size=128, input_nodes_features_size=6, output_nodes_features_size=3)
+    b = graph.Batch.from_data_list([graph.sample_to_data(meshgen.hole_plate(5))])
+    with pytest.raises(RuntimeError, match="HIP"):
+        m(b)
+    with pytest.raises(ValueError):
+        EncodeProcessDecode(1, 2, latent_size=64, input_nodes_features_size=6, output_nodes_features_size=3)
