@@ -166,7 +166,7 @@ def main():
     rooflines = {
         "edge_fwd": ("mfma", flop_edge, PEAK_FP32_MFMA, "TFLOP/s"),
         "edge_bwd": ("mfma", flop_edge, PEAK_FP32_MFMA, "TFLOP/s"),
-        "wgrad_W2": ("mfma", 2 * E * 2 * L * L, PEAK_FP32_MFMA, "TFLOP/s"),
+        "wgrad_W2": ("mfma", cfg["steps"] * 2 * E * 2 * L * L, PEAK_FP32_MFMA, "TFLOP/s"),
         "segment_sum": ("hbm", 512 * E + 4 * (N + 1) + 512 * N, PEAK_HBM, "GB/s"),
         "pq_scatter_bwd": ("hbm", 2 * 512 * E + 4 * E + 8 * (N + 1) + 2 * 512 * N, PEAK_HBM, "GB/s"),
     }

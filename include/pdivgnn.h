@@ -172,6 +172,13 @@ int pdg_wgrad_accum(int rows, const float* G, const float* X, const float* G2, c
 /* grad_W[o*ld + col0 + i] += sum over slabs; grad_b[o] += (if grad_b) sum over slabs. */
 int pdg_wgrad_reduce(const float* slabs, int nslabs, float* grad_W, int ld, int col0,
                      float* grad_b, void* stream);
+/* Weight gradient of a 128x128 Linear over a list of row segments (all message-passing steps
+ * and both edge_net evaluations in one pass): slab[b] = per-block partial of
+ * sum_seg sum_k G_seg[k]^T X_seg[k] and of sum G_seg[k] (written, not accumulated);
+ * reduce with pdg_wgrad_reduce.  g_ptrs/x_ptrs/rows are HOST arrays of nseg <= PDG_MAX_SEGS entries. */
+#define PDG_MAX_SEGS 32
+int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
+                       float* slabs, int nslabs, void* stream);
 /* Narrow weight gradient: T[c][i] = sum_k Wide[k][c] Narrow[k][i] (c < 128, i < k_narrow <= 8),
  * sums sum_k Wide[k][c] and sum_k Narrow[k][i]; added into grad arrays:
  * transpose == 0: grad_W[c*k_narrow + i] (shape 128 x k), else grad_W[i*128 + c] (k x 128);

@@ -145,20 +145,39 @@ extern "C" int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, co
   return PDG_OK;
 }
 
-__global__ void ln_colsum_finalize_kernel(const double* __restrict__ part, int n, const float* __restrict__ g,
-                                          const pdg_ln_stat* __restrict__ stp, float* __restrict__ grad_g,
-                                          float* __restrict__ grad_b, pdg_ln_bwd* __restrict__ out) {
-  __shared__ double red[2 * 16];
-  const int c = threadIdx.x;  // 128 threads, one channel each
-  double sg = 0, sx = 0;
-  for (int b = 0; b < n; ++b) {
-    sg += part[(size_t)b * 256 + c];
-    sx += part[(size_t)b * 256 + 128 + c];
+// 1024 threads: column c (of 256: 128 sum-gy, 128 sum-gy*xhat) by 4 threads, each
+// summing every 4th block partial; the 4 are combined in a fixed order.
+__global__ __launch_bounds__(1024) void ln_colsum_finalize_kernel(const double* __restrict__ part, int n,
+                                                                  const float* __restrict__ g,
+                                                                  const pdg_ln_stat* __restrict__ stp,
+                                                                  float* __restrict__ grad_g,
+                                                                  float* __restrict__ grad_b,
+                                                                  pdg_ln_bwd* __restrict__ out) {
+  __shared__ double red[4][256];
+  __shared__ double red2[2 * 16];
+  const int col = threadIdx.x & 255, q = threadIdx.x >> 8;
+  double s0 = 0, s1_ = 0, s2_ = 0, s3 = 0;
+  int b = q;
+  for (; b + 12 < n; b += 16) {
+    s0 += part[(size_t)b * 256 + col];
+    s1_ += part[(size_t)(b + 4) * 256 + col];
+    s2_ += part[(size_t)(b + 8) * 256 + col];
+    s3 += part[(size_t)(b + 12) * 256 + col];
   }
-  if (grad_b) grad_b[c] += (float)sg;
-  if (grad_g) grad_g[c] += (float)sx;
-  double s1 = (double)g[c] * sg, s2 = (double)g[c] * sx;
-  block_sum2(s1, s2, red);
+  for (; b < n; b += 4) s0 += part[(size_t)b * 256 + col];
+  red[q][col] = (s0 + s1_) + (s2_ + s3);
+  __syncthreads();
+  double s1 = 0, s2 = 0;
+  if (threadIdx.x < 128) {
+    const int c = threadIdx.x;
+    const double sg = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    const double sx = (red[0][128 + c] + red[1][128 + c]) + (red[2][128 + c] + red[3][128 + c]);
+    if (grad_b) grad_b[c] += (float)sg;
+    if (grad_g) grad_g[c] += (float)sx;
+    s1 = (double)g[c] * sg;
+    s2 = (double)g[c] * sx;
+  }
+  block_sum2(s1, s2, red2);
   if (threadIdx.x == 0) {
     const double M = stp->count;
     const double sd = stp->std_d;
@@ -175,7 +194,7 @@ extern "C" int pdg_ln_colsum_finalize(const double* partials, int nparts, const 
                                       const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
                                       void* stream) {
   PDG_CHECK_ARG(nparts > 0, "pdg_ln_colsum_finalize: no partials");
-  hipLaunchKernelGGL(ln_colsum_finalize_kernel, dim3(1), dim3(128), 0, (hipStream_t)stream, partials, nparts, ln_g,
+  hipLaunchKernelGGL(ln_colsum_finalize_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, partials, nparts, ln_g,
                      st, grad_g, grad_b, out);
   PDG_CHECK_LAUNCH("pdg_ln_colsum_finalize");
   return PDG_OK;

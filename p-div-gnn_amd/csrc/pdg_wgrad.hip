@@ -98,8 +98,16 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int n, floa
                                     int col0, float* __restrict__ gb) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= SLAB) return;
-  float s = 0.f;
-  for (int b = 0; b < n; ++b) s += slabs[(size_t)b * SLAB + e];
+  float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
+  int b = 0;
+  for (; b + 4 <= n; b += 4) {
+    p0 += slabs[(size_t)b * SLAB + e];
+    p1 += slabs[(size_t)(b + 1) * SLAB + e];
+    p2 += slabs[(size_t)(b + 2) * SLAB + e];
+    p3 += slabs[(size_t)(b + 3) * SLAB + e];
+  }
+  for (; b < n; ++b) p0 += slabs[(size_t)b * SLAB + e];
+  const float s = (p0 + p1) + (p2 + p3);
   if (e < L * L) {
     const int o = e / L, i = e % L;
     gW[(size_t)o * ld + col0 + i] += s;
@@ -205,5 +213,172 @@ extern "C" int pdg_wgrad_narrow(int rows, const float* wide, const float* narrow
   hipLaunchKernelGGL(wgrad_narrow_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, partials, grid,
                      k_narrow, transpose, grad_W, grad_b_wide, grad_b_narrow);
   PDG_CHECK_LAUNCH("pdg_wgrad_narrow(finalize)");
+  return PDG_OK;
+}
+
+// ============================================================================ segmented, LDS-staged wgrad
+// One launch per weight and backward: the row segments of every message-passing
+// step (and both edge_net evaluations) form one virtual K = sum(rows) reduction.
+// Block b owns a contiguous range of virtual rows, staged 32 rows at a time into
+// LDS (G and X tiles, double buffered, coalesced 16-byte loads), and keeps the
+// whole 128x128 partial in registers: wave w owns the 64x64 quadrant
+// (o in 64*(w>>1) + [0,64), i in 64*(w&1) + [0,64)) as 2x2 MFMA 32x32 tiles.
+struct WgradSegs {
+  const float* G[PDG_MAX_SEGS];
+  const float* X[PDG_MAX_SEGS];
+  long start[PDG_MAX_SEGS + 1];
+  int nseg;
+};
+
+constexpr int WG_ROWS = 32;
+constexpr int WG_TILE = WG_ROWS * L;   // floats per staged tile
+
+// Segment table copied to LDS once per block (the kernel-argument copy would be
+// read with dependent per-lane global loads).  Each thread stages rows
+// r_i = base + (tid >> 5) + 8 i (i < 4) of every 32-row tile and tracks the
+// segment of each of them incrementally (tiles advance monotonically).
+struct WgTable {
+  long start[PDG_MAX_SEGS + 1];
+  const float* G[PDG_MAX_SEGS];
+  const float* X[PDG_MAX_SEGS];
+};
+constexpr int WG_TABLE_FLOATS = (sizeof(WgTable) + 15) / 16 * 4;
+
+__device__ __forceinline__ void wg_load(const WgTable* tb, int nseg, long base, long r1, int (&seg)[4],
+                                        f32x4 (&gr)[4], f32x4 (&xr)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    const int row = idx >> 5, c4 = idx & 31;
+    const long vr = base + row;
+    if (vr < r1) {
+      while (seg[i] + 1 < nseg && vr >= tb->start[seg[i] + 1]) ++seg[i];
+      const long r = vr - tb->start[seg[i]];
+      gr[i] = reinterpret_cast<const f32x4*>(tb->G[seg[i]] + r * L)[c4];
+      xr[i] = reinterpret_cast<const f32x4*>(tb->X[seg[i]] + r * L)[c4];
+    } else {
+      gr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+__device__ __forceinline__ void wg_store(float* gs, float* xs, const f32x4 (&gr)[4], const f32x4 (&xr)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = threadIdx.x + 256 * i;
+    reinterpret_cast<f32x4*>(gs)[idx] = gr[i];
+    reinterpret_cast<f32x4*>(xs)[idx] = xr[i];
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void wgrad_segments_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];   // [table | 2 x (G tile | X tile)]
+  WgTable* tb = reinterpret_cast<WgTable*>(smem);
+  float* lds = smem + WG_TABLE_FLOATS;
+  const int nseg = sg.nseg;
+  for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
+  for (int i = threadIdx.x; i < PDG_MAX_SEGS; i += blockDim.x) {
+    tb->G[i] = sg.G[i];
+    tb->X[i] = sg.X[i];
+  }
+  __syncthreads();
+  const int nb = gridDim.x;
+  long per = (total + nb - 1) / nb;
+  per = (per + WG_ROWS - 1) / WG_ROWS * WG_ROWS;
+  const long r0 = min(total, per * blockIdx.x), r1 = min(total, per * (blockIdx.x + 1));
+  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
+  const int ob = 64 * (w >> 1), ib = 64 * (w & 1);
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float bsum0 = 0.f, bsum1 = 0.f;
+  f32x4 gr[4], xr[4];
+  int seg[4];
+  {
+    // first segment of this block's range (binary search, once)
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (tb->start[mid] <= r0) lo = mid; else hi = mid;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) seg[i] = lo;
+  }
+  int buf = 0;
+  if (r0 < r1) {
+    wg_load(tb, nseg, r0, r1, seg, gr, xr);
+    wg_store(lds, lds + WG_TILE, gr, xr);
+  }
+  __syncthreads();
+  for (long base = r0; base < r1; base += WG_ROWS) {
+    const bool more = base + WG_ROWS < r1;
+    if (more) wg_load(tb, nseg, base + WG_ROWS, r1, seg, gr, xr);   // next tile in flight during the MFMAs
+    const float* gs = lds + buf * 2 * WG_TILE;
+    const float* xs = gs + WG_TILE;
+#pragma unroll
+    for (int s = 0; s < WG_ROWS / 2; ++s) {
+      const int row = 2 * s + h;
+      const float a0 = gs[row * L + ob + c], a1 = gs[row * L + ob + 32 + c];
+      const float b0 = xs[row * L + ib + c], b1 = xs[row * L + ib + 32 + c];
+      bsum0 += a0;
+      bsum1 += a1;
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      float* ngs = lds + (buf ^ 1) * 2 * WG_TILE;
+      wg_store(ngs, ngs + WG_TILE, gr, xr);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  float* slab = slabs + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int i = ib + 32 * b + c;
+        slab[o * L + i] = acc[a][b][r];
+      }
+  if ((w & 1) == 0) {   // bias sums from the waves whose quadrant starts at input 0
+    const float o0 = __shfl_xor(bsum0, 32), o1 = __shfl_xor(bsum1, 32);
+    if (h == 0) {
+      slab[L * L + ob + c] = bsum0 + o0;
+      slab[L * L + ob + 32 + c] = bsum1 + o1;
+    }
+  }
+}
+
+extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
+                                  float* slabs, int nslabs, void* stream) {
+  PDG_CHECK_ARG(nseg > 0 && nseg <= PDG_MAX_SEGS, "pdg_wgrad_segments: 1..%d segments", PDG_MAX_SEGS);
+  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS, "pdg_wgrad_segments: bad nslabs");
+  WgradSegs sg;
+  long tot = 0;
+  for (int i = 0; i < nseg; ++i) {
+    PDG_CHECK_ARG(rows[i] >= 0, "pdg_wgrad_segments: negative rows");
+    PDG_CHECK_ARG(PDG_ALIGNED(g_ptrs[i]) && PDG_ALIGNED(x_ptrs[i]), "pdg_wgrad_segments: misaligned pointer");
+    sg.G[i] = g_ptrs[i];
+    sg.X[i] = x_ptrs[i];
+    sg.start[i] = tot;
+    tot += rows[i];
+  }
+  sg.start[nseg] = tot;
+  for (int i = nseg + 1; i <= PDG_MAX_SEGS; ++i) sg.start[i] = tot;
+  sg.nseg = nseg;
+  PDG_CHECK_ARG(tot > 0, "pdg_wgrad_segments: no rows");
+  hipLaunchKernelGGL(wgrad_segments_kernel, dim3(nslabs), dim3(256), (WG_TABLE_FLOATS + 4 * WG_TILE) * sizeof(float),
+                     (hipStream_t)stream, sg, tot, slabs);
+  PDG_CHECK_LAUNCH("pdg_wgrad_segments");
   return PDG_OK;
 }

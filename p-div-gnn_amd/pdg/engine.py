@@ -95,7 +95,7 @@ class EPDEngine:
         self._part_col = torch.empty(self.max_blocks * 256, **f64)
         self._part_narrow = torch.empty(self.max_blocks * (L * 6 + L + 6), **f64)
         self._nparts = ctypes.c_int(0)
-        self._nslabs = 256
+        self._nslabs = 512
         # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
         self.timed: dict | None = None
 
@@ -223,7 +223,12 @@ class EPDEngine:
         return out
 
     def backward(self, P: dict, ctx: FwdCtx, gy: torch.Tensor, G: dict) -> None:
-        """Accumulate d(loss)/d(param) into G[name] (fp32, same shapes as P)."""
+        """Accumulate d(loss)/d(param) into G[name] (fp32, same shapes as P).
+
+        The input-gradient chain runs step by step (reverse order); the weight
+        gradients of the shared 128x128 blocks are deferred: every step's row
+        segments (G, X pairs, kept resident in HBM) are reduced at the end in
+        one segmented MFMA pass per weight (pdg_wgrad_segments)."""
         s = stream_handle(self.device)
         plan = ctx.plan
         N, E = plan.n_nodes, plan.n_edges
@@ -231,13 +236,7 @@ class EPDEngine:
         T = self.transposed(P)
         st = ctx.stats
         lb = _StatBuf(4, LN_BWD_BYTES, self.device)
-        ns = self._nslabs
-        slab_names = ["W2", "Wc", "Wa", "Wb", "Wn2", "Wn1a", "Wn1b", "d1", "ne2", "ee2"]
-        slabs_all = torch.zeros(len(slab_names), ns, L * L + L, dtype=torch.float32, device=self.device)
-        slabs = {k: slabs_all[i] for i, k in enumerate(slab_names)}
-
-        def wacc(rows, Gt, X, key, G2=None, X2=None):
-            lib.pdg_wgrad_accum(rows, _p(Gt), _p(X), _p(G2), _p(X2), _p(slabs[key]), ns, s)
+        segs: dict[str, list] = {k: [] for k in ("W2", "Wc", "Wa", "Wb", "Wn2", "Wn1a", "Wn1b", "d1", "ne2", "ee2")}
 
         def colsum(rows, gy_rows, gidx, a2, st_ptr, gname, bname, lb_ptr):
             lib.pdg_ln_colsum(rows, _p(gy_rows), _p(gidx), _p(a2), st_ptr, _p(self._part_col), np_, s)
@@ -253,23 +252,21 @@ class EPDEngine:
                             _p(gx), s)
         lib.pdg_wgrad_narrow(N, _p(ctx.a1d), _p(gy), 3, 1, _p(self._part_narrow), _p(G["node_decoder.2.weight"]),
                              None, _p(G["node_decoder.2.bias"]), s)
-        wacc(N, gz1d, ctx.x_S, "d1")
+        segs["d1"].append((gz1d, ctx.x_S, N))
 
         ge_next = torch.zeros(E, L, dtype=torch.float32, device=self.device)
-        gz2n, gz1n, gaggr, gx_part = (self._empty(N, L) for _ in range(4))
-        gP, gQ, gx_t = (self._empty(N, L) for _ in range(3))
-        gz2m, gz1m, gz2e, gz1e, gC, ge_out = (self._empty(E, L) for _ in range(6))
+        gaggr, gx_part, gx_t = (self._empty(N, L) for _ in range(3))
+        gz1m, gz1e, ge_out = (self._empty(E, L) for _ in range(3))
         gx_next = gx
         for t in reversed(range(ctx.steps)):
             d = ctx.per_step[t]
+            gz2n, gz1n, gP, gQ = (self._empty(N, L) for _ in range(4))
+            gz2m, gz2e, gC = (self._empty(E, L) for _ in range(3))
             # node_net tail: n_t = LN_n(a2n_t), gy = gx_next   (x_{t+1} = n_t + x_t)
             colsum(N, gx_next, None, d["a2n"], st[d["i_n"]], "processor.node_net.4.weight",
                    "processor.node_net.4.bias", lb[0])
             lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], lb[0],
                              _p(P["processor.node_net.4.weight"]), _p(T["Wn2T"]), _p(gz2n), _p(gz1n), s)
-            wacc(N, gz2n, d["a1n"], "Wn2")
-            wacc(N, gz1n, d["aggr"], "Wn1a")
-            wacc(N, gz1n, d["x"], "Wn1b")
             lib.pdg_gemm_dual(N, _p(gz1n), _p(T["Wn1aT"]), _p(T["Wn1bT"]), None, _p(gx_next), _p(gaggr),
                               _p(gx_part), s)
             # edge_net LayerNorm sums: message (gy = gaggr[dst]) and edge update (gy = ge_next)
@@ -277,17 +274,20 @@ class EPDEngine:
                    "processor.edge_net.4.bias", lb[1])
             colsum(E, ge_next, None, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
                    "processor.edge_net.4.bias", lb[2])
-            self._t("edge_bwd", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr), _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]),
-                             _p(d["a1e"]), st[d["i_m"]], st[d["i_e"]], lb[1], lb[2],
-                             _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]), _p(gz2m), _p(gz1m),
-                             _p(gz2e), _p(gz1e), _p(gC), _p(ge_out), s)
-            self._t("wgrad_W2", wacc, E, gz2m, d["a1m"], "W2", gz2e, d["a1e"])
-            wacc(E, gC, d["e"], "Wc")
-            self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src), _p(plan.perm_src), _p(gz1m),
-                                   _p(gz1e), _p(gP), _p(gQ), s)
-            wacc(N, gP, d["x"], "Wa")
-            wacc(N, gQ, d["x"], "Wb")
+            self._t("edge_bwd", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr), _p(ge_next), _p(d["a2m"]),
+                    _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]], st[d["i_e"]], lb[1], lb[2],
+                    _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]), _p(gz2m), _p(gz1m),
+                    _p(gz2e), _p(gz1e), _p(gC), _p(ge_out), s)
+            self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
+                    _p(plan.perm_src), _p(gz1m), _p(gz1e), _p(gP), _p(gQ), s)
             lib.pdg_gemm_sum2(N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part), _p(gx_t), s)
+            segs["W2"] += [(gz2m, d["a1m"], E), (gz2e, d["a1e"], E)]
+            segs["Wc"].append((gC, d["e"], E))
+            segs["Wa"].append((gP, d["x"], N))
+            segs["Wb"].append((gQ, d["x"], N))
+            segs["Wn2"].append((gz2n, d["a1n"], N))
+            segs["Wn1a"].append((gz1n, d["aggr"], N))
+            segs["Wn1b"].append((gz1n, d["x"], N))
             gx_next, gx_t = gx_t, gx_next
             ge_next, ge_out = ge_out, ge_next
         # encoders
@@ -295,17 +295,17 @@ class EPDEngine:
         colsum(N, gx_next, None, ctx.a2_ne, st[0], "node_encoder.4.weight", "node_encoder.4.bias", lb[3])
         lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], lb[3],
                          _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), s)
-        wacc(N, gz2, ctx.a1_ne, "ne2")
+        segs["ne2"].append((gz2, ctx.a1_ne, N))
         lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
                              _p(G["node_encoder.0.bias"]), None, s)
         gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
         colsum(E, ge_next, None, ctx.a2_ee, st[1], "edge_encoder.4.weight", "edge_encoder.4.bias", lb[3])
         lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], lb[3],
                          _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), s)
-        wacc(E, gz2e_, ctx.a1_ee, "ee2")
+        segs["ee2"].append((gz2e_, ctx.a1_ee, E))
         lib.pdg_wgrad_narrow(E, _p(gz1e_), _p(ctx.e_in), 1, 0, _p(self._part_narrow), _p(G["edge_encoder.0.weight"]),
                              _p(G["edge_encoder.0.bias"]), None, s)
-        # slab reductions into the parameter gradients
+        # deferred weight gradients: one segmented pass + slab reduction per shared weight block
         red = [
             ("W2", "processor.edge_net.2.weight", L, 0, "processor.edge_net.2.bias"),
             ("Wc", "processor.edge_net.0.weight", 3 * L, 2 * L, "processor.edge_net.0.bias"),
@@ -318,5 +318,16 @@ class EPDEngine:
             ("ne2", "node_encoder.2.weight", L, 0, "node_encoder.2.bias"),
             ("ee2", "edge_encoder.2.weight", L, 0, "edge_encoder.2.bias"),
         ]
+        ns = self._nslabs
+        if getattr(self, "_slabs", None) is None or self._slabs.device != self.device:
+            self._slabs = torch.empty(ns, L * L + L, dtype=torch.float32, device=self.device)
         for key, wname, ld, col0, bname in red:
-            lib.pdg_wgrad_reduce(_p(slabs[key]), ns, _p(G[wname]), ld, col0, _p(G[bname]) if bname else None, s)
+            sl = segs[key]
+            for c0 in range(0, len(sl), 32):
+                chunk = sl[c0:c0 + 32]
+                n = len(chunk)
+                gp = (ctypes.c_void_p * n)(*[g.data_ptr() for g, _, _ in chunk])
+                xp = (ctypes.c_void_p * n)(*[x.data_ptr() for _, x, _ in chunk])
+                rw = (ctypes.c_int * n)(*[r for _, _, r in chunk])
+                self._t("wgrad_" + key, lib.pdg_wgrad_segments, n, gp, xp, rw, _p(self._slabs), ns, s)
+                lib.pdg_wgrad_reduce(_p(self._slabs), ns, _p(G[wname]), ld, col0, _p(G[bname]) if bname else None, s)

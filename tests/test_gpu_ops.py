@@ -234,3 +234,25 @@ def test_ln_colsum_and_mlp2_bwd_vs_autograd(env):
     assert rel(gg, gd.grad) < 1e-5 and rel(gb, betad.grad) < 1e-5
     assert rel(gz2, z2.grad) < 1e-5
     assert rel(gz1, (z2.grad @ Wd) * (a1d.detach() > 0)) < 1e-5
+
+
+def test_wgrad_segments_reduce(env):
+    """Segmented weight gradient: ragged segments (not multiples of the 32-row tile), one pass."""
+    lib, sh, _ = env
+    s = sh()
+    rows = [1, 33, 2000, 777, 4096, 5]
+    Gs = [rnd(r, L) for r in rows]
+    Xs = [rnd(r, L) for r in rows]
+    ns = 61
+    slabs = torch.empty(ns, L * L + L, device="cuda")
+    gp = (ctypes.c_void_p * len(rows))(*[g.data_ptr() for g in Gs])
+    xp = (ctypes.c_void_p * len(rows))(*[x.data_ptr() for x in Xs])
+    rw = (ctypes.c_int * len(rows))(*rows)
+    lib.pdg_wgrad_segments(len(rows), gp, xp, rw, slabs.data_ptr(), ns, s)
+    gW = torch.zeros(L, 2 * L, device="cuda")
+    gb = torch.zeros(L, device="cuda")
+    lib.pdg_wgrad_reduce(slabs.data_ptr(), ns, gW.data_ptr(), 2 * L, L, gb.data_ptr(), s)
+    ref = sum(g.double().T @ x.double() for g, x in zip(Gs, Xs))
+    assert rel(gW[:, L:], ref) < 1e-5
+    assert float(gW[:, :L].abs().max()) == 0
+    assert rel(gb, sum(g.double().sum(0) for g in Gs)) < 1e-5
