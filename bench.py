@@ -34,7 +34,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
-PEAK_HBM = 8.0e12           # MI355X HBM3E spec bandwidth
+PEAK_HBM = 8.0e12           # MI355X HBM3E spec bandwidth (same guide; 6.3 TB/s measured copy)
 L = 128
 
 CONFIGS = {
@@ -162,23 +162,36 @@ def main():
 
     kt = {k: sum(a.elapsed_time(b) for a, b in v) / max(len(v), 1) * 1e-3 for k, v in ev.items()}
     ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
-    flop_edge = E * 3 * 2 * L * L           # 3 (128x128) GEMMs per edge and launch, executed
-    rooflines = {
-        "edge_fwd": ("mfma", flop_edge, PEAK_FP32_MFMA, "TFLOP/s"),
-        "edge_bwd": ("mfma", flop_edge, PEAK_FP32_MFMA, "TFLOP/s"),
-        "wgrad_W2": ("mfma", cfg["steps"] * 2 * E * 2 * L * L, PEAK_FP32_MFMA, "TFLOP/s"),
-        "segment_sum": ("hbm", 512 * E + 4 * (N + 1) + 512 * N, PEAK_HBM, "GB/s"),
-        "pq_scatter_bwd": ("hbm", 2 * 512 * E + 4 * E + 8 * (N + 1) + 2 * 512 * N, PEAK_HBM, "GB/s"),
+    S = cfg["steps"]
+    # algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops and the bytes the
+    # kernel must read/write (inputs once, outputs once, int32 indices)
+    work = {
+        # 3 (128x128) GEMMs per edge; reads a2e_prev, e_prev, 4 gathered P/Q rows, src, dst;
+        # writes e_t, a1m, a2m, a1e, a2e
+        "edge_fwd": (E * 3 * 2 * L * L, E * (11 * 4 * L + 8)),
+        # 3 GEMMs per edge; reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst;
+        # writes gz2m, gz1m, gz2e, gz1e, gC, ge_out
+        "edge_bwd": (E * 3 * 2 * L * L, E * (12 * 4 * L + 4)),
+        # all steps' W2 segments: 2E rows per step of (G, X) 512-byte rows, one 64 KB slab per block
+        "wgrad_W2": (S * 2 * E * 2 * L * L, S * 2 * E * 2 * 4 * L + 512 * (L * L + L) * 4),
+        "segment_sum": (0, 4 * L * E + 4 * (N + 1) + 4 * L * N),
+        "pq_scatter_bwd": (0, 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
     }
 
     def roof(k):
-        bound, work, peak, unit = rooflines[k]
-        ach = work / kt[k]
-        scale = 1e12 if unit == "TFLOP/s" else 1e9
-        return {"kernel": k, "bound": bound, "achieved": round(ach / scale, 2), "peak": round(peak / scale, 1),
-                "unit": unit, "frac": round(ach / peak, 4), "traffic": None,
-                "work_per_launch": work, "avg_launch_ms": round(kt[k] * 1e3, 4),
-                "share_of_step": round(ktot[k] / el, 4)}
+        flops, nbytes = work[k]
+        t = kt[k]
+        f_mfma = flops / t / PEAK_FP32_MFMA
+        f_hbm = nbytes / t / PEAK_HBM
+        bound = "mfma" if f_mfma >= f_hbm else "hbm"
+        if bound == "mfma":
+            ach, peak, unit = flops / t / 1e12, PEAK_FP32_MFMA / 1e12, "TFLOP/s"
+        else:
+            ach, peak, unit = nbytes / t / 1e9, PEAK_HBM / 1e9, "GB/s"
+        return {"kernel": k, "bound": bound, "achieved": round(ach, 2), "peak": round(peak, 1), "unit": unit,
+                "frac": round(ach / peak, 4), "traffic": None, "flops_per_launch": flops,
+                "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4), "frac_hbm": round(f_hbm, 4),
+                "avg_launch_ms": round(t * 1e3, 4), "share_of_step": round(ktot[k] / el, 4)}
 
     dominant = max(["edge_fwd", "edge_bwd", "wgrad_W2"], key=lambda k: ktot[k])
     if rank == 0:

@@ -81,7 +81,9 @@ int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const 
                 const float* ln_b, const float* x_res, float* x_out, const float* W1,
                 float* P, float* Q, void* stream);
 
-/* Fused edge pass of one message-passing step (models.py:215-222, :233-238):
+/* Fused edge pass of one message-passing step (models.py:215-222, :233-238).
+ * with_edge_update == 0 skips the edge-update branch (the last step's e_S is never consumed,
+ * models.py:316): a1e/a2e/part_e unused and may be NULL.
  * e_t = LN(a2_prev) [+ e_res]; C = W1[:, 256:384] e_t + b1;
  * message:  a1m = relu(C + P[dst] + Q[src]), a2m = relu(W2 a1m + b2)
  * edge upd: a1e = relu(C + P[src] + Q[dst]), a2e = relu(W2 a1e + b2)
@@ -90,12 +92,13 @@ int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const
                  const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
                  const float* P, const float* Q, const float* W1, const float* b1,
                  const float* W2, const float* b2, float* a1m, float* a2m, float* a1e, float* a2e,
-                 double* part_m, double* part_e, int* nparts, void* stream);
+                 double* part_m, double* part_e, int with_edge_update, int* nparts, void* stream);
 
 /* PyG "add" aggregation (scatter_add_ at edge_index[1]) of LN-normalised rows:
- * out[v] = sum_{k in rowptr[v]..rowptr[v+1]} LN(rows[k]); st == NULL -> raw rows. */
+ * out[v] = sum_{k in rowptr[v]..rowptr[v+1]} LN(rows[k]); st == NULL -> raw rows.
+ * xhat_sum (nullable): sum_k (rows[k] - mean)/(std + eps), kept for the LayerNorm backward. */
 int pdg_segment_sum(int n_nodes, const int* rowptr, const float* rows, const pdg_ln_stat* st,
-                    const float* ln_g, const float* ln_b, float* out, void* stream);
+                    const float* ln_g, const float* ln_b, float* out, float* xhat_sum, void* stream);
 
 /* Processor.update first layer (models.py:240-243, :202-204):
  * a1n = relu(Wn1[:, 0:128] aggr + Wn1[:, 128:256] x + bn1). */
@@ -127,6 +130,12 @@ int pdg_decoder_bwd(int n_nodes, const float* gy, const float* a1d, const float*
 int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, const float* a2,
                   const pdg_ln_stat* st, double* partials, int* nparts, void* stream);
 
+/* Node-level form of pdg_ln_colsum for the message LayerNorm, whose upstream gradient is the
+ * gathered gaggr[dst]: sum_k gy = sum_v deg_v gaggr[v], sum_k gy*xhat = sum_v gaggr[v]*xhat_sum[v]
+ * (deg from rowptr, xhat_sum from pdg_segment_sum).  Same partial layout as pdg_ln_colsum. */
+int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* rowptr, const float* xhat_sum,
+                        double* partials, int* nparts, void* stream);
+
 /* Reduce colsum partials: grad_b += sum gy, grad_g += sum gy*xhat, and the call's
  * backward scalars (S1 = sum g*gy, S2 = sum g*gy*xhat). */
 int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g,
@@ -149,7 +158,9 @@ int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const float* W0T
 
 /* Fused edge backward of one step: both edge_net evaluations' LN/relu/Linear2 backward
  * (message: gy = gaggr[dst]; edge update: gy = ge_next), gC = gz1m + gz1e,
- * ge_out = ge_next + WcT gC.  Writes gz2m, gz1m, gz2e, gz1e, gC, ge_out. */
+ * ge_out = ge_next + WcT gC.  Writes gz2m, gz1m, gz2e, gz1e, gC, ge_out.
+ * ge_next == NULL: the edge-update branch had no consumer (last step): gz2e/gz1e are not
+ * written, gC = gz1m, ge_out = WcT gC. */
 int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                  const float* a2m, const float* a1m, const float* a2e, const float* a1e,
                  const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
@@ -159,7 +170,8 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
 
 /* Backward of the P/Q gathers: gP[v] = sum_{dst-seg(v)} gz1m + sum_{src-seg(v)} gz1e,
  * gQ[v] = sum_{src-seg(v)} gz1m + sum_{dst-seg(v)} gz1e.  src-seg uses rowptr_src and
- * perm_src (positions of the dst-sorted edges grouped by src). */
+ * perm_src (positions of the dst-sorted edges grouped by src).  gz1e may be NULL (no
+ * edge-update branch). */
 int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int* rowptr_src,
                        const int* perm_src, const float* gz1m, const float* gz1e,
                        float* gP, float* gQ, void* stream);

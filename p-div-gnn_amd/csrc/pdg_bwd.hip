@@ -145,6 +145,51 @@ extern "C" int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, co
   return PDG_OK;
 }
 
+__global__ __launch_bounds__(256) void ln_colsum_nodes_kernel(int N, const float* __restrict__ gaggr,
+                                                              const int* __restrict__ rowptr,
+                                                              const float* __restrict__ xs,
+                                                              double* __restrict__ part) {
+  __shared__ double red[8][256];
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const int nhw = blockDim.x >> 5;
+  double sg[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
+  for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
+    const float deg = (float)(rowptr[v + 1] - rowptr[v]);
+    const f32x4 g = reinterpret_cast<const f32x4*>(gaggr + (size_t)v * L)[j];
+    const f32x4 x = reinterpret_cast<const f32x4*>(xs + (size_t)v * L)[j];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      sg[c] += (double)deg * (double)g[c];
+      sx[c] += (double)g[c] * (double)x[c];
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    red[hw][4 * j + c] = sg[c];
+    red[hw][128 + 4 * j + c] = sx[c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    double s = 0;
+    for (int w = 0; w < nhw; ++w) s += red[w][i];
+    part[(size_t)blockIdx.x * 256 + i] = s;
+  }
+}
+
+extern "C" int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* rowptr, const float* xhat_sum,
+                                   double* partials, int* nparts, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_ln_colsum_nodes: n_nodes must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(xhat_sum), "pdg_ln_colsum_nodes: misaligned pointer");
+  long want = (n_nodes + 7) / 8;
+  long cap = (long)device_cus();
+  const int grid = (int)(want < cap ? want : cap);
+  hipLaunchKernelGGL(ln_colsum_nodes_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, gaggr, rowptr,
+                     xhat_sum, partials);
+  PDG_CHECK_LAUNCH("pdg_ln_colsum_nodes");
+  if (nparts) *nparts = grid;
+  return PDG_OK;
+}
+
 // 1024 threads: column c (of 256: 128 sum-gy, 128 sum-gy*xhat) by 4 threads, each
 // summing every 4th block partial; the 4 are combined in a fixed order.
 __global__ __launch_bounds__(1024) void ln_colsum_finalize_kernel(const double* __restrict__ part, int n,
@@ -348,6 +393,7 @@ extern "C" int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const
 }
 
 // ============================================================================ fused edge backward
+template <bool EU>
 __global__ __launch_bounds__(512, 2) void edge_bwd_kernel(
     int E, const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
     const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
@@ -361,8 +407,8 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_kernel(
   load_wblock(lds + WBLK, WcT, L, 0);
   __syncthreads();
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
-  const LNStat ste = *reinterpret_cast<const LNStat*>(ste_p);
-  const pdg_ln_bwd lbm = *lbm_p, lbe = *lbe_p;
+  const LNStat ste = *reinterpret_cast<const LNStat*>(EU ? ste_p : stm_p);
+  const pdg_ln_bwd lbm = *lbm_p, lbe = *(EU ? lbe_p : lbm_p);
   const int l = lane_id();
   const int nw = blockDim.x >> 6;
   const int ntiles = tiles_of(E);
@@ -383,24 +429,29 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_kernel(
     load_frag(a, a1m + (size_t)rc * L);
     relu_mask_acc(v, acc, a);
     if (valid) store_frag(gz1m + (size_t)row * L, v);
-    // ---- edge-update path: gy = ge_next
-    load_frag(v, ge_next + (size_t)rc * L);
-    load_frag(a, a2e + (size_t)rc * L);
-    ln_relu_bwd(v, a, ste, lbe, lg);
-    if (valid) store_frag(gz2e + (size_t)row * L, v);
-    zero_acc(acc);
-    gemm128(acc, lds, v);
-    load_frag(a, a1e + (size_t)rc * L);
-    relu_mask_acc(v, acc, a);
-    if (valid) store_frag(gz1e + (size_t)row * L, v);
-    // ---- gC = gz1m + gz1e (gz1m re-read from this lane's own store);  ge_out = ge_next + Wc^T gC
-    load_frag(a, gz1m + (size_t)(valid ? row : rc) * L);
-    PDG_FOR_FRAG(s) v[s] += a[s];
+    if (EU) {
+      // ---- edge-update path: gy = ge_next
+      load_frag(v, ge_next + (size_t)rc * L);
+      load_frag(a, a2e + (size_t)rc * L);
+      ln_relu_bwd(v, a, ste, lbe, lg);
+      if (valid) store_frag(gz2e + (size_t)row * L, v);
+      zero_acc(acc);
+      gemm128(acc, lds, v);
+      load_frag(a, a1e + (size_t)rc * L);
+      relu_mask_acc(v, acc, a);
+      if (valid) store_frag(gz1e + (size_t)row * L, v);
+      // gC = gz1m + gz1e (gz1m re-read from this lane's own store)
+      load_frag(a, gz1m + (size_t)(valid ? row : rc) * L);
+      PDG_FOR_FRAG(s) v[s] += a[s];
+    }
+    // ---- ge_out = ge_next + Wc^T gC
     if (valid) store_frag(gC + (size_t)row * L, v);
     zero_acc(acc);
     gemm128(acc, lds + WBLK, v);
-    load_frag(a, ge_next + (size_t)rc * L);
-    PDG_FOR_FRAG(s) ACC(acc, s) += a[s];
+    if (EU) {
+      load_frag(a, ge_next + (size_t)rc * L);
+      PDG_FOR_FRAG(s) ACC(acc, s) += a[s];
+    }
     if (valid) store_acc(ge_out + (size_t)row * L, acc);
   }
 }
@@ -412,15 +463,22 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
                             float* gz2m, float* gz1m, float* gz2e, float* gz1e, float* gC, float* ge_out,
                             void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd: n_edges must be > 0");
-  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(ge_next) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) &&
-                    PDG_ALIGNED(a2e) && PDG_ALIGNED(a1e) && PDG_ALIGNED(gz2m) && PDG_ALIGNED(gz1m) &&
-                    PDG_ALIGNED(gz2e) && PDG_ALIGNED(gz1e) && PDG_ALIGNED(gC) && PDG_ALIGNED(ge_out),
+  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(gz2m) &&
+                    PDG_ALIGNED(gz1m) && PDG_ALIGNED(gC) && PDG_ALIGNED(ge_out),
                 "pdg_edge_bwd: misaligned pointer");
+  PDG_CHECK_ARG(!ge_next || (PDG_ALIGNED(ge_next) && PDG_ALIGNED(a2e) && PDG_ALIGNED(a1e) && PDG_ALIGNED(gz2e) &&
+                             PDG_ALIGNED(gz1e) && st_e && lb_e),
+                "pdg_edge_bwd: edge-update arguments missing or misaligned");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd: ge_out must not alias ge_next");
   const int grid = persistent_grid(n_edges, 8, 1);
-  hipLaunchKernelGGL(edge_bwd_kernel, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
-                     n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
-                     gz1m, gz2e, gz1e, gC, ge_out);
+  if (ge_next)
+    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+                       n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
+                       gz1m, gz2e, gz1e, gC, ge_out);
+  else
+    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+                       n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, WcT, gz2m,
+                       gz1m, gz2e, gz1e, gC, ge_out);
   PDG_CHECK_LAUNCH("pdg_edge_bwd");
   return PDG_OK;
 }
@@ -439,13 +497,13 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* _
     const int d0 = rpd[v], d1 = rpd[v + 1];
     for (int k = d0; k < d1; ++k) {   // edges whose target is v: message x_i, edge-update x[col]
       p += reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
-      q += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+      if (gz1e) q += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
     }
     const int s0 = rps[v], s1 = rps[v + 1];
     for (int i = s0; i < s1; ++i) {   // edges whose source is v: message x_j, edge-update x[row]
       const int k = perm_s[i];
       q += reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
-      p += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+      if (gz1e) p += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
     }
     reinterpret_cast<f32x4*>(gP + (size_t)v * L)[j] = p;
     reinterpret_cast<f32x4*>(gQ + (size_t)v * L)[j] = q;
@@ -455,7 +513,7 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* _
 extern "C" int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int* rowptr_src, const int* perm_src,
                                   const float* gz1m, const float* gz1e, float* gP, float* gQ, void* stream) {
   PDG_CHECK_ARG(n_nodes > 0, "pdg_pq_scatter_bwd: n_nodes must be > 0");
-  PDG_CHECK_ARG(PDG_ALIGNED(gz1m) && PDG_ALIGNED(gz1e) && PDG_ALIGNED(gP) && PDG_ALIGNED(gQ),
+  PDG_CHECK_ARG(PDG_ALIGNED(gz1m) && (!gz1e || PDG_ALIGNED(gz1e)) && PDG_ALIGNED(gP) && PDG_ALIGNED(gQ),
                 "pdg_pq_scatter_bwd: misaligned pointer");
   long want = (n_nodes + 7) / 8;
   long cap = (long)device_cus() * 8;

@@ -307,6 +307,7 @@ extern "C" int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat*
 // tuple dies as its chunk is consumed):
 //   edge update: relu(C + P[src] + Q[dst]) -> stored to a1e
 //   message:     relu(C + P[dst] + Q[src]) -> v (and stored to a1m by the caller)
+template <bool EU>
 __device__ __forceinline__ void first_layers(float (&v)[64], const f32x16 (&C)[4], const float* __restrict__ ps,
                                              const float* __restrict__ qd, const float* __restrict__ pd,
                                              const float* __restrict__ qs, float* __restrict__ a1e_row,
@@ -317,8 +318,10 @@ __device__ __forceinline__ void first_layers(float (&v)[64], const f32x16 (&C)[4
     f32x4 xs[2], yd[2], xd[2], ys[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      xs[t] = reinterpret_cast<const f32x4*>(ps + ho + 8 * q)[t];
-      yd[t] = reinterpret_cast<const f32x4*>(qd + ho + 8 * q)[t];
+      if (EU) {
+        xs[t] = reinterpret_cast<const f32x4*>(ps + ho + 8 * q)[t];
+        yd[t] = reinterpret_cast<const f32x4*>(qd + ho + 8 * q)[t];
+      }
       xd[t] = reinterpret_cast<const f32x4*>(pd + ho + 8 * q)[t];
       ys[t] = reinterpret_cast<const f32x4*>(qs + ho + 8 * q)[t];
     }
@@ -329,16 +332,16 @@ __device__ __forceinline__ void first_layers(float (&v)[64], const f32x16 (&C)[4
       for (int j = 0; j < 4; ++j) {
         const int s = 8 * q + 4 * t + j;
         const float c = ACC(C, s);
-        e[j] = fmaxf((c + xs[t][j]) + yd[t][j], 0.f);
+        if (EU) e[j] = fmaxf((c + xs[t][j]) + yd[t][j], 0.f);
         v[s] = fmaxf((c + xd[t][j]) + ys[t][j], 0.f);
       }
-      if (valid) reinterpret_cast<f32x4*>(a1e_row + ho + 8 * q)[t] = e;
+      if (EU && valid) reinterpret_cast<f32x4*>(a1e_row + ho + 8 * q)[t] = e;
     }
     PDG_FENCE();
   }
 }
 
-template <bool RES>
+template <bool RES, bool EU>
 __global__ __launch_bounds__(512, 2) void edge_fwd_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
@@ -380,8 +383,8 @@ __global__ __launch_bounds__(512, 2) void edge_fwd_kernel(
     }
     // layer 1 of the edge update (models.py:219-222, x[row] = x[src], x[col] = x[dst]; stored,
     // re-read below) and of the message (models.py:233-238, x_i = x[dst], x_j = x[src])
-    first_layers(v, C, P + (size_t)s_node * L, Q + (size_t)d_node * L, P + (size_t)d_node * L,
-                 Q + (size_t)s_node * L, a1e + (size_t)row * L, valid);
+    first_layers<EU>(v, C, P + (size_t)s_node * L, Q + (size_t)d_node * L, P + (size_t)d_node * L,
+                     Q + (size_t)s_node * L, EU ? a1e + (size_t)row * L : nullptr, valid);
     if (valid) store_frag(a1m + (size_t)row * L, v);
     f32x16 Z[4];
     zero_acc(Z);
@@ -389,37 +392,43 @@ __global__ __launch_bounds__(512, 2) void edge_fwd_kernel(
     bias_relu(v, Z, b2);
     if (valid) store_frag(a2m + (size_t)row * L, v);
     accum_stats(v, valid, sm1, sm2);
-    // edge-update layer 2
-    load_frag(v, a1e + (size_t)(valid ? row : rc) * L);
-    zero_acc(Z);
-    gemm128(Z, lds + WBLK, v);
-    bias_relu(v, Z, b2);
-    if (valid) store_frag(a2e + (size_t)row * L, v);
-    accum_stats(v, valid, se1, se2);
+    if (EU) {
+      // edge-update layer 2
+      load_frag(v, a1e + (size_t)(valid ? row : rc) * L);
+      zero_acc(Z);
+      gemm128(Z, lds + WBLK, v);
+      bias_relu(v, Z, b2);
+      if (valid) store_frag(a2e + (size_t)row * L, v);
+      accum_stats(v, valid, se1, se2);
+    }
   }
   write_partials(sm1, sm2, part_m);
-  write_partials(se1, se2, part_e);
+  if (EU) write_partials(se1, se2, part_e);
 }
 
 extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                             const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
                             const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                             const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
-                            double* part_e, int* nparts, void* stream) {
+                            double* part_e, int with_edge_update, int* nparts, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd: n_edges must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
-                    PDG_ALIGNED(a1m) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e) &&
-                    (!e_res || PDG_ALIGNED(e_res)),
+                    PDG_ALIGNED(a1m) && PDG_ALIGNED(a2m) && (!e_res || PDG_ALIGNED(e_res)),
                 "pdg_edge_fwd: misaligned pointer");
+  PDG_CHECK_ARG(!with_edge_update || (a1e && a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
+                "pdg_edge_fwd: edge-update outputs missing or misaligned");
   const int grid = persistent_grid(n_edges, 8, 1);
-  if (e_res)
-    hipLaunchKernelGGL(edge_fwd_kernel<true>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
-                       n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m,
-                       a1e, a2e, part_m, part_e);
-  else
-    hipLaunchKernelGGL(edge_fwd_kernel<false>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
-                       n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m,
-                       a1e, a2e, part_m, part_e);
+  const size_t shm = 2 * WBLK * sizeof(float);
+  hipStream_t s = (hipStream_t)stream;
+#define PDG_EDGE_FWD(R, U)                                                                                     \
+  hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(512), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \
+                     e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e)
+  if (e_res) {
+    if (with_edge_update) PDG_EDGE_FWD(true, true); else PDG_EDGE_FWD(true, false);
+  } else {
+    if (with_edge_update) PDG_EDGE_FWD(false, true); else PDG_EDGE_FWD(false, false);
+  }
+#undef PDG_EDGE_FWD
   PDG_CHECK_LAUNCH("pdg_edge_fwd");
   if (nparts) *nparts = grid;
   return PDG_OK;
@@ -434,7 +443,7 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __re
                                                           const pdg_ln_stat* __restrict__ stp,
                                                           const float* __restrict__ lg,
                                                           const float* __restrict__ lb,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out, float* __restrict__ xsum) {
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const int nhw = blockDim.x >> 5;
   float mean = 0.f, den = 1.f, rstd = 1.f;
@@ -449,7 +458,7 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __re
   }
   for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
     const int k0 = rowptr[v], k1 = rowptr[v + 1];
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f}, xs = {0.f, 0.f, 0.f, 0.f};
     int k = k0;
     for (; k + 1 < k1; k += 2) {
       f32x4 x0 = reinterpret_cast<const f32x4*>(rows + (size_t)k * L)[j];
@@ -457,8 +466,11 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __re
       if (ln) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          x0[c] = div_den(x0[c] - mean, den, rstd) * g[c] + b[c];
-          x1[c] = div_den(x1[c] - mean, den, rstd) * g[c] + b[c];
+          const float h0 = div_den(x0[c] - mean, den, rstd), h1 = div_den(x1[c] - mean, den, rstd);
+          xs[c] += h0;
+          xs[c] += h1;
+          x0[c] = h0 * g[c] + b[c];
+          x1[c] = h1 * g[c] + b[c];
         }
       }
       acc += x0;
@@ -468,23 +480,29 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __re
       f32x4 x0 = reinterpret_cast<const f32x4*>(rows + (size_t)k * L)[j];
       if (ln) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) x0[c] = div_den(x0[c] - mean, den, rstd) * g[c] + b[c];
+        for (int c = 0; c < 4; ++c) {
+          const float h0 = div_den(x0[c] - mean, den, rstd);
+          xs[c] += h0;
+          x0[c] = h0 * g[c] + b[c];
+        }
       }
       acc += x0;
     }
     reinterpret_cast<f32x4*>(out + (size_t)v * L)[j] = acc;
+    if (xsum) reinterpret_cast<f32x4*>(xsum + (size_t)v * L)[j] = xs;
   }
 }
 
 extern "C" int pdg_segment_sum(int n_nodes, const int* rowptr, const float* rows, const pdg_ln_stat* st,
-                               const float* ln_g, const float* ln_b, float* out, void* stream) {
+                               const float* ln_g, const float* ln_b, float* out, float* xhat_sum, void* stream) {
+  PDG_CHECK_ARG(!xhat_sum || (st && PDG_ALIGNED(xhat_sum)), "pdg_segment_sum: xhat_sum needs st, 16-B alignment");
   PDG_CHECK_ARG(n_nodes > 0, "pdg_segment_sum: n_nodes must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(rows) && PDG_ALIGNED(out), "pdg_segment_sum: misaligned pointer");
   long want = (n_nodes + 7) / 8;
   long cap = (long)device_cus() * 8;
   const int grid = (int)(want < cap ? want : cap);
   hipLaunchKernelGGL(segment_sum_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, rowptr, rows,
-                     st, ln_g, ln_b, out);
+                     st, ln_g, ln_b, out, xhat_sum);
   PDG_CHECK_LAUNCH("pdg_segment_sum");
   return PDG_OK;
 }

@@ -166,23 +166,28 @@ class EPDEngine:
             x_t = self._empty(N, L)
             lib.pdg_node_pq(N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_t), _p(W1),
                             _p(Pm), _p(Qm), s)
+            # the last step's edge update has no consumer (models.py:316 decodes nodes only)
+            eu = t < steps - 1
             e_t = self._empty(E, L)
-            a1m, a2m, a1e, a2e = (self._empty(E, L) for _ in range(4))
-            self._t("edge_fwd", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t),
-                             _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
-                             _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), np_, s)
+            a1m, a2m = self._empty(E, L), self._empty(E, L)
+            a1e, a2e = (self._empty(E, L), self._empty(E, L)) if eu else (None, None)
+            self._t("edge_fwd", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
+                    _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
+                    _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
             self._finalize(self._part_a, E * L, st[i_m], s)
-            self._finalize(self._part_b, E * L, st[i_e], s)
+            if eu:
+                self._finalize(self._part_b, E * L, st[i_e], s)
             aggr = self._empty(N, L)
+            xs = self._empty(N, L) if need_grad else None
             self._t("segment_sum", lib.pdg_segment_sum, N, _p(plan.rowptr_dst), _p(a2m), st[i_m], _p(ge), _p(be),
-                    _p(aggr), s)
+                    _p(aggr), _p(xs), s)
             a1n, a2n = self._empty(N, L), self._empty(N, L)
             lib.pdg_node_mlp1(N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(a1n), s)
             lib.pdg_mlp2_fwd(N, _p(a1n), _p(Wn2), _p(bn2), _p(a2n), _p(self._part_a), np_, s)
             self._finalize(self._part_a, N * L, st[i_n], s)
             if need_grad:
-                ctx.per_step.append(dict(x=x_t, e=e_t, a1m=a1m, a2m=a2m, a1e=a1e, a2e=a2e, aggr=aggr,
-                                         a1n=a1n, a2n=a2n, i_m=i_m, i_e=i_e, i_n=i_n))
+                ctx.per_step.append(dict(x=x_t, e=e_t, a1m=a1m, a2m=a2m, a1e=a1e, a2e=a2e, aggr=aggr, xs=xs,
+                                         a1n=a1n, a2n=a2n, i_m=i_m, i_e=i_e, i_n=i_n, eu=eu))
             a2n_prev, stn_prev, gn_prev, bn_prev = a2n, st[i_n], gn, bnn
             a2e_prev, ste_prev, ge_prev, be_prev = a2e, st[i_e], ge, be
             x_prev, e_prev = x_t, e_t
@@ -254,14 +259,19 @@ class EPDEngine:
                              None, _p(G["node_decoder.2.bias"]), s)
         segs["d1"].append((gz1d, ctx.x_S, N))
 
-        ge_next = torch.zeros(E, L, dtype=torch.float32, device=self.device)
+        ge_next = None              # d loss / d e_S: the last edge update has no consumer
         gaggr, gx_part, gx_t = (self._empty(N, L) for _ in range(3))
-        gz1m, gz1e, ge_out = (self._empty(E, L) for _ in range(3))
+        gz1m, gz1e = self._empty(E, L), self._empty(E, L)
+        ge_bufs = [self._empty(E, L), self._empty(E, L)]
         gx_next = gx
         for t in reversed(range(ctx.steps)):
             d = ctx.per_step[t]
+            eu = d["eu"]
+            assert eu == (ge_next is not None)
             gz2n, gz1n, gP, gQ = (self._empty(N, L) for _ in range(4))
-            gz2m, gz2e, gC = (self._empty(E, L) for _ in range(3))
+            gz2m, gC = self._empty(E, L), self._empty(E, L)
+            gz2e = self._empty(E, L) if eu else None
+            ge_out = ge_bufs[t % 2]
             # node_net tail: n_t = LN_n(a2n_t), gy = gx_next   (x_{t+1} = n_t + x_t)
             colsum(N, gx_next, None, d["a2n"], st[d["i_n"]], "processor.node_net.4.weight",
                    "processor.node_net.4.bias", lb[0])
@@ -269,19 +279,25 @@ class EPDEngine:
                              _p(P["processor.node_net.4.weight"]), _p(T["Wn2T"]), _p(gz2n), _p(gz1n), s)
             lib.pdg_gemm_dual(N, _p(gz1n), _p(T["Wn1aT"]), _p(T["Wn1bT"]), None, _p(gx_next), _p(gaggr),
                               _p(gx_part), s)
-            # edge_net LayerNorm sums: message (gy = gaggr[dst]) and edge update (gy = ge_next)
-            colsum(E, gaggr, plan.dst, d["a2m"], st[d["i_m"]], "processor.edge_net.4.weight",
-                   "processor.edge_net.4.bias", lb[1])
-            colsum(E, ge_next, None, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
-                   "processor.edge_net.4.bias", lb[2])
+            # edge_net LayerNorm sums.  message: gy = gaggr[dst], reduced per node from the forward's
+            # sum of xhat over each destination segment; edge update: gy = ge_next (per edge)
+            lib.pdg_ln_colsum_nodes(N, _p(gaggr), _p(plan.rowptr_dst), _p(d["xs"]), _p(self._part_col), np_, s)
+            lib.pdg_ln_colsum_finalize(_p(self._part_col), self._nparts.value, _p(P["processor.edge_net.4.weight"]),
+                                       st[d["i_m"]], _p(G["processor.edge_net.4.weight"]),
+                                       _p(G["processor.edge_net.4.bias"]), lb[1], s)
+            if eu:
+                colsum(E, ge_next, None, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
+                       "processor.edge_net.4.bias", lb[2])
             self._t("edge_bwd", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr), _p(ge_next), _p(d["a2m"]),
-                    _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]], st[d["i_e"]], lb[1], lb[2],
-                    _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]), _p(gz2m), _p(gz1m),
-                    _p(gz2e), _p(gz1e), _p(gC), _p(ge_out), s)
+                    _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]], st[d["i_e"]] if eu else None, lb[1],
+                    lb[2] if eu else None, _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]),
+                    _p(gz2m), _p(gz1m), _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), s)
             self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
-                    _p(plan.perm_src), _p(gz1m), _p(gz1e), _p(gP), _p(gQ), s)
+                    _p(plan.perm_src), _p(gz1m), _p(gz1e if eu else None), _p(gP), _p(gQ), s)
             lib.pdg_gemm_sum2(N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part), _p(gx_t), s)
-            segs["W2"] += [(gz2m, d["a1m"], E), (gz2e, d["a1e"], E)]
+            segs["W2"].append((gz2m, d["a1m"], E))
+            if eu:
+                segs["W2"].append((gz2e, d["a1e"], E))
             segs["Wc"].append((gC, d["e"], E))
             segs["Wa"].append((gP, d["x"], N))
             segs["Wb"].append((gQ, d["x"], N))
@@ -289,7 +305,7 @@ class EPDEngine:
             segs["Wn1a"].append((gz1n, d["aggr"], N))
             segs["Wn1b"].append((gz1n, d["x"], N))
             gx_next, gx_t = gx_t, gx_next
-            ge_next, ge_out = ge_out, ge_next
+            ge_next = ge_out
         # encoders
         gz2, gz1 = self._empty(N, L), self._empty(N, L)
         colsum(N, gx_next, None, ctx.a2_ne, st[0], "node_encoder.4.weight", "node_encoder.4.bias", lb[3])

@@ -28,14 +28,15 @@ SIGNATURES: dict[str, list] = {
     "pdg_encoder_fwd": [I, I, P, P, P, P, P, P, P, P, P, P],
     "pdg_ln_finalize": [P, I, c_double, P, P],
     "pdg_node_pq": [I, P, P, P, P, P, P, P, P, P, P],
-    "pdg_edge_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
-    "pdg_segment_sum": [I, P, P, P, P, P, P, P],
+    "pdg_edge_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
+    "pdg_segment_sum": [I, P, P, P, P, P, P, P, P],
     "pdg_node_mlp1": [I, P, P, P, P, P, P],
     "pdg_mlp2_fwd": [I, P, P, P, P, P, P, P],
     "pdg_decoder_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
     "pdg_any_nonzero": [P, c_int64, P, P],
     "pdg_decoder_bwd": [I, P, P, P, P, P, P, P],
     "pdg_ln_colsum": [I, P, P, P, P, P, P, P],
+    "pdg_ln_colsum_nodes": [I, P, P, P, P, P, P],
     "pdg_ln_colsum_finalize": [P, I, P, P, P, P, P, P],
     "pdg_mlp2_bwd": [I, P, P, P, P, P, P, P, P, P, P, P],
     "pdg_gemm_dual": [I, P, P, P, P, P, P, P, P],

@@ -122,17 +122,29 @@ def test_segment_sum_with_layernorm(env, N, E):
                               dtype=torch.uint8).cuda())
     out = torch.empty(N, L, device="cuda")
     rp_d = rp.int().cuda()
+    xs = torch.empty(N, L, device="cuda")
     lib.pdg_segment_sum(N, rp_d.data_ptr(), rows.data_ptr(), st.data_ptr(), g.data_ptr(), b.data_ptr(),
-                        out.data_ptr(), s)
-    normed = (r64.cpu() - mean) / den * g.double().cpu() + b.double().cpu()
+                        out.data_ptr(), xs.data_ptr(), s)
+    xhat = (r64.cpu() - mean) / den
+    normed = xhat * g.double().cpu() + b.double().cpu()
     ref = torch.zeros(N, L, dtype=torch.float64).index_add_(0, dst, normed)
     assert rel(out, ref) < TOL
+    assert rel(xs, torch.zeros(N, L, dtype=torch.float64).index_add_(0, dst, xhat)) < TOL
+    # node-level LayerNorm-backward sums of the gathered gradient gy_k = gaggr[dst_k]
+    gaggr = rnd(N, L)
+    part = torch.empty(4096 * 256, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    lib.pdg_ln_colsum_nodes(N, gaggr.data_ptr(), rp_d.data_ptr(), xs.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
+    tot = part[: n.value * 256].view(n.value, 256).sum(0).cpu()
+    gy = gaggr.double().cpu()[dst]
+    assert rel(tot[:L], gy.sum(0)) < 1e-6
+    assert rel(tot[L:], (gy * xhat).sum(0)) < 1e-5
     # zero in-degree nodes are exactly zero
     deg0 = (rp[1:] - rp[:-1]) == 0
     if deg0.any():
         assert float(out.cpu()[deg0].abs().max()) == 0.0
     raw = torch.empty(N, L, device="cuda")
-    lib.pdg_segment_sum(N, rp_d.data_ptr(), rows.data_ptr(), None, None, None, raw.data_ptr(), s)
+    lib.pdg_segment_sum(N, rp_d.data_ptr(), rows.data_ptr(), None, None, None, raw.data_ptr(), None, s)
     assert rel(raw, torch.zeros(N, L, dtype=torch.float64).index_add_(0, dst, r64.cpu())) < TOL
 
 
