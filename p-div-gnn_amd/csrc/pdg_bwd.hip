@@ -13,12 +13,17 @@
 
 using namespace pdg;
 
+#define PDG_TILE_LOOP(M)                                                              \
+  const int nw_ = blockDim.x >> 6;                                                    \
+  const int ntiles_ = tiles_of(M);                                                    \
+  for (int tile = blockIdx.x * nw_ + wave_id(); tile < ntiles_; tile += gridDim.x * nw_)
+
 // ga2 -> gz2 for one fragment (in place on gy): LN backward and relu mask.
-__device__ __forceinline__ void ln_relu_bwd(float (&gy)[64], const float (&a2)[64], const LNStat& st,
+__device__ __forceinline__ void ln_relu_bwd(float (&gy)[FRAG], const float (&a2)[FRAG], const LNStat& st,
                                             const pdg_ln_bwd& lb, const float* __restrict__ g) {
-  const f32x4* gp = reinterpret_cast<const f32x4*>(g + half_off());
+  const f32x4* gp = reinterpret_cast<const f32x4*>(g + quarter_off());
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
+  for (int t = 0; t < 8; ++t) {
     const f32x4 gg = gp[t];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -31,12 +36,12 @@ __device__ __forceinline__ void ln_relu_bwd(float (&gy)[64], const float (&a2)[6
   }
 }
 
-__device__ __forceinline__ void relu_mask_acc(float (&v)[64], const f32x16 (&acc)[4], const float (&a)[64]) {
+__device__ __forceinline__ void relu_mask_acc(float (&v)[FRAG], const Acc& acc, const float (&a)[FRAG]) {
   PDG_FOR_FRAG(s) v[s] = a[s] > 0.f ? ACC(acc, s) : 0.f;
 }
 
 // ============================================================================ decoder backward
-__global__ __launch_bounds__(256, 2) void decoder_bwd_kernel(int N, const float* __restrict__ gy,
+__global__ __launch_bounds__(384, 3) void decoder_bwd_kernel(int N, const float* __restrict__ gy,
                                                               const float* __restrict__ a1d,
                                                               const float* __restrict__ Wd2,
                                                               const float* __restrict__ Wd1T,
@@ -48,21 +53,19 @@ __global__ __launch_bounds__(256, 2) void decoder_bwd_kernel(int N, const float*
   for (int i = threadIdx.x; i < 3 * L; i += blockDim.x) w2l[i] = Wd2[i];
   __syncthreads();
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(N);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(N) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < N;
     const int rc = valid ? row : N - 1;
     const float g0 = gy[(size_t)rc * 3], g1 = gy[(size_t)rc * 3 + 1], g2 = gy[(size_t)rc * 3 + 2];
-    float v[64];
-    const int ho = half_off();
-    const float* w0 = w2l + ho;
+    float v[FRAG];
+    const int qo = quarter_off();
+    const float* w0 = w2l + qo;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 2; ++q) {
       f32x4 a[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = reinterpret_cast<const f32x4*>(a1d + (size_t)rc * L + ho + 16 * q)[t];
+      for (int t = 0; t < 4; ++t) a[t] = reinterpret_cast<const f32x4*>(a1d + (size_t)rc * L + qo + 16 * q)[t];
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -74,7 +77,7 @@ __global__ __launch_bounds__(256, 2) void decoder_bwd_kernel(int N, const float*
       PDG_FENCE();
     }
     if (valid) store_frag(gz1d + (size_t)row * L, v);
-    f32x16 acc[4];
+    Acc acc;
     zero_acc(acc);
     gemm128(acc, lds, v);
     if (valid) store_acc(gx + (size_t)row * L, acc);
@@ -86,8 +89,8 @@ extern "C" int pdg_decoder_bwd(int n_nodes, const float* gy, const float* a1d, c
   PDG_CHECK_ARG(n_nodes > 0, "pdg_decoder_bwd: n_nodes must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(a1d) && PDG_ALIGNED(gz1d) && PDG_ALIGNED(gx) && PDG_ALIGNED(Wd1T),
                 "pdg_decoder_bwd: misaligned pointer");
-  const int grid = persistent_grid(n_nodes, 4, 2);
-  hipLaunchKernelGGL(decoder_bwd_kernel, dim3(grid), dim3(256), (WBLK + 3 * L) * sizeof(float), (hipStream_t)stream,
+  const int grid = persistent_grid(n_nodes, 6, 2);
+  hipLaunchKernelGGL(decoder_bwd_kernel, dim3(grid), dim3(384), (WBLK + 3 * L) * sizeof(float), (hipStream_t)stream,
                      n_nodes, gy, a1d, Wd2, Wd1T, gz1d, gx);
   PDG_CHECK_LAUNCH("pdg_decoder_bwd");
   return PDG_OK;
@@ -246,7 +249,7 @@ extern "C" int pdg_ln_colsum_finalize(const double* partials, int nparts, const 
 }
 
 // ============================================================================ MLP tail backward
-__global__ __launch_bounds__(256, 2) void mlp2_bwd_kernel(int M, const float* __restrict__ gyr,
+__global__ __launch_bounds__(384, 3) void mlp2_bwd_kernel(int M, const float* __restrict__ gyr,
                                                            const int* __restrict__ gidx,
                                                            const float* __restrict__ a2,
                                                            const float* __restrict__ a1,
@@ -261,19 +264,17 @@ __global__ __launch_bounds__(256, 2) void mlp2_bwd_kernel(int M, const float* __
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const pdg_ln_bwd lb = *lbp;
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(M);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(M) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < M;
     const int rc = valid ? row : M - 1;
     const int gr = gidx ? gidx[rc] : rc;
-    float v[64], a[64];
+    float v[FRAG], a[FRAG];
     load_frag(v, gyr + (size_t)gr * L);
     load_frag(a, a2 + (size_t)rc * L);
     ln_relu_bwd(v, a, st, lb, lg);
     if (valid) store_frag(gz2 + (size_t)row * L, v);
-    f32x16 acc[4];
+    Acc acc;
     zero_acc(acc);
     gemm128(acc, lds, v);
     load_frag(a, a1 + (size_t)rc * L);
@@ -289,15 +290,15 @@ extern "C" int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, con
   PDG_CHECK_ARG(PDG_ALIGNED(gy_rows) && PDG_ALIGNED(a2) && PDG_ALIGNED(a1) && PDG_ALIGNED(gz2) &&
                     PDG_ALIGNED(gz1) && PDG_ALIGNED(W2T),
                 "pdg_mlp2_bwd: misaligned pointer");
-  const int grid = persistent_grid(rows, 4, 2);
-  hipLaunchKernelGGL(mlp2_bwd_kernel, dim3(grid), dim3(256), WBLK * sizeof(float), (hipStream_t)stream, rows,
+  const int grid = persistent_grid(rows, 6, 2);
+  hipLaunchKernelGGL(mlp2_bwd_kernel, dim3(grid), dim3(384), WBLK * sizeof(float), (hipStream_t)stream, rows,
                      gy_rows, gidx, a2, a1, st, lb, ln_g, W2T, gz2, gz1);
   PDG_CHECK_LAUNCH("pdg_mlp2_bwd");
   return PDG_OK;
 }
 
 // ============================================================================ dual / summed GEMMs
-__global__ __launch_bounds__(512, 2) void gemm_dual_kernel(int M, const float* __restrict__ in,
+__global__ __launch_bounds__(768, 3) void gemm_dual_kernel(int M, const float* __restrict__ in,
                                                             const float* __restrict__ W0T,
                                                             const float* __restrict__ W1T,
                                                             const float* __restrict__ res0,
@@ -308,15 +309,13 @@ __global__ __launch_bounds__(512, 2) void gemm_dual_kernel(int M, const float* _
   load_wblock(lds + WBLK, W1T, L, 0);
   __syncthreads();
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(M);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(M) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < M;
     const int rc = valid ? row : M - 1;
-    float v[64], r[64];
+    float v[FRAG], r[FRAG];
     load_frag(v, in + (size_t)rc * L);
-    f32x16 acc[4];
+    Acc acc;
     zero_acc(acc);
     gemm128(acc, lds, v);
     if (res0) {
@@ -340,14 +339,14 @@ extern "C" int pdg_gemm_dual(int rows, const float* in, const float* W0T, const 
   PDG_CHECK_ARG(PDG_ALIGNED(in) && PDG_ALIGNED(out0) && PDG_ALIGNED(out1) && PDG_ALIGNED(W0T) &&
                     PDG_ALIGNED(W1T) && (!res0 || PDG_ALIGNED(res0)) && (!res1 || PDG_ALIGNED(res1)),
                 "pdg_gemm_dual: misaligned pointer");
-  const int grid = persistent_grid(rows, 8, 1);
-  hipLaunchKernelGGL(gemm_dual_kernel, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream, rows,
+  const int grid = persistent_grid(rows, 12, 1);
+  hipLaunchKernelGGL(gemm_dual_kernel, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream, rows,
                      in, W0T, W1T, res0, res1, out0, out1);
   PDG_CHECK_LAUNCH("pdg_gemm_dual");
   return PDG_OK;
 }
 
-__global__ __launch_bounds__(512, 2) void gemm_sum2_kernel(int M, const float* __restrict__ in0,
+__global__ __launch_bounds__(768, 3) void gemm_sum2_kernel(int M, const float* __restrict__ in0,
                                                             const float* __restrict__ in1,
                                                             const float* __restrict__ W0T,
                                                             const float* __restrict__ W1T,
@@ -358,14 +357,12 @@ __global__ __launch_bounds__(512, 2) void gemm_sum2_kernel(int M, const float* _
   load_wblock(lds + WBLK, W1T, L, 0);
   __syncthreads();
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(M);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(M) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < M;
     const int rc = valid ? row : M - 1;
-    float v[64];
-    f32x16 acc[4];
+    float v[FRAG];
+    Acc acc;
     zero_acc(acc);
     load_frag(v, in0 + (size_t)rc * L);
     gemm128(acc, lds, v);
@@ -385,8 +382,8 @@ extern "C" int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const
   PDG_CHECK_ARG(PDG_ALIGNED(in0) && PDG_ALIGNED(in1) && PDG_ALIGNED(out) && PDG_ALIGNED(W0T) &&
                     PDG_ALIGNED(W1T) && (!res || PDG_ALIGNED(res)),
                 "pdg_gemm_sum2: misaligned pointer");
-  const int grid = persistent_grid(rows, 8, 1);
-  hipLaunchKernelGGL(gemm_sum2_kernel, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream, rows,
+  const int grid = persistent_grid(rows, 12, 1);
+  hipLaunchKernelGGL(gemm_sum2_kernel, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream, rows,
                      in0, in1, W0T, W1T, res, out);
   PDG_CHECK_LAUNCH("pdg_gemm_sum2");
   return PDG_OK;
@@ -394,7 +391,7 @@ extern "C" int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const
 
 // ============================================================================ fused edge backward
 template <bool EU>
-__global__ __launch_bounds__(512, 2) void edge_bwd_kernel(
+__global__ __launch_bounds__(768, 3) void edge_bwd_kernel(
     int E, const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
     const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
     const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ stm_p, const pdg_ln_stat* __restrict__ ste_p,
@@ -410,15 +407,13 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_kernel(
   const LNStat ste = *reinterpret_cast<const LNStat*>(EU ? ste_p : stm_p);
   const pdg_ln_bwd lbm = *lbm_p, lbe = *(EU ? lbe_p : lbm_p);
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(E);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(E) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < E;
     const int rc = valid ? row : E - 1;
     const int d_node = dst[rc];
-    float v[64], a[64];
-    f32x16 acc[4];
+    float v[FRAG], a[FRAG];
+    Acc acc;
     // ---- message path: gy = gaggr[dst]   (scatter_add_ backward = gather)
     load_frag(v, gaggr + (size_t)d_node * L);
     load_frag(a, a2m + (size_t)rc * L);
@@ -430,6 +425,8 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_kernel(
     relu_mask_acc(v, acc, a);
     if (valid) store_frag(gz1m + (size_t)row * L, v);
     if (EU) {
+      float m[FRAG];
+      PDG_FOR_FRAG(s) m[s] = v[s];   // keep gz1m for gC
       // ---- edge-update path: gy = ge_next
       load_frag(v, ge_next + (size_t)rc * L);
       load_frag(a, a2e + (size_t)rc * L);
@@ -440,9 +437,7 @@ __global__ __launch_bounds__(512, 2) void edge_bwd_kernel(
       load_frag(a, a1e + (size_t)rc * L);
       relu_mask_acc(v, acc, a);
       if (valid) store_frag(gz1e + (size_t)row * L, v);
-      // gC = gz1m + gz1e (gz1m re-read from this lane's own store)
-      load_frag(a, gz1m + (size_t)(valid ? row : rc) * L);
-      PDG_FOR_FRAG(s) v[s] += a[s];
+      PDG_FOR_FRAG(s) v[s] = m[s] + v[s];   // gC = gz1m + gz1e
     }
     // ---- ge_out = ge_next + Wc^T gC
     if (valid) store_frag(gC + (size_t)row * L, v);
@@ -470,13 +465,13 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
                              PDG_ALIGNED(gz1e) && st_e && lb_e),
                 "pdg_edge_bwd: edge-update arguments missing or misaligned");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd: ge_out must not alias ge_next");
-  const int grid = persistent_grid(n_edges, 8, 1);
+  const int grid = persistent_grid(n_edges, 12, 1);
   if (ge_next)
-    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
                        gz1m, gz2e, gz1e, gC, ge_out);
   else
-    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, WcT, gz2m,
                        gz1m, gz2e, gz1e, gC, ge_out);
   PDG_CHECK_LAUNCH("pdg_edge_bwd");

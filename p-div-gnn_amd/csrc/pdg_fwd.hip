@@ -79,12 +79,19 @@ extern "C" int pdg_format_inputs(int n_nodes, int n_edges, const float* pos, con
   return PDG_OK;
 }
 
-// ============================================================================ stats helpers
-__device__ __forceinline__ void accum_stats(const float (&v)[64], bool valid, double& s1, double& s2) {
+// ============================================================================ tile helpers
+// Persistent tile loop: wave w of block b takes tiles b*nw + w, then strides by
+// gridDim*nw; a tile is 16 rows, lane row = tile*16 + (lane & 15).
+#define PDG_TILE_LOOP(M)                                                              \
+  const int nw_ = blockDim.x >> 6;                                                    \
+  const int ntiles_ = tiles_of(M);                                                    \
+  for (int tile = blockIdx.x * nw_ + wave_id(); tile < ntiles_; tile += gridDim.x * nw_)
+
+__device__ __forceinline__ void accum_stats(const float (&v)[FRAG], bool valid, double& s1, double& s2) {
   if (!valid) return;
-  // 64 values of one row half: fp32 partial per 16, fp64 across
+  // 32 values of one quarter row: fp32 partials per 16, fp64 across
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int q = 0; q < 2; ++q) {
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) { const float x = v[16 * q + j]; a += x; b += x * x; }
@@ -102,50 +109,49 @@ __device__ __forceinline__ void write_partials(double s1, double s2, double* par
   }
 }
 
-// v = LN(a2 row) [+ residual row], four fenced chunks of 16 floats.
+// v = LN(a2 row) [+ residual row], four fenced chunks of 8 floats.
 template <bool RES>
-__device__ __forceinline__ void ln_res_frag(float (&v)[64], const float* __restrict__ a2row,
+__device__ __forceinline__ void ln_res_frag(float (&v)[FRAG], const float* __restrict__ a2row,
                                             const float* __restrict__ resrow, const LNStat& st,
                                             const float* __restrict__ g, const float* __restrict__ b) {
-  const int ho = half_off();
+  const int qo = quarter_off();
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    f32x4 x[4], r[4], gg[4], bb[4];
+    f32x4 x[2], r[2], gg[2], bb[2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      x[t] = reinterpret_cast<const f32x4*>(a2row + ho + 16 * q)[t];
-      if (RES) r[t] = reinterpret_cast<const f32x4*>(resrow + ho + 16 * q)[t];
-      gg[t] = reinterpret_cast<const f32x4*>(g + ho + 16 * q)[t];
-      bb[t] = reinterpret_cast<const f32x4*>(b + ho + 16 * q)[t];
+    for (int t = 0; t < 2; ++t) {
+      x[t] = reinterpret_cast<const f32x4*>(a2row + qo + 8 * q)[t];
+      if (RES) r[t] = reinterpret_cast<const f32x4*>(resrow + qo + 8 * q)[t];
+      gg[t] = reinterpret_cast<const f32x4*>(g + qo + 8 * q)[t];
+      bb[t] = reinterpret_cast<const f32x4*>(b + qo + 8 * q)[t];
     }
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         float y = div_den(x[t][j] - st.mean, st.den, st.rstd) * gg[t][j] + bb[t][j];
         if (RES) y += r[t][j];
-        v[16 * q + 4 * t + j] = y;
+        v[8 * q + 4 * t + j] = y;
       }
     PDG_FENCE();
   }
 }
 
-// v[s] = relu(acc[s] + bias[64h + s]), two fenced chunks.
-__device__ __forceinline__ void bias_relu(float (&v)[64], const f32x16 (&acc)[4], const float* __restrict__ bias) {
-  const f32x4* bp = reinterpret_cast<const f32x4*>(bias + half_off());
+// v[s] = relu(acc[s] + bias[32q + s]).
+__device__ __forceinline__ void bias_relu(float (&v)[FRAG], const Acc& acc, const float* __restrict__ bias) {
+  const f32x4* bp = reinterpret_cast<const f32x4*>(bias + quarter_off());
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
+  for (int t = 0; t < 8; ++t) {
     const f32x4 bb = bp[t];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) v[4 * t + j] = fmaxf(ACC(acc, 4 * t + j) + bb[j], 0.f);
-    if (t == 7) PDG_FENCE();
+    for (int j = 0; j < 4; ++j) v[4 * t + j] = fmaxf(acc.b[t][j] + bb[j], 0.f);
   }
 }
 
 // ============================================================================ encoder
 // models.py:260-274.  W2 in LDS (A-image); W0 (128 x IN) and b0 appended.
 template <int IN>
-__global__ __launch_bounds__(256, 2) void encoder_kernel(int M, const float* __restrict__ x_in,
+__global__ __launch_bounds__(384, 3) void encoder_kernel(int M, const float* __restrict__ x_in,
                                                           const float* __restrict__ W0,
                                                           const float* __restrict__ b0,
                                                           const float* __restrict__ W2,
@@ -159,24 +165,22 @@ __global__ __launch_bounds__(256, 2) void encoder_kernel(int M, const float* __r
   for (int i = threadIdx.x; i < 128 * IN; i += blockDim.x) w0l[i] = W0[i];
   for (int i = threadIdx.x; i < 128; i += blockDim.x) b0l[i] = b0[i];
   __syncthreads();
-  const int l = lane_id(), h = l >> 5;
-  const int nw = blockDim.x >> 6;
+  const int l = lane_id();
   double s1 = 0, s2 = 0;
-  const int ntiles = tiles_of(M);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(M) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < M;
     const int rc = valid ? row : M - 1;
     float xi[IN];
 #pragma unroll
     for (int i = 0; i < IN; ++i) xi[i] = x_in[(size_t)rc * IN + i];
-    float v[64];
-    const int ho = half_off();
+    float v[FRAG];
+    const int qo = quarter_off();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < 2; ++q) {
 #pragma unroll
       for (int s = 16 * q; s < 16 * q + 16; ++s) {
-        const int o = ho + s;
+        const int o = qo + s;
         float d = 0.f;
 #pragma unroll
         for (int i = 0; i < IN; ++i) d = fmaf(w0l[o * IN + i], xi[i], d);
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(256, 2) void encoder_kernel(int M, const float* __r
       PDG_FENCE();
     }
     if (valid) store_frag(a1 + (size_t)row * L, v);
-    f32x16 acc[4];
+    Acc acc;
     zero_acc(acc);
     gemm128(acc, lds, v);
     bias_relu(v, acc, b2);
@@ -202,13 +206,13 @@ extern "C" int pdg_encoder_fwd(int rows, int in_features, const float* x_in, con
   PDG_CHECK_ARG(in_features == 1 || in_features == 6, "pdg_encoder_fwd: in_features must be 1 or 6");
   PDG_CHECK_ARG(PDG_ALIGNED(a1) && PDG_ALIGNED(a2) && PDG_ALIGNED(W2) && PDG_ALIGNED(b2),
                 "pdg_encoder_fwd: misaligned pointer");
-  const int grid = persistent_grid(rows, 4, 2);
+  const int grid = persistent_grid(rows, 6, 2);
   const size_t shm = (size_t)(WBLK + 128 * in_features + 128) * sizeof(float);
   if (in_features == 6)
-    hipLaunchKernelGGL(encoder_kernel<6>, dim3(grid), dim3(256), shm, (hipStream_t)stream, rows, x_in, W0,
+    hipLaunchKernelGGL(encoder_kernel<6>, dim3(grid), dim3(384), shm, (hipStream_t)stream, rows, x_in, W0,
                        b0, W2, b2, a1, a2, partials);
   else
-    hipLaunchKernelGGL(encoder_kernel<1>, dim3(grid), dim3(256), shm, (hipStream_t)stream, rows, x_in, W0,
+    hipLaunchKernelGGL(encoder_kernel<1>, dim3(grid), dim3(384), shm, (hipStream_t)stream, rows, x_in, W0,
                        b0, W2, b2, a1, a2, partials);
   PDG_CHECK_LAUNCH("pdg_encoder_fwd");
   if (nparts) *nparts = grid;
@@ -250,7 +254,7 @@ extern "C" int pdg_ln_finalize(const double* partials, int nparts, double count,
 
 // ============================================================================ node P/Q pre-pass
 template <bool RES>
-__global__ __launch_bounds__(512, 2) void node_pq_kernel(int N, const float* __restrict__ a2p,
+__global__ __launch_bounds__(768, 3) void node_pq_kernel(int N, const float* __restrict__ a2p,
                                                           const pdg_ln_stat* __restrict__ stp,
                                                           const float* __restrict__ lg,
                                                           const float* __restrict__ lb,
@@ -264,16 +268,14 @@ __global__ __launch_bounds__(512, 2) void node_pq_kernel(int N, const float* __r
   __syncthreads();
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(N);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(N) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < N;
     const int rc = valid ? row : N - 1;
-    float v[64];
+    float v[FRAG];
     ln_res_frag<RES>(v, a2p + (size_t)rc * L, RES ? xres + (size_t)rc * L : nullptr, st, lg, lb);
     if (valid) store_frag(xout + (size_t)row * L, v);
-    f32x16 acc[4];
+    Acc acc;
     zero_acc(acc);
     gemm128(acc, lds, v);
     if (valid) store_acc(P + (size_t)row * L, acc);
@@ -290,12 +292,12 @@ extern "C" int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat*
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(x_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
                     PDG_ALIGNED(W1) && (!x_res || PDG_ALIGNED(x_res)),
                 "pdg_node_pq: misaligned pointer");
-  const int grid = persistent_grid(n_nodes, 8, 1);
+  const int grid = persistent_grid(n_nodes, 12, 1);
   if (x_res)
-    hipLaunchKernelGGL(node_pq_kernel<true>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+    hipLaunchKernelGGL(node_pq_kernel<true>, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream,
                        n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q);
   else
-    hipLaunchKernelGGL(node_pq_kernel<false>, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+    hipLaunchKernelGGL(node_pq_kernel<false>, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream,
                        n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q);
   PDG_CHECK_LAUNCH("pdg_node_pq");
   return PDG_OK;
@@ -303,46 +305,45 @@ extern "C" int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat*
 
 // ============================================================================ fused edge pass
 // First layer of both edge_net evaluations from the shared C = W_c e + b1, in
-// four fenced 16-float chunks aligned with the accumulator tuples C[q] (each
-// tuple dies as its chunk is consumed):
-//   edge update: relu(C + P[src] + Q[dst]) -> stored to a1e
+// four fenced chunks of 8 floats (each accumulator block pair dies as its chunk
+// is consumed):
+//   edge update: relu(C + P[src] + Q[dst]) -> stored to a1e (when EU)
 //   message:     relu(C + P[dst] + Q[src]) -> v (and stored to a1m by the caller)
 template <bool EU>
-__device__ __forceinline__ void first_layers(float (&v)[64], const f32x16 (&C)[4], const float* __restrict__ ps,
+__device__ __forceinline__ void first_layers(float (&v)[FRAG], const Acc& C, const float* __restrict__ ps,
                                              const float* __restrict__ qd, const float* __restrict__ pd,
                                              const float* __restrict__ qs, float* __restrict__ a1e_row,
                                              bool valid) {
-  const int ho = half_off();
+  const int qo = quarter_off();
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < 4; ++q) {
     f32x4 xs[2], yd[2], xd[2], ys[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (EU) {
-        xs[t] = reinterpret_cast<const f32x4*>(ps + ho + 8 * q)[t];
-        yd[t] = reinterpret_cast<const f32x4*>(qd + ho + 8 * q)[t];
+        xs[t] = reinterpret_cast<const f32x4*>(ps + qo + 8 * q)[t];
+        yd[t] = reinterpret_cast<const f32x4*>(qd + qo + 8 * q)[t];
       }
-      xd[t] = reinterpret_cast<const f32x4*>(pd + ho + 8 * q)[t];
-      ys[t] = reinterpret_cast<const f32x4*>(qs + ho + 8 * q)[t];
+      xd[t] = reinterpret_cast<const f32x4*>(pd + qo + 8 * q)[t];
+      ys[t] = reinterpret_cast<const f32x4*>(qs + qo + 8 * q)[t];
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       f32x4 e;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int s = 8 * q + 4 * t + j;
-        const float c = ACC(C, s);
+        const float c = C.b[2 * q + t][j];
         if (EU) e[j] = fmaxf((c + xs[t][j]) + yd[t][j], 0.f);
-        v[s] = fmaxf((c + xd[t][j]) + ys[t][j], 0.f);
+        v[8 * q + 4 * t + j] = fmaxf((c + xd[t][j]) + ys[t][j], 0.f);
       }
-      if (EU && valid) reinterpret_cast<f32x4*>(a1e_row + ho + 8 * q)[t] = e;
+      if (EU && valid) reinterpret_cast<f32x4*>(a1e_row + qo + 8 * q)[t] = e;
     }
     PDG_FENCE();
   }
 }
 
 template <bool RES, bool EU>
-__global__ __launch_bounds__(512, 2) void edge_fwd_kernel(
+__global__ __launch_bounds__(768, 3) void edge_fwd_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
     const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ P,
@@ -356,37 +357,31 @@ __global__ __launch_bounds__(512, 2) void edge_fwd_kernel(
   __syncthreads();
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(E);
   double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(E) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < E;
     const int rc = valid ? row : E - 1;
     const int s_node = src[rc], d_node = dst[rc];
-    float v[64];
+    float v[FRAG];
     // e_t = LN(a2_prev) + e_res   (models.py:225 residual of the previous step)
     ln_res_frag<RES>(v, a2p + (size_t)rc * L, RES ? eres + (size_t)rc * L : nullptr, st, lg, lb);
     if (valid) store_frag(eout + (size_t)row * L, v);
     // C = W_c e_t + b1 (shared by both edge_net evaluations)
-    f32x16 C[4];
+    Acc C;
     zero_acc(C);
     gemm128(C, lds, v);
     {
-      const f32x4* bp = reinterpret_cast<const f32x4*>(b1 + half_off());
+      const f32x4* bp = reinterpret_cast<const f32x4*>(b1 + quarter_off());
 #pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        const f32x4 bb = bp[t];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ACC(C, 4 * t + j) += bb[j];
-      }
+      for (int t = 0; t < 8; ++t) C.b[t] += bp[t];
     }
     // layer 1 of the edge update (models.py:219-222, x[row] = x[src], x[col] = x[dst]; stored,
     // re-read below) and of the message (models.py:233-238, x_i = x[dst], x_j = x[src])
     first_layers<EU>(v, C, P + (size_t)s_node * L, Q + (size_t)d_node * L, P + (size_t)d_node * L,
                      Q + (size_t)s_node * L, EU ? a1e + (size_t)row * L : nullptr, valid);
     if (valid) store_frag(a1m + (size_t)row * L, v);
-    f32x16 Z[4];
+    Acc Z;
     zero_acc(Z);
     gemm128(Z, lds + WBLK, v);
     bias_relu(v, Z, b2);
@@ -417,11 +412,11 @@ extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat
                 "pdg_edge_fwd: misaligned pointer");
   PDG_CHECK_ARG(!with_edge_update || (a1e && a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd: edge-update outputs missing or misaligned");
-  const int grid = persistent_grid(n_edges, 8, 1);
+  const int grid = persistent_grid(n_edges, 12, 1);
   const size_t shm = 2 * WBLK * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
 #define PDG_EDGE_FWD(R, U)                                                                                     \
-  hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(512), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \
+  hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(768), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \
                      e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e)
   if (e_res) {
     if (with_edge_update) PDG_EDGE_FWD(true, true); else PDG_EDGE_FWD(true, false);
@@ -508,7 +503,7 @@ extern "C" int pdg_segment_sum(int n_nodes, const int* rowptr, const float* rows
 }
 
 // ============================================================================ node MLP layer 1
-__global__ __launch_bounds__(512, 2) void node_mlp1_kernel(int N, const float* __restrict__ aggr,
+__global__ __launch_bounds__(768, 3) void node_mlp1_kernel(int N, const float* __restrict__ aggr,
                                                             const float* __restrict__ x,
                                                             const float* __restrict__ Wn1,
                                                             const float* __restrict__ bn1,
@@ -518,14 +513,12 @@ __global__ __launch_bounds__(512, 2) void node_mlp1_kernel(int N, const float* _
   load_wblock(lds + WBLK, Wn1, 2 * L, L);   // x block
   __syncthreads();
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(N);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(N) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < N;
     const int rc = valid ? row : N - 1;
-    float v[64];
-    f32x16 acc[4];
+    float v[FRAG];
+    Acc acc;
     zero_acc(acc);
     load_frag(v, aggr + (size_t)rc * L);
     gemm128(acc, lds, v);
@@ -541,15 +534,15 @@ extern "C" int pdg_node_mlp1(int n_nodes, const float* aggr, const float* x, con
   PDG_CHECK_ARG(n_nodes > 0, "pdg_node_mlp1: n_nodes must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(aggr) && PDG_ALIGNED(x) && PDG_ALIGNED(a1n) && PDG_ALIGNED(Wn1),
                 "pdg_node_mlp1: misaligned pointer");
-  const int grid = persistent_grid(n_nodes, 8, 1);
-  hipLaunchKernelGGL(node_mlp1_kernel, dim3(grid), dim3(512), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+  const int grid = persistent_grid(n_nodes, 12, 1);
+  hipLaunchKernelGGL(node_mlp1_kernel, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream,
                      n_nodes, aggr, x, Wn1, bn1, a1n);
   PDG_CHECK_LAUNCH("pdg_node_mlp1");
   return PDG_OK;
 }
 
 // ============================================================================ MLP layer 2 (+ LN partials)
-__global__ __launch_bounds__(256, 2) void mlp2_fwd_kernel(int M, const float* __restrict__ a1,
+__global__ __launch_bounds__(384, 3) void mlp2_fwd_kernel(int M, const float* __restrict__ a1,
                                                            const float* __restrict__ W2,
                                                            const float* __restrict__ b2,
                                                            float* __restrict__ a2, double* __restrict__ part) {
@@ -557,16 +550,14 @@ __global__ __launch_bounds__(256, 2) void mlp2_fwd_kernel(int M, const float* __
   load_wblock(lds, W2, L, 0);
   __syncthreads();
   const int l = lane_id();
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(M);
   double s1 = 0, s2 = 0;
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  PDG_TILE_LOOP(M) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < M;
     const int rc = valid ? row : M - 1;
-    float v[64];
+    float v[FRAG];
     load_frag(v, a1 + (size_t)rc * L);
-    f32x16 acc[4];
+    Acc acc;
     zero_acc(acc);
     gemm128(acc, lds, v);
     bias_relu(v, acc, b2);
@@ -580,8 +571,8 @@ extern "C" int pdg_mlp2_fwd(int rows, const float* a1, const float* W2, const fl
                             double* partials, int* nparts, void* stream) {
   PDG_CHECK_ARG(rows > 0, "pdg_mlp2_fwd: rows must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(a1) && PDG_ALIGNED(a2) && PDG_ALIGNED(W2), "pdg_mlp2_fwd: misaligned pointer");
-  const int grid = persistent_grid(rows, 4, 2);
-  hipLaunchKernelGGL(mlp2_fwd_kernel, dim3(grid), dim3(256), WBLK * sizeof(float), (hipStream_t)stream, rows,
+  const int grid = persistent_grid(rows, 6, 2);
+  hipLaunchKernelGGL(mlp2_fwd_kernel, dim3(grid), dim3(384), WBLK * sizeof(float), (hipStream_t)stream, rows,
                      a1, W2, b2, a2, partials);
   PDG_CHECK_LAUNCH("pdg_mlp2_fwd");
   if (nparts) *nparts = grid;
@@ -589,7 +580,7 @@ extern "C" int pdg_mlp2_fwd(int rows, const float* a1, const float* W2, const fl
 }
 
 // ============================================================================ decoder
-__global__ __launch_bounds__(256, 2) void decoder_kernel(int N, const float* __restrict__ a2p,
+__global__ __launch_bounds__(384, 3) void decoder_kernel(int N, const float* __restrict__ a2p,
                                                           const pdg_ln_stat* __restrict__ stp,
                                                           const float* __restrict__ lg,
                                                           const float* __restrict__ lb,
@@ -608,39 +599,42 @@ __global__ __launch_bounds__(256, 2) void decoder_kernel(int N, const float* __r
   for (int i = threadIdx.x; i < 3 * L; i += blockDim.x) w2l[i] = Wd2[i];
   __syncthreads();
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
-  const int l = lane_id(), h = l >> 5;
-  const int nw = blockDim.x >> 6;
-  const int ntiles = tiles_of(N);
-  for (int tile = blockIdx.x * nw + wave_id(); tile < ntiles; tile += gridDim.x * nw) {
-    const int row = tile * 32 + (l & 31);
+  const int l = lane_id(), q = l >> 4;
+  PDG_TILE_LOOP(N) {
+    const int row = tile * TILE + (l & 15);
     const bool valid = row < N;
     const int rc = valid ? row : N - 1;
-    float v[64];
+    float v[FRAG];
     ln_res_frag<true>(v, a2p + (size_t)rc * L, xres + (size_t)rc * L, st, lg, lb);
     if (valid) store_frag(xout + (size_t)row * L, v);
-    f32x16 acc[4];
+    Acc acc;
     zero_acc(acc);
     gemm128(acc, lds, v);
     bias_relu(v, acc, bd1);
     if (valid) store_frag(a1d + (size_t)row * L, v);
-    // Linear(128 -> 3): half-row partial dots, combined across the two lane halves
+    // Linear(128 -> 3): quarter-row partial dots, combined across the four lane quarters
     float o3[3];
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
-      const float* wp = w2l + o * L + half_off();
+      const float* wp = w2l + o * L + quarter_off();
       float d = 0.f;
 #pragma unroll
-      for (int s = 0; s < 64; ++s) d = fmaf(wp[s], v[s], d);
+      for (int s = 0; s < FRAG; ++s) d = fmaf(wp[s], v[s], d);
       o3[o] = d;
       PDG_FENCE();
     }
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
-      const float other = __shfl_xor(o3[o], 32);
-      o3[o] = (h == 0 ? o3[o] + other : other + o3[o]) + bd2[o];
-      if (scale) o3[o] = o3[o] * st8[5] + st8[4];
+      // fixed combination order (q0 + q1) + (q2 + q3) in every lane
+      const float x1 = __shfl_xor(o3[o], 16);
+      const float lo = (q & 1) ? x1 + o3[o] : o3[o] + x1;     // pair (0,1) or (2,3)
+      const float x2 = __shfl_xor(lo, 32);
+      float r = (q & 2) ? x2 + lo : lo + x2;
+      r = r + bd2[o];
+      if (scale) r = r * st8[5] + st8[4];
+      o3[o] = r;
     }
-    if (valid && h == 0) {
+    if (valid && q == 0) {
       y[(size_t)row * 3 + 0] = o3[0];
       y[(size_t)row * 3 + 1] = o3[1];
       y[(size_t)row * 3 + 2] = o3[2];
@@ -658,9 +652,9 @@ extern "C" int pdg_decoder_fwd(int n_nodes, const float* a2_prev, const pdg_ln_s
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(x_res) && PDG_ALIGNED(x_out) && PDG_ALIGNED(a1d) &&
                     PDG_ALIGNED(Wd1) && PDG_ALIGNED(Wd2),
                 "pdg_decoder_fwd: misaligned pointer");
-  const int grid = persistent_grid(n_nodes, 4, 2);
-  hipLaunchKernelGGL(decoder_kernel, dim3(grid), dim3(256), (WBLK + 3 * L) * sizeof(float), (hipStream_t)stream, n_nodes,
-                     a2_prev, st, ln_g, ln_b, x_res, x_out, Wd1, bd1, a1d, Wd2, bd2, stats8, scale_output, y);
+  const int grid = persistent_grid(n_nodes, 6, 2);
+  hipLaunchKernelGGL(decoder_kernel, dim3(grid), dim3(384), (WBLK + 3 * L) * sizeof(float), (hipStream_t)stream,
+                     n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, Wd1, bd1, a1d, Wd2, bd2, stats8, scale_output, y);
   PDG_CHECK_LAUNCH("pdg_decoder_fwd");
   return PDG_OK;
 }

@@ -32,7 +32,8 @@ constexpr int MAX_BLOCKS = 2048;
 
 #define PDG_ALIGNED(p) ((((uintptr_t)(p)) & 15u) == 0)
 
-__host__ __device__ inline int tiles_of(long rows) { return (int)((rows + 31) / 32); }
+// Wave tiles of 16 rows (pdg_common.hpp).
+__host__ __device__ inline int tiles_of(long rows) { return (int)((rows + 15) / 16); }
 
 // Persistent grid: enough blocks to cover the tiles, at most `per_cu` blocks per CU.
 inline int persistent_grid(long rows, int waves_per_block, int per_cu) {

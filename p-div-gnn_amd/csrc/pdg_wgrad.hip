@@ -17,6 +17,14 @@
 using namespace pdg;
 
 constexpr int SLAB = L * L + L;   // floats per slab
+typedef float f32x16 __attribute__((ext_vector_type(16)));   // v_mfma_f32_32x32x2_f32 accumulator
+
+__device__ __forceinline__ void zero_acc16(f32x16 (&acc)[4]) {
+#pragma unroll
+  for (int nb = 0; nb < 4; ++nb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[nb][r] = 0.f;
+}
 
 __device__ __forceinline__ void wgrad_pass(int M, int r0, int r1, const float* __restrict__ G,
                                            const float* __restrict__ X, f32x16 (&acc)[4], double& bsum) {
@@ -66,7 +74,7 @@ __global__ __launch_bounds__(256) void wgrad_accum_kernel(int M, const float* __
   const int r0 = (int)min((long)M, chunk * blockIdx.x);
   const int r1 = (int)min((long)M, chunk * (blockIdx.x + 1));
   f32x16 acc[4];
-  zero_acc(acc);
+  zero_acc16(acc);
   double bsum = 0;
   wgrad_pass(M, r0, r1, G, X, acc, bsum);
   if (G2) wgrad_pass(M, r0, r1, G2, X2, acc, bsum);
