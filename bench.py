@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """P-DivGNN training throughput on MI355X: mesh-nodes/sec (fwd+bwd), 1..8 GPUs.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 A step is one full training step of the reference's hot loop
@@ -12,7 +12,9 @@ gradient bucket (N > 1) and the Adam update — all on the HIP kernels of
 libpdivgnn_hip.so.  Workload per GPU (weak scaling, graph-level data
 parallelism): BASELINE.json configs[1] = 8 synthetic periodic triangulated
 71x71 meshes (5,041 nodes, 29,968 edges each).  value = nodes processed by all
-ranks / max-over-ranks wall time.
+ranks / max-over-ranks wall time.  --config 5 times inference instead (one
+forward of a 100k-node mesh, 15 layers, model.forward under no_grad as
+gnn_inference.py calls it; metric mesh-nodes/sec (inference)).
 
 Also reported: the roofline of the dominant kernel (HIP events around its
 launches inside the timed region) and the reference algorithm's CPU path (the
@@ -44,6 +46,8 @@ CONFIGS = {
             graphs=32, n=71, hole=(0.0, 0.0), divergence=True, steps=10),
     4: dict(workload="P-DivGNN hole plates, 8 x ~4.8k-node meshes per GPU (global batch 8*N)",
             graphs=8, n=71, hole=(0.08, 0.12), divergence=True, steps=10),
+    5: dict(workload="inference, one synthetic 100,489-node periodic mesh per GPU, 15 MP layers (BASELINE configs[4])",
+            graphs=1, n=317, hole=(0.0, 0.0), divergence=False, steps=15, inference=True),
 }
 
 
@@ -76,7 +80,13 @@ def cpu_baseline(cfg, samples, seconds: float = 20.0):
     args = (b.pos, b.mean_stress, b.nodes_types, b.edge_index, b.edge_attr)
     gt = (b.local_stress - st["mean_local_stress"]) / st["std_local_stress"]
 
+    infer = cfg.get("inference", False)
+
     def step():
+        if infer:
+            with torch.no_grad():
+                O.epd_forward(P, st, *args, cfg["steps"], scale_output=True)
+            return
         pred = O.epd_forward(P, st, *args, cfg["steps"], scale_output=False)
         total, _, _ = O.batch_loss(pred, gt, b.ptr, [d.op_div_matrix], b.nodes_types, cfg["divergence"], 10.0)
         for p in P.values():
@@ -91,9 +101,9 @@ def cpu_baseline(cfg, samples, seconds: float = 20.0):
         el = time.perf_counter() - t0
         if el > seconds or n >= 50:
             break
+    what = "inference forwards" if infer else f"training steps (fwd+NMSE{'+div' if cfg['divergence'] else ''}+bwd)"
     return {"value": round(n * d.num_nodes / el, 1), "unit": "nodes/s", "cores": threads, "kind": "port",
-            "sample": f"{n} training steps (fwd+NMSE{'+div' if cfg['divergence'] else ''}+bwd) of one "
-                      f"{d.num_nodes}-node graph, {cfg['steps']} MP steps, fp32, torch CPU "
+            "sample": f"{n} {what} of one {d.num_nodes}-node graph, {cfg['steps']} MP steps, fp32, torch CPU "
                       f"({threads} threads), oracle/epd_oracle.py"}
 
 
@@ -136,8 +146,16 @@ def main():
     plan = plan_for(batch)
     N, E = plan.n_nodes, plan.n_edges
 
+    infer = cfg.get("inference", False)
+    if infer:
+        def run_step():
+            with torch.no_grad():
+                return {"total": model(batch, scale_output=True).local_stress.abs().mean()}
+    else:
+        def run_step():
+            return trainer.step(batch)
     for _ in range(args.warmup):
-        trainer.step(batch)
+        run_step()
     torch.cuda.synchronize()
     eng = trainer.engine
     timed_kernels = ["edge_fwd", "edge_bwd", "wgrad_W2", "segment_sum", "pq_scatter_bwd"]
@@ -147,7 +165,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = trainer.step(batch)
+        out = run_step()
     torch.cuda.synchronize()
     if pg is not None:
         dist.barrier()
@@ -160,7 +178,8 @@ def main():
         el = float(t)
     loss = float(out["total"])
 
-    kt = {k: sum(a.elapsed_time(b) for a, b in v) / max(len(v), 1) * 1e-3 for k, v in ev.items()}
+    ev = {k: v for k, v in ev.items() if v}
+    kt = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) * 1e-3 for k, v in ev.items()}
     ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
     S = cfg["steps"]
     # algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops and the bytes the
@@ -193,10 +212,11 @@ def main():
                 "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4), "frac_hbm": round(f_hbm, 4),
                 "avg_launch_ms": round(t * 1e3, 4), "share_of_step": round(ktot[k] / el, 4)}
 
-    dominant = max(["edge_fwd", "edge_bwd", "wgrad_W2"], key=lambda k: ktot[k])
+    dominant = max([k for k in ("edge_fwd", "edge_bwd", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])
     if rank == 0:
         res = {
-            "metric": "mesh-nodes/sec (fwd+bwd) on periodic FEM graphs",
+            "metric": ("mesh-nodes/sec (inference) on periodic FEM graphs" if infer
+                       else "mesh-nodes/sec (fwd+bwd) on periodic FEM graphs"),
             "value": round(world * N * args.steps / el, 1),
             "unit": "nodes/s",
             "n_gpus": world,
@@ -213,7 +233,7 @@ def main():
                        "message_passing_steps": cfg["steps"], "latent": L, "divergence": cfg["divergence"],
                        "parallelism": f"graph-DP x{world}", "final_loss": round(loss, 6)},
             "roofline": roof(dominant),
-            "roofline_gather_scatter": [roof("segment_sum"), roof("pq_scatter_bwd")],
+            "roofline_gather_scatter": [roof(k) for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
             "kernel_ms": {k: round(v * 1e3, 4) for k, v in kt.items()},
         }
         if world == 1 and not args.no_cpu_baseline:

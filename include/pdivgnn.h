@@ -137,7 +137,8 @@ int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* rowptr, cons
                         double* partials, int* nparts, void* stream);
 
 /* Reduce colsum partials: grad_b += sum gy, grad_g += sum gy*xhat, and the call's
- * backward scalars (S1 = sum g*gy, S2 = sum g*gy*xhat). */
+ * backward scalars (S1 = sum g*gy, S2 = sum g*gy*xhat).  Row nparts of `partials`
+ * (256 doubles after the last partial) is used as scratch. */
 int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g,
                            const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
                            void* stream);

@@ -193,38 +193,41 @@ extern "C" int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* r
   return PDG_OK;
 }
 
-// 1024 threads: column c (of 256: 128 sum-gy, 128 sum-gy*xhat) by 4 threads, each
-// summing every 4th block partial; the 4 are combined in a fixed order.
-__global__ __launch_bounds__(1024) void ln_colsum_finalize_kernel(const double* __restrict__ part, int n,
-                                                                  const float* __restrict__ g,
-                                                                  const pdg_ln_stat* __restrict__ stp,
-                                                                  float* __restrict__ grad_g,
-                                                                  float* __restrict__ grad_b,
-                                                                  pdg_ln_bwd* __restrict__ out) {
-  __shared__ double red[4][256];
-  __shared__ double red2[2 * 16];
-  const int col = threadIdx.x & 255, q = threadIdx.x >> 8;
-  double s0 = 0, s1_ = 0, s2_ = 0, s3 = 0;
-  int b = q;
-  for (; b + 12 < n; b += 16) {
-    s0 += part[(size_t)b * 256 + col];
-    s1_ += part[(size_t)(b + 4) * 256 + col];
-    s2_ += part[(size_t)(b + 8) * 256 + col];
-    s3 += part[(size_t)(b + 12) * 256 + col];
-  }
-  for (; b < n; b += 4) s0 += part[(size_t)b * 256 + col];
-  red[q][col] = (s0 + s1_) + (s2_ + s3);
+// Two-level reduction of the per-block partials (P x 256 doubles): one block per
+// column sums its P partials with 256 threads and a fixed-order tree, then a
+// single block turns the 256 column sums into parameter gradients and S1/S2.
+__device__ __forceinline__ double block_tree_sum(double x, double* red) {
+  red[threadIdx.x] = x;
   __syncthreads();
-  double s1 = 0, s2 = 0;
-  if (threadIdx.x < 128) {
-    const int c = threadIdx.x;
-    const double sg = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
-    const double sx = (red[0][128 + c] + red[1][128 + c]) + (red[2][128 + c] + red[3][128 + c]);
-    if (grad_b) grad_b[c] += (float)sg;
-    if (grad_g) grad_g[c] += (float)sx;
-    s1 = (double)g[c] * sg;
-    s2 = (double)g[c] * sx;
+  for (int o = blockDim.x >> 1; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
   }
+  return red[0];
+}
+
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const double* __restrict__ part, int n, int width,
+                                                            double* __restrict__ out) {
+  __shared__ double red[256];
+  const int col = blockIdx.x;
+  double s = 0;
+  for (int b = threadIdx.x; b < n; b += blockDim.x) s += part[(size_t)b * width + col];
+  const double t = block_tree_sum(s, red);
+  if (threadIdx.x == 0) out[col] = t;
+}
+
+__global__ __launch_bounds__(128) void ln_colsum_finalize_kernel(const double* __restrict__ cols,
+                                                                 const float* __restrict__ g,
+                                                                 const pdg_ln_stat* __restrict__ stp,
+                                                                 float* __restrict__ grad_g,
+                                                                 float* __restrict__ grad_b,
+                                                                 pdg_ln_bwd* __restrict__ out) {
+  __shared__ double red2[2 * 16];
+  const int c = threadIdx.x;
+  const double sg = cols[c], sx = cols[128 + c];
+  if (grad_b) grad_b[c] += (float)sg;
+  if (grad_g) grad_g[c] += (float)sx;
+  double s1 = (double)g[c] * sg, s2 = (double)g[c] * sx;
   block_sum2(s1, s2, red2);
   if (threadIdx.x == 0) {
     const double M = stp->count;
@@ -241,9 +244,13 @@ __global__ __launch_bounds__(1024) void ln_colsum_finalize_kernel(const double* 
 extern "C" int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g,
                                       const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
                                       void* stream) {
-  PDG_CHECK_ARG(nparts > 0, "pdg_ln_colsum_finalize: no partials");
-  hipLaunchKernelGGL(ln_colsum_finalize_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, partials, nparts, ln_g,
-                     st, grad_g, grad_b, out);
+  PDG_CHECK_ARG(nparts > 0 && nparts < MAX_BLOCKS, "pdg_ln_colsum_finalize: bad nparts");
+  // the 256 column sums go into the row right after the last partial (see the header)
+  double* cols = const_cast<double*>(partials) + (size_t)nparts * 256;
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(256), dim3(256), 0, (hipStream_t)stream, partials, nparts, 256, cols);
+  PDG_CHECK_LAUNCH("pdg_ln_colsum_finalize(reduce)");
+  hipLaunchKernelGGL(ln_colsum_finalize_kernel, dim3(1), dim3(128), 0, (hipStream_t)stream, cols, ln_g, st, grad_g,
+                     grad_b, out);
   PDG_CHECK_LAUNCH("pdg_ln_colsum_finalize");
   return PDG_OK;
 }

@@ -181,14 +181,24 @@ __global__ __launch_bounds__(256) void wgrad_narrow_kernel(int M, const float* _
   }
 }
 
-__global__ void wgrad_narrow_finalize_kernel(const double* __restrict__ part, int n, int K, int transpose,
-                                             float* __restrict__ gW, float* __restrict__ gbw,
-                                             float* __restrict__ gbn) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+// One block per output element: 256 threads sum the per-block partials, fixed-order tree.
+__global__ __launch_bounds__(256) void wgrad_narrow_finalize_kernel(const double* __restrict__ part, int n, int K,
+                                                                    int transpose, float* __restrict__ gW,
+                                                                    float* __restrict__ gbw,
+                                                                    float* __restrict__ gbn) {
+  __shared__ double red[256];
+  const int e = blockIdx.x;
   const int tot = L * K + L + K;
-  if (e >= tot) return;
   double s = 0;
-  for (int b = 0; b < n; ++b) s += part[(size_t)b * tot + e];
+  for (int b = threadIdx.x; b < n; b += blockDim.x) s += part[(size_t)b * tot + e];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = blockDim.x >> 1; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  s = red[0];
   if (e < L * K) {
     const int c = e / K, i = e % K;
     if (transpose) gW[i * L + c] += (float)s;
@@ -218,8 +228,8 @@ extern "C" int pdg_wgrad_narrow(int rows, const float* wide, const float* narrow
     hipLaunchKernelGGL(wgrad_narrow_kernel<6>, dim3(grid), dim3(256), 0, s, rows, wide, narrow, partials);
   PDG_CHECK_LAUNCH("pdg_wgrad_narrow");
   const int tot = L * k_narrow + L + k_narrow;
-  hipLaunchKernelGGL(wgrad_narrow_finalize_kernel, dim3((tot + 255) / 256), dim3(256), 0, s, partials, grid,
-                     k_narrow, transpose, grad_W, grad_b_wide, grad_b_narrow);
+  hipLaunchKernelGGL(wgrad_narrow_finalize_kernel, dim3(tot), dim3(256), 0, s, partials, grid, k_narrow, transpose,
+                     grad_W, grad_b_wide, grad_b_narrow);
   PDG_CHECK_LAUNCH("pdg_wgrad_narrow(finalize)");
   return PDG_OK;
 }

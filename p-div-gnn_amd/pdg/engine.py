@@ -171,7 +171,7 @@ class EPDEngine:
             e_t = self._empty(E, L)
             a1m, a2m = self._empty(E, L), self._empty(E, L)
             a1e, a2e = (self._empty(E, L), self._empty(E, L)) if eu else (None, None)
-            self._t("edge_fwd", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
+            self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
                     _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
                     _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
             self._finalize(self._part_a, E * L, st[i_m], s)
@@ -288,7 +288,7 @@ class EPDEngine:
             if eu:
                 colsum(E, ge_next, None, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
                        "processor.edge_net.4.bias", lb[2])
-            self._t("edge_bwd", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr), _p(ge_next), _p(d["a2m"]),
+            self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr), _p(ge_next), _p(d["a2m"]),
                     _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]], st[d["i_e"]] if eu else None, lb[1],
                     lb[2] if eu else None, _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]),
                     _p(gz2m), _p(gz1m), _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), s)
