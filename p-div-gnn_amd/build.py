@@ -15,11 +15,14 @@ import sys
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-CSRC = HERE / "csrc"
-OUT = HERE / "pdg" / "libpdivgnn_hip.so"
-BUILD = HERE / "build"
+CSRC = Path(os.environ.get("PDG_CSRC", HERE / "csrc"))
+# PDG_OUT / PDG_BUILD_DIR / PDG_EXTRA_FLAGS build side-by-side variants for A/B timing
+# (loaded with PDG_LIB=...); the default build is the shipped library.
+OUT = Path(os.environ.get("PDG_OUT", HERE / "pdg" / "libpdivgnn_hip.so"))
+BUILD = Path(os.environ.get("PDG_BUILD_DIR", HERE / "build"))
 ARCH = os.environ.get("PDG_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         *os.environ.get("PDG_EXTRA_FLAGS", "").split()]
 
 
 def hipcc() -> str:
@@ -31,7 +34,7 @@ def hipcc() -> str:
 
 def _compile(src: Path, report: bool) -> Path:
     obj = BUILD / (src.stem + ".o")
-    deps = [src] + list(CSRC.glob("*.hpp")) + [HERE.parent / "include" / "pdivgnn.h"]
+    deps = [src] + list(CSRC.glob("*.hpp")) + [CSRC.parent.parent / "include" / "pdivgnn.h"]
     if obj.exists() and all(obj.stat().st_mtime >= d.stat().st_mtime for d in deps) and not report:
         return obj
     cmd = [hipcc(), *FLAGS, "-c", str(src), "-o", str(obj)]
@@ -46,7 +49,8 @@ def _compile(src: Path, report: bool) -> Path:
 
 
 def build(force: bool = False, report: bool = False) -> Path:
-    BUILD.mkdir(exist_ok=True)
+    BUILD.mkdir(parents=True, exist_ok=True)
+    OUT.parent.mkdir(parents=True, exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip"))
     if force:
         for o in BUILD.glob("*.o"):

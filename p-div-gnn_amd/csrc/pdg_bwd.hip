@@ -13,18 +13,13 @@
 
 using namespace pdg;
 
-#define PDG_TILE_LOOP(M)                                                              \
-  const int nw_ = blockDim.x >> 6;                                                    \
-  const int ntiles_ = tiles_of(M);                                                    \
-  for (int tile = blockIdx.x * nw_ + wave_id(); tile < ntiles_; tile += gridDim.x * nw_)
-
 // ga2 -> gz2 for one fragment (in place on gy): LN backward and relu mask.
 __device__ __forceinline__ void ln_relu_bwd(float (&gy)[FRAG], const float (&a2)[FRAG], const LNStat& st,
                                             const pdg_ln_bwd& lb, const float* __restrict__ g) {
-  const f32x4* gp = reinterpret_cast<const f32x4*>(g + quarter_off());
+  const float* gp = g + lane_col();
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-    const f32x4 gg = gp[t];
+    const f32x4 gg = ld4(gp, t);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int s = 4 * t + j;
@@ -59,19 +54,20 @@ __global__ __launch_bounds__(384, 3) void decoder_bwd_kernel(int N, const float*
     const int rc = valid ? row : N - 1;
     const float g0 = gy[(size_t)rc * 3], g1 = gy[(size_t)rc * 3 + 1], g2 = gy[(size_t)rc * 3 + 2];
     float v[FRAG];
-    const int qo = quarter_off();
-    const float* w0 = w2l + qo;
+    const int lc = lane_col();
+    const float* w0 = w2l + lc;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       f32x4 a[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = reinterpret_cast<const f32x4*>(a1d + (size_t)rc * L + qo + 16 * q)[t];
+      for (int t = 0; t < 4; ++t) a[t] = ld4(a1d + (size_t)rc * L + lc, 4 * q + t);
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int s = 16 * q + 4 * t + j;
-          const float ga = fmaf(g2, w0[2 * L + s], fmaf(g1, w0[L + s], g0 * w0[s]));
+          const int f = 16 * (4 * q + t) + j;   // feature offset beyond lane_col()
+          const float ga = fmaf(g2, w0[2 * L + f], fmaf(g1, w0[L + f], g0 * w0[f]));
           v[s] = a[t][j] > 0.f ? ga : 0.f;
         }
       PDG_FENCE();
@@ -398,7 +394,7 @@ extern "C" int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const
 
 // ============================================================================ fused edge backward
 template <bool EU>
-__global__ __launch_bounds__(768, 3) void edge_bwd_kernel(
+__global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_bwd_kernel(
     int E, const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
     const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
     const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ stm_p, const pdg_ln_stat* __restrict__ ste_p,
@@ -472,13 +468,13 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
                              PDG_ALIGNED(gz1e) && st_e && lb_e),
                 "pdg_edge_bwd: edge-update arguments missing or misaligned");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd: ge_out must not alias ge_next");
-  const int grid = persistent_grid(n_edges, 12, 1);
+  const int grid = persistent_grid(n_edges, EDGE_WAVES, 1);
   if (ge_next)
-    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(64 * EDGE_WAVES), 2 * WBLK * sizeof(float), (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
                        gz1m, gz2e, gz1e, gC, ge_out);
   else
-    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(768), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(64 * EDGE_WAVES), 2 * WBLK * sizeof(float), (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, WcT, gz2m,
                        gz1m, gz2e, gz1e, gC, ge_out);
   PDG_CHECK_LAUNCH("pdg_edge_bwd");

@@ -4,33 +4,40 @@
 // (rows x 128) fp32 array in HBM, natural feature order, 512 B per row.
 //
 // Wave tile: one 64-lane wave owns 16 consecutive rows.  Lane l holds row
-// (l & 15) and the quarter q = l >> 4, i.e. features [32q, 32q+32) of that row,
-// in a 32-float register fragment `v[s]` = feature 32q + s.  Loading a fragment
-// is 8 x 16-byte loads of one contiguous 128-byte quarter row.
+// (l & 15) and, with q = l >> 4, the 32 features {16T + 4q + j : T < 8, j < 4}
+// of that row in a register fragment v[4T + j]: eight 16-byte chunks, chunk T
+// at byte 64T + 16q of the row.  One fragment-load instruction therefore reads
+// 64 contiguous bytes of each of the 16 rows (16 half-lines; the next chunk
+// reads the other halves), and a row is covered by 4 lanes side by side.
 //
 // GEMM on the matrix cores (v_mfma_f32_16x16x4_f32, exact fp32, 32 cycles per
 // instruction per SIMD): for a 128x128 weight W (nn.Linear layout, out x in) the
 // fragment is the B operand (B[k][j]: k = lane quarter, j = row) and the weight
-// the A operand, read from an LDS image.  Step s of the 32-step K loop sums the
-// four inputs {32q + s : q = 0..3}.  The image holds in row R = 16*ob + i the
-// weight row pi(ob, i) = 32*(i>>2) + 4*ob + (i&3), which makes the accumulator
-// layout equal to the fragment layout: register r of output block ob in lane
-// quarter q is output feature 32q + 4*ob + r.  Chained layers therefore stay in
-// registers with no LDS transpose.  Fragment (32) + accumulator (32) + A
-// fragments (16) leave room for 3 waves per SIMD.
+// the A operand, read from a plain row-major LDS copy of W.  MFMA (T, j) sums
+// the four inputs {16T + 4k + j : k < 4}; output block ob's D row i = 4q + r is
+// output feature 16 ob + i, so register r of accumulator block ob in lane
+// quarter q is feature 16 ob + 4q + r: the accumulator layout equals the
+// fragment layout and chained layers stay in registers.  Fragment (32) +
+// accumulator (32) + A fragments (16) leave room for 3 waves per SIMD.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/pdivgnn.h"
+#include "pdg_runtime.hpp"
 
 namespace pdg {
 
 constexpr int L = 128;                  // latent size (the reference's configs all use 128)
 constexpr int TILE = 16;                // rows per wave tile
 constexpr int FRAG = 32;                // fragment floats per lane
-constexpr int WPAD = 132;               // LDS row stride of a 128x128 weight block (floats)
-constexpr int WBLK = 128 * WPAD;        // floats per weight block in LDS (67,584 B)
+constexpr int WPAD = 136;               // LDS row stride of a 128x128 weight block (floats): 136 = 8 mod 64
+                                        // makes the ds_read_b128 A reads of gemm128 bank-conflict free
+constexpr int WBLK = 128 * WPAD;        // floats per weight block in LDS (69,632 B)
+#ifndef PDG_EDGE_WAVES
+#define PDG_EDGE_WAVES 12
+#endif
+constexpr int EDGE_WAVES = PDG_EDGE_WAVES;  // waves per block of the fused edge kernels (one block per CU)
 constexpr float LN_EPS = 1e-5f;         // torch_geometric LayerNorm default eps
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -51,8 +58,38 @@ __device__ __forceinline__ int opaque(int x) {
   return x;
 }
 
-// Per-lane offset of the lane's quarter row: 32 * q.
-__device__ __forceinline__ int quarter_off() { return opaque(32 * (lane_id() >> 4)); }
+// XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (b and
+// b + 8 share one L2), so logical block (b & 7) * (G / 8) + (b >> 3) gives each
+// XCD a contiguous range of tiles per round of the persistent loop.  Edges are
+// dst-sorted and mesh-local, so the P/Q rows one XCD gathers for its range stay
+// in that XCD's L2.  Speed only: any order is correct.
+__device__ __forceinline__ int xcd_block() {
+#ifdef PDG_NO_XCD_REMAP
+  return blockIdx.x;
+#else
+  const int g = gridDim.x, b = blockIdx.x;
+  return (g & 7) ? b : (b & 7) * (g >> 3) + (b >> 3);
+#endif
+}
+
+// Persistent wave-tile loop over tiles_of(M) tiles of 16 rows.
+#define PDG_TILE_LOOP(M)                                                              \
+  const int nw_ = blockDim.x >> 6;                                                    \
+  const int ntiles_ = tiles_of(M);                                                    \
+  for (int tile = xcd_block() * nw_ + wave_id(); tile < ntiles_; tile += gridDim.x * nw_)
+
+// Per-lane feature offset 4q of every fragment chunk (chunk T adds 16T).
+__device__ __forceinline__ int lane_col() { return opaque(4 * (lane_id() >> 4)); }
+
+// Chunk T (4 floats) of a row or feature vector, `p` already offset by lane_col().
+__device__ __forceinline__ f32x4 ld4(const float* __restrict__ p, int T) {
+  return *reinterpret_cast<const f32x4*>(p + 16 * T);
+}
+__device__ __forceinline__ void st4(float* __restrict__ p, int T, const f32x4& x) {
+  *reinterpret_cast<f32x4*>(p + 16 * T) = x;
+}
+// Feature index of fragment element s in lane quarter q.
+__device__ __forceinline__ int frag_feature(int s, int q) { return 16 * (s >> 2) + 4 * q + (s & 3); }
 
 // x / den as the reference computes it (models.py LayerNorm: out = x / (std + eps)),
 // via the reciprocal and one Newton correction: 3 instructions instead of the
@@ -63,16 +100,13 @@ __device__ __forceinline__ float div_den(float x, float den, float rstd) {
   return fmaf(r, rstd, q);
 }
 
-__device__ __forceinline__ int wperm(int ob, int i) { return 32 * (i >> 2) + 4 * ob + (i & 3); }
-
-// Copy a 128x128 block W[o][col0 + k] (row stride ld floats) into the LDS A-image.
+// Copy a 128x128 block W[o][col0 + k] (row stride ld floats) into LDS, row stride WPAD.
 __device__ __forceinline__ void load_wblock(float* __restrict__ lds, const float* __restrict__ W,
                                             int ld, int col0) {
   for (int idx = threadIdx.x; idx < 128 * 32; idx += blockDim.x) {
-    const int R = idx >> 5, c4 = idx & 31;
-    const int o = wperm(R >> 4, R & 15);
+    const int o = idx >> 5, c4 = idx & 31;
     const f32x4 val = *reinterpret_cast<const f32x4*>(W + (size_t)o * ld + col0 + 4 * c4);
-    *reinterpret_cast<f32x4*>(lds + R * WPAD + 4 * c4) = val;
+    *reinterpret_cast<f32x4*>(lds + o * WPAD + 4 * c4) = val;
   }
 }
 
@@ -95,18 +129,23 @@ __device__ __forceinline__ void zero_acc(Acc& acc) {
 // each dependent chain has a 64-cycle spacing (> the 40-cycle MFMA latency).
 // Scheduling barriers keep the compiler from hoisting all 64 LDS reads.
 __device__ __forceinline__ void gemm128(Acc& acc, const float* __restrict__ wl, const float (&v)[FRAG]) {
+#ifdef PDG_DIAG_NOGEMM   // timing experiment only: results are wrong
+  acc.b[0][0] += v[0];
+  return;
+#endif
   const int l = lane_id();
-  const float* base = wl + opaque((l & 15) * WPAD + 32 * (l >> 4));
+  const float* base = wl + opaque((l & 15) * WPAD + 4 * (l >> 4));
   f32x4 a0[2], a1[2];
   a0[0] = *reinterpret_cast<const f32x4*>(base + 0 * 16 * WPAD);
   a0[1] = *reinterpret_cast<const f32x4*>(base + 1 * 16 * WPAD);
+  // A fragment of output block ob, input chunk t: W[16 ob + i][16 t + 4 k .. + 3]
 #pragma unroll
   for (int it = 0; it < 32; it += 2) {
     // iteration it: input group t = it >> 2, output-block pair p = it & 3 (blocks 2p, 2p+1)
     {
       const int nt = (it + 1) >> 2, np = (it + 1) & 3;
-      a1[0] = *reinterpret_cast<const f32x4*>(base + (2 * np) * 16 * WPAD + 4 * nt);
-      a1[1] = *reinterpret_cast<const f32x4*>(base + (2 * np + 1) * 16 * WPAD + 4 * nt);
+      a1[0] = *reinterpret_cast<const f32x4*>(base + (2 * np) * 16 * WPAD + 16 * nt);
+      a1[1] = *reinterpret_cast<const f32x4*>(base + (2 * np + 1) * 16 * WPAD + 16 * nt);
       const int t = it >> 2, p = it & 3;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -118,8 +157,8 @@ __device__ __forceinline__ void gemm128(Acc& acc, const float* __restrict__ wl, 
     {
       if (it + 2 < 32) {
         const int nt = (it + 2) >> 2, np = (it + 2) & 3;
-        a0[0] = *reinterpret_cast<const f32x4*>(base + (2 * np) * 16 * WPAD + 4 * nt);
-        a0[1] = *reinterpret_cast<const f32x4*>(base + (2 * np + 1) * 16 * WPAD + 4 * nt);
+        a0[0] = *reinterpret_cast<const f32x4*>(base + (2 * np) * 16 * WPAD + 16 * nt);
+        a0[1] = *reinterpret_cast<const f32x4*>(base + (2 * np + 1) * 16 * WPAD + 16 * nt);
       }
       const int t = (it + 1) >> 2, p = (it + 1) & 3;
 #pragma unroll
@@ -134,27 +173,27 @@ __device__ __forceinline__ void gemm128(Acc& acc, const float* __restrict__ wl, 
 
 // ----------------------------------------------------------------------------- fragment I/O
 __device__ __forceinline__ void load_frag(float (&v)[FRAG], const float* __restrict__ row) {
-  const f32x4* p = reinterpret_cast<const f32x4*>(row + quarter_off());
+  const float* p = row + lane_col();
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-    const f32x4 x = p[t];
+    const f32x4 x = ld4(p, t);
     v[4 * t + 0] = x[0]; v[4 * t + 1] = x[1]; v[4 * t + 2] = x[2]; v[4 * t + 3] = x[3];
   }
 }
 
 __device__ __forceinline__ void store_frag(float* __restrict__ row, const float (&v)[FRAG]) {
-  f32x4* p = reinterpret_cast<f32x4*>(row + quarter_off());
+  float* p = row + lane_col();
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     f32x4 x; x[0] = v[4 * t]; x[1] = v[4 * t + 1]; x[2] = v[4 * t + 2]; x[3] = v[4 * t + 3];
-    p[t] = x;
+    st4(p, t, x);
   }
 }
 
 __device__ __forceinline__ void store_acc(float* __restrict__ row, const Acc& acc) {
-  f32x4* p = reinterpret_cast<f32x4*>(row + quarter_off());
+  float* p = row + lane_col();
 #pragma unroll
-  for (int t = 0; t < 8; ++t) p[t] = acc.b[t];
+  for (int t = 0; t < 8; ++t) st4(p, t, acc.b[t]);
 }
 
 // ----------------------------------------------------------------------------- reductions

@@ -82,11 +82,6 @@ extern "C" int pdg_format_inputs(int n_nodes, int n_edges, const float* pos, con
 // ============================================================================ tile helpers
 // Persistent tile loop: wave w of block b takes tiles b*nw + w, then strides by
 // gridDim*nw; a tile is 16 rows, lane row = tile*16 + (lane & 15).
-#define PDG_TILE_LOOP(M)                                                              \
-  const int nw_ = blockDim.x >> 6;                                                    \
-  const int ntiles_ = tiles_of(M);                                                    \
-  for (int tile = blockIdx.x * nw_ + wave_id(); tile < ntiles_; tile += gridDim.x * nw_)
-
 __device__ __forceinline__ void accum_stats(const float (&v)[FRAG], bool valid, double& s1, double& s2) {
   if (!valid) return;
   // 32 values of one quarter row: fp32 partials per 16, fp64 across
@@ -114,16 +109,16 @@ template <bool RES>
 __device__ __forceinline__ void ln_res_frag(float (&v)[FRAG], const float* __restrict__ a2row,
                                             const float* __restrict__ resrow, const LNStat& st,
                                             const float* __restrict__ g, const float* __restrict__ b) {
-  const int qo = quarter_off();
+  const int lc = lane_col();
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     f32x4 x[2], r[2], gg[2], bb[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      x[t] = reinterpret_cast<const f32x4*>(a2row + qo + 8 * q)[t];
-      if (RES) r[t] = reinterpret_cast<const f32x4*>(resrow + qo + 8 * q)[t];
-      gg[t] = reinterpret_cast<const f32x4*>(g + qo + 8 * q)[t];
-      bb[t] = reinterpret_cast<const f32x4*>(b + qo + 8 * q)[t];
+      x[t] = ld4(a2row + lc, 2 * q + t);
+      if (RES) r[t] = ld4(resrow + lc, 2 * q + t);
+      gg[t] = ld4(g + lc, 2 * q + t);
+      bb[t] = ld4(b + lc, 2 * q + t);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -137,12 +132,12 @@ __device__ __forceinline__ void ln_res_frag(float (&v)[FRAG], const float* __res
   }
 }
 
-// v[s] = relu(acc[s] + bias[32q + s]).
+// v[s] = relu(acc[s] + bias[feature of s]).
 __device__ __forceinline__ void bias_relu(float (&v)[FRAG], const Acc& acc, const float* __restrict__ bias) {
-  const f32x4* bp = reinterpret_cast<const f32x4*>(bias + quarter_off());
+  const float* bp = bias + lane_col();
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-    const f32x4 bb = bp[t];
+    const f32x4 bb = ld4(bp, t);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[4 * t + j] = fmaxf(acc.b[t][j] + bb[j], 0.f);
   }
@@ -175,12 +170,12 @@ __global__ __launch_bounds__(384, 3) void encoder_kernel(int M, const float* __r
 #pragma unroll
     for (int i = 0; i < IN; ++i) xi[i] = x_in[(size_t)rc * IN + i];
     float v[FRAG];
-    const int qo = quarter_off();
+    const int lc = lane_col();
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
 #pragma unroll
       for (int s = 16 * q; s < 16 * q + 16; ++s) {
-        const int o = qo + s;
+        const int o = lc + 16 * (s >> 2) + (s & 3);
         float d = 0.f;
 #pragma unroll
         for (int i = 0; i < IN; ++i) d = fmaf(w0l[o * IN + i], xi[i], d);
@@ -314,18 +309,18 @@ __device__ __forceinline__ void first_layers(float (&v)[FRAG], const Acc& C, con
                                              const float* __restrict__ qd, const float* __restrict__ pd,
                                              const float* __restrict__ qs, float* __restrict__ a1e_row,
                                              bool valid) {
-  const int qo = quarter_off();
+  const int lc = lane_col();
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     f32x4 xs[2], yd[2], xd[2], ys[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (EU) {
-        xs[t] = reinterpret_cast<const f32x4*>(ps + qo + 8 * q)[t];
-        yd[t] = reinterpret_cast<const f32x4*>(qd + qo + 8 * q)[t];
+        xs[t] = ld4(ps + lc, 2 * q + t);
+        yd[t] = ld4(qd + lc, 2 * q + t);
       }
-      xd[t] = reinterpret_cast<const f32x4*>(pd + qo + 8 * q)[t];
-      ys[t] = reinterpret_cast<const f32x4*>(qs + qo + 8 * q)[t];
+      xd[t] = ld4(pd + lc, 2 * q + t);
+      ys[t] = ld4(qs + lc, 2 * q + t);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -336,14 +331,14 @@ __device__ __forceinline__ void first_layers(float (&v)[FRAG], const Acc& C, con
         if (EU) e[j] = fmaxf((c + xs[t][j]) + yd[t][j], 0.f);
         v[8 * q + 4 * t + j] = fmaxf((c + xd[t][j]) + ys[t][j], 0.f);
       }
-      if (EU && valid) reinterpret_cast<f32x4*>(a1e_row + qo + 8 * q)[t] = e;
+      if (EU && valid) st4(a1e_row + lc, 2 * q + t, e);
     }
     PDG_FENCE();
   }
 }
 
 template <bool RES, bool EU>
-__global__ __launch_bounds__(768, 3) void edge_fwd_kernel(
+__global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
     const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ P,
@@ -359,10 +354,17 @@ __global__ __launch_bounds__(768, 3) void edge_fwd_kernel(
   const int l = lane_id();
   double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
   PDG_TILE_LOOP(E) {
+#ifdef PDG_DIAG_L2   // timing experiment only: every access hits a 256-row window
+    const int row = (tile * TILE + (l & 15)) & 255;
+    const bool valid = tile * TILE + (l & 15) < E;
+    const int rc = row;
+    const int s_node = src[rc] & 255, d_node = dst[rc] & 255;
+#else
     const int row = tile * TILE + (l & 15);
     const bool valid = row < E;
     const int rc = valid ? row : E - 1;
     const int s_node = src[rc], d_node = dst[rc];
+#endif
     float v[FRAG];
     // e_t = LN(a2_prev) + e_res   (models.py:225 residual of the previous step)
     ln_res_frag<RES>(v, a2p + (size_t)rc * L, RES ? eres + (size_t)rc * L : nullptr, st, lg, lb);
@@ -372,9 +374,9 @@ __global__ __launch_bounds__(768, 3) void edge_fwd_kernel(
     zero_acc(C);
     gemm128(C, lds, v);
     {
-      const f32x4* bp = reinterpret_cast<const f32x4*>(b1 + quarter_off());
+      const float* bp = b1 + lane_col();
 #pragma unroll
-      for (int t = 0; t < 8; ++t) C.b[t] += bp[t];
+      for (int t = 0; t < 8; ++t) C.b[t] += ld4(bp, t);
     }
     // layer 1 of the edge update (models.py:219-222, x[row] = x[src], x[col] = x[dst]; stored,
     // re-read below) and of the message (models.py:233-238, x_i = x[dst], x_j = x[src])
@@ -412,11 +414,11 @@ extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat
                 "pdg_edge_fwd: misaligned pointer");
   PDG_CHECK_ARG(!with_edge_update || (a1e && a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd: edge-update outputs missing or misaligned");
-  const int grid = persistent_grid(n_edges, 12, 1);
+  const int grid = persistent_grid(n_edges, EDGE_WAVES, 1);
   const size_t shm = 2 * WBLK * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
 #define PDG_EDGE_FWD(R, U)                                                                                     \
-  hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(768), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \
+  hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(64 * EDGE_WAVES), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \
                      e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e)
   if (e_res) {
     if (with_edge_update) PDG_EDGE_FWD(true, true); else PDG_EDGE_FWD(true, false);
@@ -616,10 +618,10 @@ __global__ __launch_bounds__(384, 3) void decoder_kernel(int N, const float* __r
     float o3[3];
 #pragma unroll
     for (int o = 0; o < 3; ++o) {
-      const float* wp = w2l + o * L + quarter_off();
+      const float* wp = w2l + o * L + lane_col();
       float d = 0.f;
 #pragma unroll
-      for (int s = 0; s < FRAG; ++s) d = fmaf(wp[s], v[s], d);
+      for (int s = 0; s < FRAG; ++s) d = fmaf(wp[16 * (s >> 2) + (s & 3)], v[s], d);
       o3[o] = d;
       PDG_FENCE();
     }
