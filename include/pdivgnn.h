@@ -182,8 +182,9 @@ int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int* rowptr_src
  * so repeated calls over message-passing steps sum in a fixed order. */
 int pdg_wgrad_accum(int rows, const float* G, const float* X, const float* G2, const float* X2,
                     float* slabs, int nslabs, void* stream);
-/* grad_W[o*ld + col0 + i] += sum over slabs; grad_b[o] += (if grad_b) sum over slabs. */
-int pdg_wgrad_reduce(const float* slabs, int nslabs, float* grad_W, int ld, int col0,
+/* grad_W[o*ld + col0 + i] += sum over slabs; grad_b[o] += (if grad_b) sum over slabs.
+ * Two fixed-order passes; the slabs are scratch and are overwritten. */
+int pdg_wgrad_reduce(float* slabs, int nslabs, float* grad_W, int ld, int col0,
                      float* grad_b, void* stream);
 /* Weight gradient of a 128x128 Linear over a list of row segments (all message-passing steps
  * and both edge_net evaluations in one pass): slab[b] = per-block partial of

@@ -102,20 +102,34 @@ extern "C" int pdg_wgrad_accum(int rows, const float* G, const float* X, const f
   return PDG_OK;
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int n, float* __restrict__ gW, int ld,
-                                    int col0, float* __restrict__ gb) {
+// Two-level slab reduction (fixed order): pass 1 sums each chunk of WR_CHUNK slabs into
+// the chunk's first slab (only the thread owning element e touches column e of those
+// slabs), pass 2 adds the chunk sums in chunk order into the gradient.
+constexpr int WR_CHUNK = 32;
+
+__global__ __launch_bounds__(256) void wgrad_chunk_kernel(float* __restrict__ slabs, int n) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= SLAB) return;
+  const int b0 = blockIdx.y * WR_CHUNK, b1 = min(n, b0 + WR_CHUNK);
   float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f;
-  int b = 0;
-  for (; b + 4 <= n; b += 4) {
+  int b = b0;
+  for (; b + 4 <= b1; b += 4) {
     p0 += slabs[(size_t)b * SLAB + e];
     p1 += slabs[(size_t)(b + 1) * SLAB + e];
     p2 += slabs[(size_t)(b + 2) * SLAB + e];
     p3 += slabs[(size_t)(b + 3) * SLAB + e];
   }
-  for (; b < n; ++b) p0 += slabs[(size_t)b * SLAB + e];
-  const float s = (p0 + p1) + (p2 + p3);
+  for (; b < b1; ++b) p0 += slabs[(size_t)b * SLAB + e];
+  slabs[(size_t)b0 * SLAB + e] = (p0 + p1) + (p2 + p3);
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slabs, int nch,
+                                                           float* __restrict__ gW, int ld, int col0,
+                                                           float* __restrict__ gb) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= SLAB) return;
+  float s = 0.f;
+  for (int c = 0; c < nch; ++c) s += slabs[(size_t)c * WR_CHUNK * SLAB + e];
   if (e < L * L) {
     const int o = e / L, i = e % L;
     gW[(size_t)o * ld + col0 + i] += s;
@@ -124,11 +138,15 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slabs, int n, floa
   }
 }
 
-extern "C" int pdg_wgrad_reduce(const float* slabs, int nslabs, float* grad_W, int ld, int col0, float* grad_b,
+extern "C" int pdg_wgrad_reduce(float* slabs, int nslabs, float* grad_W, int ld, int col0, float* grad_b,
                                 void* stream) {
   PDG_CHECK_ARG(nslabs > 0 && grad_W != nullptr, "pdg_wgrad_reduce: bad args");
+  const int nch = (nslabs + WR_CHUNK - 1) / WR_CHUNK;
+  hipLaunchKernelGGL(wgrad_chunk_kernel, dim3((SLAB + 255) / 256, nch), dim3(256), 0, (hipStream_t)stream, slabs,
+                     nslabs);
+  PDG_CHECK_LAUNCH("pdg_wgrad_reduce(chunks)");
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((SLAB + 255) / 256), dim3(256), 0, (hipStream_t)stream, slabs,
-                     nslabs, grad_W, ld, col0, grad_b);
+                     nch, grad_W, ld, col0, grad_b);
   PDG_CHECK_LAUNCH("pdg_wgrad_reduce");
   return PDG_OK;
 }
@@ -377,6 +395,208 @@ __global__ __launch_bounds__(256, 2) void wgrad_segments_kernel(WgradSegs sg, lo
   }
 }
 
+// ---------------------------------------------------------------------------- bf16x6 form
+// The same segmented reduction on the bf16 matrix cores with fp32 accuracy:
+// every operand value is split exactly into three bf16 terms x = x0 + x1 + x2
+// (round-to-nearest hi, mid, lo: 24 significant bits) and
+//   G^T X = sum over the six products with i + j <= 2 of Gi^T Xj,
+// accumulated in fp32 from the smallest terms up; the dropped products are
+// below 2^-24 |G||X|, the size of one fp32 rounding.  v_mfma_f32_32x32x16_bf16
+// does 16x the flops of v_mfma_f32_32x32x2_f32 per cycle, so the six products
+// cost 2.7x less matrix-core time than one fp32 product and the pass is bound
+// by HBM (reading G and X once).
+//
+// Block: 4 waves, three blocks per CU.  Per round it stages 32 rows: thread t
+// loads rows 4(t>>5) .. +3, columns 4(t&31) .. +3 of G and X (two full 512-B
+// rows per wave instruction), splits them and writes the terms row-major into
+// LDS images [term][32 rows][256 B] (ds_write_b64).  The MFMA operands need 8
+// consecutive ROWS of one column per lane; ds_read_b64_tr_b16 reads them
+// transposed (4 rows x 16 columns per 16-lane group).  The 16-B chunks of row r
+// are XOR-swizzled by ((r & 3) << 2 | (r >> 2) & 3): both the writes and each
+// 32-lane half of the transposed reads then hit 64 distinct banks.  Wave w owns the 64x64
+// output quadrant (o in 64(w>>1) + [0,64), i in 64(w&1) + [0,64)).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int X6_ROWS = 32;                       // rows staged per round
+constexpr int X6_ROWB = 256;                      // bytes per row of one term image
+constexpr int X6_TERM = X6_ROWS * X6_ROWB;        // bytes per term image (8 KB)
+
+// Byte address of byte `b` (0..255) of image row `r`.
+__device__ __forceinline__ int x6_addr(int r, int b) {
+  return r * X6_ROWB + (b ^ (((r & 3) << 6) | (((r >> 2) & 3) << 4)));
+}
+
+// bf16 round-to-nearest-even of x, as the upper half of a float.
+__device__ __forceinline__ unsigned bf16_rne(float x) {
+  const unsigned u = __float_as_uint(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+
+// x = hi + mid + lo exactly.
+__device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& lo) {
+  h = bf16_rne(x);
+  const float r1 = x - __uint_as_float(h << 16);
+  m = bf16_rne(r1);
+  lo = bf16_rne(r1 - __uint_as_float(m << 16));
+}
+
+// Split 4 rows x 4 columns and write them: row i of this thread goes to image row 4 rg + i.
+__device__ __forceinline__ void x6_store(unsigned char* img, int cg, int rg, const f32x4 (&v)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    unsigned h[4], m[4], lo[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) split3(v[i][c], h[c], m[c], lo[c]);
+    const int off = x6_addr(4 * rg + i, 8 * cg);
+    *reinterpret_cast<u32x2*>(img + off) = u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+    *reinterpret_cast<u32x2*>(img + X6_TERM + off) = u32x2{m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
+    *reinterpret_cast<u32x2*>(img + 2 * X6_TERM + off) = u32x2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
+  }
+}
+
+__device__ __forceinline__ void x6_load(const WgTable* tb, int nseg, long base, long r1, int& seg, int cg,
+                                        f32x4 (&gr)[4], f32x4 (&xr)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long vr = base + i;
+    if (vr < r1) {
+      while (seg + 1 < nseg && vr >= tb->start[seg + 1]) ++seg;
+      const long r = vr - tb->start[seg];
+      gr[i] = reinterpret_cast<const f32x4*>(tb->G[seg] + r * L)[cg];
+      xr[i] = reinterpret_cast<const f32x4*>(tb->X[seg] + r * L)[cg];
+    } else {
+      gr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+// MFMA operand of columns col0 + (l & 31), rows 16 ks + 8 (l >> 5) + 0..7, from term image `img`:
+// two transposed reads of 4 rows each, at the lane's addresses ofs0 / ofs1 (row
+// 16 ks + 8 (l >> 5) + ((l & 15) >> 2) [+ 4], columns col0 + 16 ((l >> 4) & 1) + 4 (l & 3) .. +3).
+__device__ __forceinline__ bf16x8 x6_operand(const unsigned char* img, int ofs0, int ofs1) {
+  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + ofs0));
+  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + ofs1));
+  s16x4 v0 = a, v1 = b;
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 r = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__global__ __launch_bounds__(256, 3) void wgrad_x6_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem6[];   // [table | G terms | X terms]
+  WgTable* tb = reinterpret_cast<WgTable*>(smem6);
+  unsigned char* gimg = smem6 + WG_TABLE_FLOATS * 4;
+  unsigned char* ximg = gimg + 3 * X6_TERM;
+  const int nseg = sg.nseg;
+  for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
+  for (int i = threadIdx.x; i < PDG_MAX_SEGS; i += blockDim.x) {
+    tb->G[i] = sg.G[i];
+    tb->X[i] = sg.X[i];
+  }
+  __syncthreads();
+  const int nb = gridDim.x;
+  long per = (total + nb - 1) / nb;
+  per = (per + X6_ROWS - 1) / X6_ROWS * X6_ROWS;
+  const long r0 = min(total, per * blockIdx.x), r1 = min(total, per * (blockIdx.x + 1));
+  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int ob = 64 * (w >> 1), ib = 64 * (w & 1);
+  // transposed-read row and column byte of this lane inside its 16-lane group (see x6_operand)
+  const int lrow = 8 * h + ((l & 15) >> 2);
+  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
+  int seg;
+  {
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (tb->start[mid] <= r0) lo = mid; else hi = mid;
+    }
+    seg = lo;
+  }
+  f32x4 gr[4], xr[4];
+  if (r0 < r1) {
+    x6_load(tb, nseg, r0 + 4 * rg, r1, seg, cg, gr, xr);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bsum += gr[i];
+    x6_store(gimg, cg, rg, gr);
+    x6_store(ximg, cg, rg, xr);
+  }
+  __syncthreads();
+  for (long base = r0; base < r1; base += X6_ROWS) {
+    const bool more = base + X6_ROWS < r1;
+    if (more) x6_load(tb, nseg, base + X6_ROWS + 4 * rg, r1, seg, cg, gr, xr);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 A[2][3], B[2][3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int row = 16 * ks + lrow;
+        const int g0 = x6_addr(row, lcolb + 2 * (ob + 32 * a)), g1 = x6_addr(row + 4, lcolb + 2 * (ob + 32 * a));
+        const int x0 = x6_addr(row, lcolb + 2 * (ib + 32 * a)), x1 = x6_addr(row + 4, lcolb + 2 * (ib + 32 * a));
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          A[a][p] = x6_operand(gimg + p * X6_TERM, g0, g1);
+          B[a][p] = x6_operand(ximg + p * X6_TERM, x0, x1);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          f32x16 t = acc[a][b];
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2], B[b][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][2], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][1], t, 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][0], t, 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bsum += gr[i];
+      x6_store(gimg, cg, rg, gr);
+      x6_store(ximg, cg, rg, xr);
+    }
+    __syncthreads();
+  }
+  float* slab = slabs + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int i = ib + 32 * b + c;
+        slab[o * L + i] = acc[a][b][r];
+      }
+  // bias sums: the 8 row groups of each column group, in row-group order
+  float* red = reinterpret_cast<float*>(gimg);   // the images are dead now
+  *reinterpret_cast<f32x4*>(red + 4 * threadIdx.x) = bsum;
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int col = threadIdx.x, g = col >> 2, j = col & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += red[4 * (32 * q + g) + j];
+    slab[L * L + col] = s;
+  }
+}
+
 extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
                                   float* slabs, int nslabs, void* stream) {
   PDG_CHECK_ARG(nseg > 0 && nseg <= PDG_MAX_SEGS, "pdg_wgrad_segments: 1..%d segments", PDG_MAX_SEGS);
@@ -395,8 +615,13 @@ extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const fl
   for (int i = nseg + 1; i <= PDG_MAX_SEGS; ++i) sg.start[i] = tot;
   sg.nseg = nseg;
   PDG_CHECK_ARG(tot > 0, "pdg_wgrad_segments: no rows");
+#ifdef PDG_WGRAD_F32
   hipLaunchKernelGGL(wgrad_segments_kernel, dim3(nslabs), dim3(256), (WG_TABLE_FLOATS + 4 * WG_TILE) * sizeof(float),
                      (hipStream_t)stream, sg, tot, slabs);
+#else
+  hipLaunchKernelGGL(wgrad_x6_kernel, dim3(nslabs), dim3(256), WG_TABLE_FLOATS * 4 + 6 * X6_TERM, (hipStream_t)stream,
+                     sg, tot, slabs);
+#endif
   PDG_CHECK_LAUNCH("pdg_wgrad_segments");
   return PDG_OK;
 }

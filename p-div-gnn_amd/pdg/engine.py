@@ -95,7 +95,8 @@ class EPDEngine:
         self._part_col = torch.empty(self.max_blocks * 256, **f64)
         self._part_narrow = torch.empty(self.max_blocks * (L * 6 + L + 6), **f64)
         self._nparts = ctypes.c_int(0)
-        self._nslabs = 512
+        # one weight-gradient slab per block of pdg_wgrad_segments: three blocks per CU
+        self._nslabs = 3 * torch.cuda.get_device_properties(self.device).multi_processor_count
         # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
         self.timed: dict | None = None
 
