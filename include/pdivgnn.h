@@ -87,7 +87,8 @@ int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const 
  * e_t = LN(a2_prev) [+ e_res]; C = W1[:, 256:384] e_t + b1;
  * message:  a1m = relu(C + P[dst] + Q[src]), a2m = relu(W2 a1m + b2)
  * edge upd: a1e = relu(C + P[src] + Q[dst]), a2e = relu(W2 a1e + b2)
- * writes e_t, a1m, a2m, a1e, a2e and LayerNorm partials of a2m and a2e. */
+ * writes e_t, a1m, a2m, a1e, a2e and LayerNorm partials of a2m and a2e.  a1m and a1e are only
+ * needed by the backward: NULL skips storing them (inference). */
 int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                  const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
                  const float* P, const float* Q, const float* W1, const float* b1,

@@ -300,38 +300,72 @@ extern "C" int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat*
 
 // ============================================================================ fused edge pass
 // First layer of both edge_net evaluations from the shared C = W_c e + b1, in
-// four fenced chunks of 8 floats (each accumulator block pair dies as its chunk
-// is consumed):
-//   edge update: relu(C + P[src] + Q[dst]) -> stored to a1e (when EU)
-//   message:     relu(C + P[dst] + Q[src]) -> v (and stored to a1m by the caller)
+// four chunks of 8 features (each accumulator block pair dies as its chunk is
+// consumed); the gathered P/Q rows of chunk q+1 are in flight while chunk q is
+// computed:
+//   edge update: relu(C + P[src] + Q[dst]) -> ve (kept for layer 2, stored to a1e)
+//   message:     relu(C + P[dst] + Q[src]) -> v  (stored to a1m by the caller)
+// Registers (<= 168 for 3 waves/SIMD) allow one of: the next chunk's gathers in
+// flight, or the edge-update layer-1 output kept for layer 2 instead of re-read;
+// measured, keeping it is faster (edge_fwd -5 %, prefetching -1.5 %).
+#ifndef PDG_EF_PREFETCH
+#define PDG_EF_PREFETCH 0
+#endif
+#ifndef PDG_EF_KEEP_A1E
+#define PDG_EF_KEEP_A1E 1
+#endif
+struct Gather8 {
+  f32x4 xs[2], yd[2], xd[2], ys[2];
+};
+
 template <bool EU>
-__device__ __forceinline__ void first_layers(float (&v)[FRAG], const Acc& C, const float* __restrict__ ps,
+__device__ __forceinline__ void gather_chunk(Gather8& g, int q, const float* __restrict__ ps,
                                              const float* __restrict__ qd, const float* __restrict__ pd,
-                                             const float* __restrict__ qs, float* __restrict__ a1e_row,
-                                             bool valid) {
+                                             const float* __restrict__ qs) {
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (EU) {
+      g.xs[t] = ld4(ps, 2 * q + t);
+      g.yd[t] = ld4(qd, 2 * q + t);
+    }
+    g.xd[t] = ld4(pd, 2 * q + t);
+    g.ys[t] = ld4(qs, 2 * q + t);
+  }
+}
+
+template <bool EU>
+__device__ __forceinline__ void first_layers(float (&v)[FRAG], float (&ve)[FRAG], const Acc& C,
+                                             const float* __restrict__ ps, const float* __restrict__ qd,
+                                             const float* __restrict__ pd, const float* __restrict__ qs,
+                                             float* __restrict__ a1e_row, bool valid) {
   const int lc = lane_col();
+  ps += lc; qd += lc; pd += lc; qs += lc;
+#if PDG_EF_PREFETCH
+  Gather8 g[2];
+  gather_chunk<EU>(g[0], 0, ps, qd, pd, qs);
+#else
+  Gather8 g[1];
+#endif
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    f32x4 xs[2], yd[2], xd[2], ys[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (EU) {
-        xs[t] = ld4(ps + lc, 2 * q + t);
-        yd[t] = ld4(qd + lc, 2 * q + t);
-      }
-      xd[t] = ld4(pd + lc, 2 * q + t);
-      ys[t] = ld4(qs + lc, 2 * q + t);
-    }
+#if PDG_EF_PREFETCH
+    if (q < 3) gather_chunk<EU>(g[(q + 1) & 1], q + 1, ps, qd, pd, qs);
+    const Gather8& c8 = g[q & 1];
+#else
+    gather_chunk<EU>(g[0], q, ps, qd, pd, qs);
+    const Gather8& c8 = g[0];
+#endif
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       f32x4 e;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float c = C.b[2 * q + t][j];
-        if (EU) e[j] = fmaxf((c + xs[t][j]) + yd[t][j], 0.f);
-        v[8 * q + 4 * t + j] = fmaxf((c + xd[t][j]) + ys[t][j], 0.f);
+        if (EU) e[j] = fmaxf((c + c8.xs[t][j]) + c8.yd[t][j], 0.f);
+        v[8 * q + 4 * t + j] = fmaxf((c + c8.xd[t][j]) + c8.ys[t][j], 0.f);
+        if (EU && PDG_EF_KEEP_A1E) ve[8 * q + 4 * t + j] = e[j];
       }
-      if (EU && valid) st4(a1e_row + lc, 2 * q + t, e);
+      if (EU && valid && a1e_row) st4(a1e_row + lc, 2 * q + t, e);
     }
     PDG_FENCE();
   }
@@ -354,17 +388,10 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kern
   const int l = lane_id();
   double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
   PDG_TILE_LOOP(E) {
-#ifdef PDG_DIAG_L2   // timing experiment only: every access hits a 256-row window
-    const int row = (tile * TILE + (l & 15)) & 255;
-    const bool valid = tile * TILE + (l & 15) < E;
-    const int rc = row;
-    const int s_node = src[rc] & 255, d_node = dst[rc] & 255;
-#else
     const int row = tile * TILE + (l & 15);
     const bool valid = row < E;
     const int rc = valid ? row : E - 1;
     const int s_node = src[rc], d_node = dst[rc];
-#endif
     float v[FRAG];
     // e_t = LN(a2_prev) + e_res   (models.py:225 residual of the previous step)
     ln_res_frag<RES>(v, a2p + (size_t)rc * L, RES ? eres + (size_t)rc * L : nullptr, st, lg, lb);
@@ -378,11 +405,12 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kern
 #pragma unroll
       for (int t = 0; t < 8; ++t) C.b[t] += ld4(bp, t);
     }
-    // layer 1 of the edge update (models.py:219-222, x[row] = x[src], x[col] = x[dst]; stored,
-    // re-read below) and of the message (models.py:233-238, x_i = x[dst], x_j = x[src])
-    first_layers<EU>(v, C, P + (size_t)s_node * L, Q + (size_t)d_node * L, P + (size_t)d_node * L,
-                     Q + (size_t)s_node * L, EU ? a1e + (size_t)row * L : nullptr, valid);
-    if (valid) store_frag(a1m + (size_t)row * L, v);
+    // layer 1 of the edge update (models.py:219-222, x[row] = x[src], x[col] = x[dst]) and of
+    // the message (models.py:233-238, x_i = x[dst], x_j = x[src])
+    float ve[FRAG];
+    first_layers<EU>(v, ve, C, P + (size_t)s_node * L, Q + (size_t)d_node * L, P + (size_t)d_node * L,
+                     Q + (size_t)s_node * L, (EU && a1e) ? a1e + (size_t)row * L : nullptr, valid);
+    if (valid && a1m) store_frag(a1m + (size_t)row * L, v);   // a1m / a1e: kept for the backward only
     Acc Z;
     zero_acc(Z);
     gemm128(Z, lds + WBLK, v);
@@ -391,9 +419,11 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kern
     accum_stats(v, valid, sm1, sm2);
     if (EU) {
       // edge-update layer 2
-      load_frag(v, a1e + (size_t)(valid ? row : rc) * L);
+#if !PDG_EF_KEEP_A1E
+      load_frag(ve, a1e + (size_t)(valid ? row : rc) * L);
+#endif
       zero_acc(Z);
-      gemm128(Z, lds + WBLK, v);
+      gemm128(Z, lds + WBLK, ve);
       bias_relu(v, Z, b2);
       if (valid) store_frag(a2e + (size_t)row * L, v);
       accum_stats(v, valid, se1, se2);
@@ -412,7 +442,7 @@ extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
                     PDG_ALIGNED(a1m) && PDG_ALIGNED(a2m) && (!e_res || PDG_ALIGNED(e_res)),
                 "pdg_edge_fwd: misaligned pointer");
-  PDG_CHECK_ARG(!with_edge_update || (a1e && a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
+  PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd: edge-update outputs missing or misaligned");
   const int grid = persistent_grid(n_edges, EDGE_WAVES, 1);
   const size_t shm = 2 * WBLK * sizeof(float);

@@ -157,10 +157,9 @@ class _EPDFunction(torch.autograd.Function):
     def forward(ctx, model, plan, stats8, scale_output, scale_input, pos, mean_stress, nodes_types, edge_attr,
                 *params):
         P = dict(zip(PARAM_NAMES, params))
-        need_grad = any(p.requires_grad for p in params)
         y, fctx = model._engine_for(pos.device).forward(
             P, stats8, plan, pos, mean_stress, nodes_types, edge_attr, model.message_passing_steps,
-            scale_input, scale_output, need_grad)
+            scale_input, scale_output, True)
         ctx.fctx = fctx
         ctx.model = model
         ctx.save_for_backward(*params)
@@ -229,6 +228,13 @@ class EncodeProcessDecode(StressFieldBaseModel):
         ms = ms.float().contiguous()
         types = mesh_graph.nodes_types.reshape(-1).to(torch.int64).contiguous()
         ea = mesh_graph.edge_attr.reshape(-1).float().contiguous()
+        if not (torch.is_grad_enabled() and any(p.requires_grad for p in params)):
+            # inference (gnn_inference.py runs under no_grad): nothing is kept for a backward
+            P = dict(zip(PARAM_NAMES, params))
+            y, _ = self._engine_for(dev).forward(P, self.stats_tensor(dev), plan, pos, ms, types, ea,
+                                                 self.message_passing_steps, bool(scale_input),
+                                                 bool(scale_output), False)
+            return Data(local_stress=y, edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)
         y = _EPDFunction.apply(self, plan, self.stats_tensor(dev), bool(scale_output), bool(scale_input), pos, ms,
                                types, ea, *params)
         return Data(local_stress=y, edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)

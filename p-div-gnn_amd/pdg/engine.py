@@ -170,8 +170,10 @@ class EPDEngine:
             # the last step's edge update has no consumer (models.py:316 decodes nodes only)
             eu = t < steps - 1
             e_t = self._empty(E, L)
-            a1m, a2m = self._empty(E, L), self._empty(E, L)
-            a1e, a2e = (self._empty(E, L), self._empty(E, L)) if eu else (None, None)
+            a2m = self._empty(E, L)
+            a1m = self._empty(E, L) if need_grad else None          # layer-1 outputs: backward only
+            a2e = self._empty(E, L) if eu else None
+            a1e = self._empty(E, L) if (eu and need_grad) else None
             self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
                     _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
                     _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
