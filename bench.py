@@ -35,6 +35,10 @@ sys.path[:0] = [str(ROOT), str(ROOT / "p-div-gnn_amd")]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+PMC_FILE = ROOT / "profiles" / "r01_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
+PMC_NAMES = {"edge_fwd": "void edge_fwd_kernel<true, true>", "edge_bwd": "void edge_bwd_kernel<true>",
+             "segment_sum": "segment_sum_kernel", "pq_scatter_bwd": "pq_scatter_bwd_kernel",
+             "wgrad_W2": "wgrad_x6_kernel"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
 PEAK_HBM = 8.0e12           # MI355X HBM3E spec bandwidth (same guide; 6.3 TB/s measured copy)
 L = 128
@@ -120,12 +124,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one process per GPU; PDG_DIST_BACKEND=gloo with more ranks than GPUs only rehearses the
+    # multi-rank flow (ranks share devices round-robin)
+    backend = os.environ.get("PDG_DIST_BACKEND", "nccl")
+    dev_index = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     pg = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
         pg = dist.group.WORLD
 
     from gnn_local_stress.models import EncodeProcessDecode
@@ -197,6 +208,14 @@ def main():
         "pq_scatter_bwd": (0, 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
     }
 
+    pmc = {}
+    if PMC_FILE.exists() and args.config == 2:
+        data = json.loads(PMC_FILE.read_text())
+        for k, prefix in PMC_NAMES.items():
+            hit = [v for name, v in data.items() if name.startswith(prefix)]
+            if hit:
+                pmc[k] = round(hit[0]["total"])
+
     def roof(k):
         flops, nbytes = work[k]
         t = kt[k]
@@ -208,7 +227,11 @@ def main():
         else:
             ach, peak, unit = nbytes / t / 1e9, PEAK_HBM / 1e9, "GB/s"
         return {"kernel": k, "bound": bound, "achieved": round(ach, 2), "peak": round(peak, 1), "unit": unit,
-                "frac": round(ach / peak, 4), "traffic": None, "flops_per_launch": flops,
+                "frac": round(ach / peak, 4), "traffic": pmc.get(k),
+                "traffic_source": (f"profiles/{PMC_FILE.name}: 2*FETCH_SIZE+WRITE_SIZE per dispatch"
+                                   + (" (mean over all weights' wgrad dispatches)" if k == "wgrad_W2" else "")
+                                   if k in pmc else None),
+                "flops_per_launch": flops,
                 "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4), "frac_hbm": round(f_hbm, 4),
                 "avg_launch_ms": round(t * 1e3, 4), "share_of_step": round(ktot[k] / el, 4)}
 

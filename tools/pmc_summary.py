@@ -2,8 +2,13 @@
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of a wide
 coalesced read -> bytes_read = 2 * FETCH_SIZE * 1024; WRITE_SIZE (KB) is exact for 16-B stores.
-Prints the mean per dispatch for each kernel name."""
+Prints the mean per dispatch for each kernel name; --json FILE also writes
+{kernel name: {"read": B, "write": B, "total": B, "dispatches": n}}.
+
+    python tools/pmc_summary.py fetch/counter_collection.csv write/counter_collection.csv [--json out.json]
+"""
 import csv
+import json
 import sys
 from collections import defaultdict
 
@@ -14,12 +19,27 @@ def load(path, counter):
         if r.get("Counter_Name") != counter:
             continue
         acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
-fetch = load(sys.argv[1], "FETCH_SIZE")
-write = load(sys.argv[2], "WRITE_SIZE")
-for k in sorted(set(fetch) | set(write)):
-    f = fetch.get(k, 0.0) * 1024 * 2
-    w = write.get(k, 0.0) * 1024
-    print(f"{k[:70]:70s} read {f/1e6:10.1f} MB  write {w/1e6:10.1f} MB  total {(f+w)/1e6:10.1f} MB")
+def main(argv):
+    out_json = None
+    if "--json" in argv:
+        i = argv.index("--json")
+        out_json = argv[i + 1]
+        argv = argv[:i] + argv[i + 2:]
+    fetch = load(argv[0], "FETCH_SIZE")
+    write = load(argv[1], "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, (0.0, 0))[0] * 1024 * 2
+        w = write.get(k, (0.0, 0))[0] * 1024
+        n = max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1])
+        res[k] = {"read": f, "write": w, "total": f + w, "dispatches": n}
+        print(f"{k[:70]:70s} read {f/1e6:10.1f} MB  write {w/1e6:10.1f} MB  total {(f+w)/1e6:10.1f} MB")
+    if out_json:
+        json.dump(res, open(out_json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
