@@ -37,7 +37,7 @@ import torch.distributed as dist  # noqa: E402
 
 PMC_FILE = ROOT / "profiles" / "r01_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
 PMC_NAMES = {"edge_fwd": "void edge_fwd_kernel<true, true>", "edge_bwd": "void edge_bwd_kernel<true>",
-             "segment_sum": "segment_sum_kernel", "pq_scatter_bwd": "pq_scatter_bwd_kernel",
+             "segment_sum": "segment_sum_kernel", "node_net": "node_net_kernel", "pq_scatter_bwd": "pq_scatter_bwd_kernel",
              "wgrad_W2": "wgrad_x6_kernel"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
 PEAK_HBM = 8.0e12           # MI355X HBM3E spec bandwidth (same guide; 6.3 TB/s measured copy)
@@ -169,7 +169,7 @@ def main():
         run_step()
     torch.cuda.synchronize()
     eng = trainer.engine
-    timed_kernels = ["edge_fwd", "edge_bwd", "wgrad_W2", "segment_sum", "pq_scatter_bwd"]
+    timed_kernels = ["edge_fwd", "edge_bwd", "wgrad_W2", "segment_sum", "node_net", "pq_scatter_bwd"]
     eng.timed = {k: [] for k in timed_kernels}
     if pg is not None:
         dist.barrier()
@@ -204,7 +204,10 @@ def main():
         "edge_bwd": (E * 3 * 2 * L * L, E * (12 * 4 * L + 4)),
         # all steps' W2 segments: 2E rows per step of (G, X) 512-byte rows, one 64 KB slab per block
         "wgrad_W2": (S * 2 * E * 2 * L * L, S * 2 * E * 2 * 4 * L + 512 * (L * L + L) * 4),
-        "segment_sum": (0, 4 * L * E + 4 * (N + 1) + 4 * L * N),
+        # dst-segment sum of LN(a2m): reads a2m (E rows) and rowptr, writes aggr (+ x-hat sums)
+        "segment_sum": (0, 4 * L * E + 4 * (N + 1) + (1 if infer else 2) * 4 * L * N),
+        # node_net, 2 GEMMs (K = 256, 128) per node: reads aggr, x; writes a2n (+ a1n)
+        "node_net": (N * 2 * L * (2 * L + L), 2 * 4 * L * N + (1 if infer else 2) * 4 * L * N),
         "pq_scatter_bwd": (0, 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
     }
 
@@ -257,6 +260,7 @@ def main():
                        "parallelism": f"graph-DP x{world}", "final_loss": round(loss, 6)},
             "roofline": roof(dominant),
             "roofline_gather_scatter": [roof(k) for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
+            "roofline_node_net": roof("node_net") if "node_net" in kt else None,
             "kernel_ms": {k: round(v * 1e3, 4) for k, v in kt.items()},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -110,6 +110,14 @@ int pdg_node_mlp1(int n_nodes, const float* aggr, const float* x, const float* W
 int pdg_mlp2_fwd(int rows, const float* a1, const float* W2, const float* b2, float* a2,
                  double* partials, int* nparts, void* stream);
 
+/* Fused node_net of one step (models.py:240-243): a1n = relu(Wn1 [aggr | x] + bn1),
+ * a2n = relu(Wn2 a1n + bn2) and LayerNorm partials of a2n, in one pass with the weights held
+ * in registers.  Bitwise the same a1n / a2n as pdg_node_mlp1 + pdg_mlp2_fwd.  a1n is only
+ * needed by the backward and may be NULL. */
+int pdg_node_net(int n_nodes, const float* aggr, const float* x, const float* Wn1, const float* bn1,
+                 const float* Wn2, const float* bn2, float* a1n, float* a2n, double* partials,
+                 int* nparts, void* stream);
+
 /* Decoder (models.py:282-286, :316-321): x_S = LN(a2_prev) + x_res; a1d = relu(Wd1 x_S + bd1);
  * y = Wd2 a1d + bd2 (3 outputs); if scale_output: y = y * std_local_stress + mean_local_stress. */
 int pdg_decoder_fwd(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,

@@ -180,13 +180,15 @@ class EPDEngine:
             self._finalize(self._part_a, E * L, st[i_m], s)
             if eu:
                 self._finalize(self._part_b, E * L, st[i_e], s)
+            # aggregation (models.py:215-217) and node_net (:240-243)
             aggr = self._empty(N, L)
             xs = self._empty(N, L) if need_grad else None
             self._t("segment_sum", lib.pdg_segment_sum, N, _p(plan.rowptr_dst), _p(a2m), st[i_m], _p(ge), _p(be),
                     _p(aggr), _p(xs), s)
-            a1n, a2n = self._empty(N, L), self._empty(N, L)
-            lib.pdg_node_mlp1(N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(a1n), s)
-            lib.pdg_mlp2_fwd(N, _p(a1n), _p(Wn2), _p(bn2), _p(a2n), _p(self._part_a), np_, s)
+            a1n = self._empty(N, L) if need_grad else None
+            a2n = self._empty(N, L)
+            self._t("node_net", lib.pdg_node_net, N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(Wn2), _p(bn2), _p(a1n),
+                    _p(a2n), _p(self._part_a), np_, s)
             self._finalize(self._part_a, N * L, st[i_n], s)
             if need_grad:
                 ctx.per_step.append(dict(x=x_t, e=e_t, a1m=a1m, a2m=a2m, a1e=a1e, a2e=a2e, aggr=aggr, xs=xs,

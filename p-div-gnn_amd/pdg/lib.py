@@ -32,6 +32,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_segment_sum": [I, P, P, P, P, P, P, P, P],
     "pdg_node_mlp1": [I, P, P, P, P, P, P],
     "pdg_mlp2_fwd": [I, P, P, P, P, P, P, P],
+    "pdg_node_net": [I, P, P, P, P, P, P, P, P, P, P, P],
     "pdg_decoder_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
     "pdg_any_nonzero": [P, c_int64, P, P],
     "pdg_decoder_bwd": [I, P, P, P, P, P, P, P],

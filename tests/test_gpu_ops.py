@@ -298,3 +298,38 @@ def test_wgrad_segments_dynamic_range(env):
     worst = float(((gW.double() - ref).abs() / scale).max())
     print(f"wgrad_segments dynamic-range worst |err|/sum|GX| {worst:.3e}")
     assert worst < 1e-6
+
+
+@pytest.mark.parametrize("N", [5, 1031, 4099, 40328])
+def test_node_net_matches_separate_kernels(env, N):
+    """Fused node_net (register-stationary weights) == pdg_node_mlp1 + pdg_mlp2_fwd bitwise;
+    LayerNorm partial totals equal to fp32 rounding; against float64 torch."""
+    lib, sh, _ = env
+    s = sh()
+    aggr = rnd(N, L) * 3.0
+    x = rnd(N, L)
+    W1, b1 = lin(L, 2 * L)
+    W2, b2 = lin(L, L)
+    n = ctypes.c_int(0)
+    a10, a20 = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
+    part0 = torch.zeros(4096, dtype=torch.float64, device="cuda")
+    lib.pdg_node_mlp1(N, aggr.data_ptr(), x.data_ptr(), W1.data_ptr(), b1.data_ptr(), a10.data_ptr(), s)
+    lib.pdg_mlp2_fwd(N, a10.data_ptr(), W2.data_ptr(), b2.data_ptr(), a20.data_ptr(), part0.data_ptr(),
+                     ctypes.byref(n), s)
+    n0 = n.value
+    a11, a21 = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
+    part1 = torch.zeros(4096, dtype=torch.float64, device="cuda")
+    assert lib.pdg_node_net(N, aggr.data_ptr(), x.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
+                            b2.data_ptr(), a11.data_ptr(), a21.data_ptr(), part1.data_ptr(), ctypes.byref(n), s) == 0
+    n1 = n.value
+    assert torch.equal(a10, a11) and torch.equal(a20, a21)
+    t0 = part0[: 2 * n0].view(n0, 2).sum(0)
+    t1 = part1[: 2 * n1].view(n1, 2).sum(0)
+    assert float(((t0 - t1).abs() / t0.abs()).max()) < 1e-6
+    a2i = torch.empty(N, L, device="cuda")   # inference form: a1n not stored
+    lib.pdg_node_net(N, aggr.data_ptr(), x.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                     None, a2i.data_ptr(), part1.data_ptr(), ctypes.byref(n), s)
+    assert torch.equal(a2i, a20)
+    h1 = torch.relu(torch.cat([aggr, x], 1).double() @ W1.double().T + b1.double())
+    h2 = torch.relu(h1 @ W2.double().T + b2.double())
+    assert rel(a21, h2) < TOL
