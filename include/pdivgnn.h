@@ -158,6 +158,14 @@ int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a
                  const pdg_ln_stat* st, const pdg_ln_bwd* lb, const float* ln_g, const float* W2T,
                  float* gz2, float* gz1, void* stream);
 
+/* Fused node_net backward of one step (the work of pdg_mlp2_bwd + pdg_gemm_dual with
+ * res0 = NULL, res1 = gy): gz2 = LN_bwd(gy) * [a2n > 0]; gz1 = (Wn2^T gz2) * [a1n > 0];
+ * gaggr = Wn1a^T gz1; gx_part = Wn1b^T gz1 + gy.  Weights held in registers; bitwise the
+ * results of the separate kernels. */
+int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, const float* a1n, const pdg_ln_stat* st,
+                 const pdg_ln_bwd* lb, const float* ln_g, const float* Wn2T, const float* Wn1aT,
+                 const float* Wn1bT, float* gz2, float* gz1, float* gaggr, float* gx_part, void* stream);
+
 /* out0 = W0T in [+ res0]; out1 = W1T in [+ res1]  (two 128x128 products of one input). */
 int pdg_gemm_dual(int rows, const float* in, const float* W0T, const float* W1T,
                   const float* res0, const float* res1, float* out0, float* out1, void* stream);

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
     const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
     float* __restrict__ a1_out, float* __restrict__ a2_out, double* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) float xin[2 * XBUF];
-  __shared__ __attribute__((aligned(16))) float a1t[TILE * AS];
+  __shared__ __attribute__((aligned(16))) float a1t[2 * TILE * AS];   // double-buffered: one barrier per tile
   const int w = wave_id(), l = lane_id();
   const bool loader = w >= NU_COMPUTE;
   const int ntiles = tiles_of(N);
@@ -101,14 +101,14 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
 #pragma unroll
       for (int c = 0; c < 4; ++c) a1[c] = fmaxf(acc[c] + bias1[c], 0.f);
       // D row 4q + c of this wave's block = feature 16w + 4q + c of node row r
-      *reinterpret_cast<f32x4*>(a1t + r * AS + 16 * w + 4 * q) = a1;
+      *reinterpret_cast<f32x4*>(a1t + (i & 1) * TILE * AS + r * AS + 16 * w + 4 * q) = a1;
       if (valid && a1_out) *reinterpret_cast<f32x4*>(a1_out + (size_t)row * L + 16 * w + 4 * q) = a1;
     }
     __syncthreads();
     if (!loader) {
       // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* ar = a1t + r * AS + 4 * q;
+      const float* ar = a1t + (i & 1) * TILE * AS + r * AS + 4 * q;
 #pragma unroll
       for (int T = 0; T < 8; ++T) {
         const f32x4 bv = *reinterpret_cast<const f32x4*>(ar + 16 * T);
@@ -127,7 +127,6 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
         s2 += (double)p2;
       }
     }
-    __syncthreads();
   }
   __shared__ double red[2 * (NU_THREADS / 64)];
   block_sum2(s1, s2, red);
@@ -152,5 +151,148 @@ extern "C" int pdg_node_net(int n_nodes, const float* aggr, const float* x, cons
                      bn1, Wn2, bn2, a1n, a2n, partials);
   PDG_CHECK_LAUNCH("pdg_node_net");
   if (nparts) *nparts = grid;
+  return PDG_OK;
+}
+
+// ============================================================================ node_net backward
+// Backward of node_net for one step, the work of pdg_mlp2_bwd + pdg_gemm_dual in one pass
+// (models.py:240-243 / :202-208): with gy = d loss / d x_{t+1} (the residual branch's input),
+//   gz2  = LN_bwd(gy) * [a2 > 0]                 (loader waves, elementwise, -> LDS + HBM)
+//   gz1  = (W2^T gz2) * [a1 > 0]                 (compute waves, K = 128)
+//   gaggr = W1a^T gz1,  gx_part = W1b^T gz1 + gy  (compute waves, two K = 128 products)
+// Same register-stationary structure as node_net_kernel (wave w owns output features
+// [16w, 16w+16) of all three products: 96 VGPRs of transposed weights); bitwise the
+// results of the separate kernels.
+namespace {
+
+constexpr int GS = L + 8;                      // LDS row stride of the gz2 / gz1 tiles
+
+// Loader waves: tile t's gz2 rows into `buf` (and to HBM).  Lane lt covers chunks lt and
+// lt + 256 of the 16 x 32 (row, 16-B chunk) tile.
+__device__ __forceinline__ void load_gz2_tile(float* __restrict__ buf, int t, int N, int lt,
+                                              const float* __restrict__ gy, const float* __restrict__ a2,
+                                              const LNStat& st, const pdg_ln_bwd& lb,
+                                              const float* __restrict__ g, float* __restrict__ gz2_out) {
+  f32x4 gv[2], av[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
+    const bool ok = node < N;
+    gv[u] = ok ? reinterpret_cast<const f32x4*>(gy + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    av[u] = ok ? reinterpret_cast<const f32x4*>(a2 + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
+    const f32x4 gg = reinterpret_cast<const f32x4*>(g)[j];
+    f32x4 z;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {   // ln_relu_bwd (pdg_bwd.hip), element by element
+      const float xhat = div_den(av[u][e] - st.mean, st.den, st.rstd);
+      const float ga = st.rstd * (gg[e] * gv[u][e] - lb.c1) - xhat * lb.c2;
+      z[e] = av[u][e] > 0.f ? ga : 0.f;
+    }
+    *reinterpret_cast<f32x4*>(buf + rr * GS + 4 * j) = z;
+    if (node < N) reinterpret_cast<f32x4*>(gz2_out + (size_t)node * L)[j] = z;
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
+    int N, const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ a1,
+    const pdg_ln_stat* __restrict__ stp, const pdg_ln_bwd* __restrict__ lbp, const float* __restrict__ lg,
+    const float* __restrict__ W2T, const float* __restrict__ W1aT, const float* __restrict__ W1bT,
+    float* __restrict__ gz2_out, float* __restrict__ gz1_out, float* __restrict__ gaggr,
+    float* __restrict__ gx_part) {
+  __shared__ __attribute__((aligned(16))) float gz2t[2 * TILE * GS];
+  __shared__ __attribute__((aligned(16))) float gz1t[2 * TILE * GS];
+  const int w = wave_id(), l = lane_id();
+  const bool loader = w >= NU_COMPUTE;
+  const int ntiles = tiles_of(N);
+  const int lt = threadIdx.x - 64 * NU_COMPUTE;
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const pdg_ln_bwd lb = *lbp;
+  const int r = l & 15, q = l >> 4;
+  const int oc = 16 * w + 4 * q;   // this lane's 4 output features (D rows 4q .. 4q+3 of block w)
+  f32x4 w2f[8], waf[8], wbf[8];
+  if (!loader) {
+    const float* p2 = W2T + (size_t)(16 * w + r) * L + 4 * q;
+    const float* pa = W1aT + (size_t)(16 * w + r) * L + 4 * q;
+    const float* pb = W1bT + (size_t)(16 * w + r) * L + 4 * q;
+#pragma unroll
+    for (int T = 0; T < 8; ++T) {
+      w2f[T] = *reinterpret_cast<const f32x4*>(p2 + 16 * T);
+      waf[T] = *reinterpret_cast<const f32x4*>(pa + 16 * T);
+      wbf[T] = *reinterpret_cast<const f32x4*>(pb + 16 * T);
+    }
+  }
+  if (loader && nu_tile(0) < ntiles) load_gz2_tile(gz2t, nu_tile(0), N, lt, gy, a2, st, lb, lg, gz2_out);
+  __syncthreads();
+  for (int i = 0;; ++i) {
+    const int tile = nu_tile(i);
+    if (tile >= ntiles) break;   // uniform across the block
+    const int row = tile * TILE + r;
+    const bool valid = row < N;
+    const int rc = valid ? row : N - 1;
+    float* g1 = gz1t + (i & 1) * TILE * GS;
+    if (loader) {
+      const int nt = nu_tile(i + 1);
+      if (nt < ntiles) load_gz2_tile(gz2t + ((i + 1) & 1) * TILE * GS, nt, N, lt, gy, a2, st, lb, lg, gz2_out);
+    } else {
+      const f32x4 a1v = *reinterpret_cast<const f32x4*>(a1 + (size_t)rc * L + oc);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* zr = gz2t + (i & 1) * TILE * GS + r * GS + 4 * q;
+#pragma unroll
+      for (int T = 0; T < 8; ++T) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(zr + 16 * T);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[T][jj], bv[jj], acc, 0, 0, 0);
+      }
+      f32x4 z1;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) z1[c] = a1v[c] > 0.f ? acc[c] : 0.f;   // relu_mask_acc
+      *reinterpret_cast<f32x4*>(g1 + r * GS + oc) = z1;
+      if (valid) *reinterpret_cast<f32x4*>(gz1_out + (size_t)row * L + oc) = z1;
+    }
+    __syncthreads();
+    if (!loader) {
+      const f32x4 res = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + oc);
+      f32x4 acc_a = {0.f, 0.f, 0.f, 0.f}, acc_b = {0.f, 0.f, 0.f, 0.f};
+      const float* zr = g1 + r * GS + 4 * q;
+#pragma unroll
+      for (int T = 0; T < 8; ++T) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(zr + 16 * T);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          acc_a = __builtin_amdgcn_mfma_f32_16x16x4f32(waf[T][jj], bv[jj], acc_a, 0, 0, 0);
+          acc_b = __builtin_amdgcn_mfma_f32_16x16x4f32(wbf[T][jj], bv[jj], acc_b, 0, 0, 0);
+        }
+      }
+      acc_b += res;
+      if (valid) {
+        *reinterpret_cast<f32x4*>(gaggr + (size_t)row * L + oc) = acc_a;
+        *reinterpret_cast<f32x4*>(gx_part + (size_t)row * L + oc) = acc_b;
+      }
+    }
+  }
+}
+
+extern "C" int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, const float* a1n, const pdg_ln_stat* st,
+                            const pdg_ln_bwd* lb, const float* ln_g, const float* Wn2T, const float* Wn1aT,
+                            const float* Wn1bT, float* gz2, float* gz1, float* gaggr, float* gx_part, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_node_bwd: n_nodes must be > 0");
+  PDG_CHECK_ARG(gy && a2n && a1n && st && lb && ln_g && gz2 && gz1 && gaggr && gx_part,
+                "pdg_node_bwd: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2n) && PDG_ALIGNED(a1n) && PDG_ALIGNED(Wn2T) &&
+                    PDG_ALIGNED(Wn1aT) && PDG_ALIGNED(Wn1bT) && PDG_ALIGNED(gz2) && PDG_ALIGNED(gz1) &&
+                    PDG_ALIGNED(gaggr) && PDG_ALIGNED(gx_part) && PDG_ALIGNED(ln_g),
+                "pdg_node_bwd: misaligned pointer");
+  const int tiles = tiles_of(n_nodes);
+  const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
+  const int grid = tiles < cap ? tiles : cap;
+  hipLaunchKernelGGL(node_bwd_kernel, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes, gy, a2n, a1n,
+                     st, lb, ln_g, Wn2T, Wn1aT, Wn1bT, gz2, gz1, gaggr, gx_part);
+  PDG_CHECK_LAUNCH("pdg_node_bwd");
   return PDG_OK;
 }

@@ -280,10 +280,9 @@ class EPDEngine:
             # node_net tail: n_t = LN_n(a2n_t), gy = gx_next   (x_{t+1} = n_t + x_t)
             colsum(N, gx_next, None, d["a2n"], st[d["i_n"]], "processor.node_net.4.weight",
                    "processor.node_net.4.bias", lb[0])
-            lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], lb[0],
-                             _p(P["processor.node_net.4.weight"]), _p(T["Wn2T"]), _p(gz2n), _p(gz1n), s)
-            lib.pdg_gemm_dual(N, _p(gz1n), _p(T["Wn1aT"]), _p(T["Wn1bT"]), None, _p(gx_next), _p(gaggr),
-                              _p(gx_part), s)
+            self._t("node_bwd", lib.pdg_node_bwd, N, _p(gx_next), _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], lb[0],
+                    _p(P["processor.node_net.4.weight"]), _p(T["Wn2T"]), _p(T["Wn1aT"]), _p(T["Wn1bT"]),
+                    _p(gz2n), _p(gz1n), _p(gaggr), _p(gx_part), s)
             # edge_net LayerNorm sums.  message: gy = gaggr[dst], reduced per node from the forward's
             # sum of xhat over each destination segment; edge update: gy = ge_next (per edge)
             lib.pdg_ln_colsum_nodes(N, _p(gaggr), _p(plan.rowptr_dst), _p(d["xs"]), _p(self._part_col), np_, s)

@@ -40,6 +40,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_ln_colsum_nodes": [I, P, P, P, P, P, P],
     "pdg_ln_colsum_finalize": [P, I, P, P, P, P, P, P],
     "pdg_mlp2_bwd": [I, P, P, P, P, P, P, P, P, P, P, P],
+    "pdg_node_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdg_gemm_dual": [I, P, P, P, P, P, P, P, P],
     "pdg_gemm_sum2": [I, P, P, P, P, P, P, P],
     "pdg_edge_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],

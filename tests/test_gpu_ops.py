@@ -333,3 +333,35 @@ def test_node_net_matches_separate_kernels(env, N):
     h1 = torch.relu(torch.cat([aggr, x], 1).double() @ W1.double().T + b1.double())
     h2 = torch.relu(h1 @ W2.double().T + b2.double())
     assert rel(a21, h2) < TOL
+
+
+@pytest.mark.parametrize("N", [7, 1031, 40328])
+def test_node_bwd_matches_separate_kernels(env, N):
+    """Fused node_net backward == pdg_mlp2_bwd + pdg_gemm_dual (res1 = gy) bitwise."""
+    import struct
+    lib, sh, _ = env
+    s = sh()
+    gy = rnd(N, L)
+    a1 = torch.relu(rnd(N, L))
+    a2 = torch.relu(rnd(N, L))
+    g = rnd(L) * 0.3 + 1.0
+    W2T, _ = lin(L, L)
+    WaT, _ = lin(L, L)
+    WbT, _ = lin(L, L)
+    r64 = a2.double()
+    mean, sd = float(r64.mean()), float(r64.std(unbiased=False))
+    den = float(torch.tensor(sd, dtype=torch.float32) + 1e-5)
+    st = torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, N * L)),
+                          dtype=torch.uint8).cuda()
+    lb = torch.frombuffer(bytearray(struct.pack("ffdd", 0.013, -0.021, 1.0, 2.0)), dtype=torch.uint8).cuda()
+    outs0 = [torch.empty(N, L, device="cuda") for _ in range(4)]
+    lib.pdg_mlp2_bwd(N, gy.data_ptr(), None, a2.data_ptr(), a1.data_ptr(), st.data_ptr(), lb.data_ptr(),
+                     g.data_ptr(), W2T.data_ptr(), outs0[0].data_ptr(), outs0[1].data_ptr(), s)
+    lib.pdg_gemm_dual(N, outs0[1].data_ptr(), WaT.data_ptr(), WbT.data_ptr(), None, gy.data_ptr(),
+                      outs0[2].data_ptr(), outs0[3].data_ptr(), s)
+    outs1 = [torch.empty(N, L, device="cuda") for _ in range(4)]
+    assert lib.pdg_node_bwd(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), lb.data_ptr(),
+                            g.data_ptr(), W2T.data_ptr(), WaT.data_ptr(), WbT.data_ptr(), *[o.data_ptr() for o in outs1],
+                            s) == 0
+    for a, b in zip(outs0, outs1):
+        assert torch.equal(a, b)

@@ -6,8 +6,13 @@ TAG=$1; CFG=$2; shift 2
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out/$TAG"
 for v in "$@"; do
-  if [ "$v" = default ]; then lib=$R/p-div-gnn_amd/pdg/libpdivgnn_hip.so; else lib=$R/variants/$v/libpdivgnn_hip.so; fi
-  PDG_LIB=$lib timeout -k 10 300 python "$R/bench.py" --config "$CFG" --no-cpu-baseline \
+  # a variant is either a library (variants/<v>/libpdivgnn_hip.so, run by this tree's bench) or a
+  # whole tree (variants/<v>/bench.py with its own in-tree library)
+  benchpy=$R/bench.py
+  if [ "$v" = default ]; then lib=$R/p-div-gnn_amd/pdg/libpdivgnn_hip.so
+  elif [ -f "$R/variants/$v/bench.py" ]; then benchpy=$R/variants/$v/bench.py; lib=$R/variants/$v/p-div-gnn_amd/pdg/libpdivgnn_hip.so
+  else lib=$R/variants/$v/libpdivgnn_hip.so; fi
+  PDG_LIB=$lib timeout -k 10 300 python "$benchpy" --config "$CFG" --no-cpu-baseline \
     > "$R/gpurun_out/$TAG/$v.c$CFG.log" 2>&1 || { echo "$v failed"; tail -5 "$R/gpurun_out/$TAG/$v.c$CFG.log"; exit 1; }
   python - "$R/gpurun_out/$TAG/$v.c$CFG.log" "$v" <<'PY'
 import json, sys
