@@ -171,7 +171,8 @@ def main():
     eng = trainer.engine
     # HIP events bracket the timed kernels' launches in the last `ev_steps` steps of the timed
     # region (each event pair costs a few us of queue time; sampling keeps the region clean)
-    timed_kernels = ["edge_fwd", "edge_bwd", "wgrad_W2", "segment_sum", "node_net", "node_bwd", "pq_scatter_bwd"]
+    timed_kernels = ["edge_fwd", "edge_bwd", "wgrad_W2", "segment_sum", "node_net", "node_bwd", "node_pq",
+                     "gemm_sum2", "pq_scatter_bwd"]
     ev_steps = min(args.steps, 3)
     if pg is not None:
         dist.barrier()

@@ -80,6 +80,11 @@ int pdg_ln_finalize(const double* partials, int nparts, double count, pdg_ln_sta
 int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                 const float* ln_b, const float* x_res, float* x_out, const float* W1,
                 float* P, float* Q, void* stream);
+/* Same result as pdg_node_pq (bitwise), with Wa/Wb held in registers by 8 compute waves and
+ * the LN + residual rows staged by 4 loader waves (better for node-sized row counts). */
+int pdg_node_pq_rw(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                   const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
+                   float* Q, void* stream);
 
 /* Fused edge pass of one message-passing step (models.py:215-222, :233-238).
  * with_edge_update == 0 skips the edge-update branch (the last step's e_S is never consumed,
@@ -173,6 +178,9 @@ int pdg_gemm_dual(int rows, const float* in, const float* W0T, const float* W1T,
 /* out = res + W0T in0 + W1T in1. */
 int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
                   const float* res, float* out, void* stream);
+/* Same result as pdg_gemm_sum2 (bitwise), weights held in registers. */
+int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
+                     const float* res, float* out, void* stream);
 
 /* Fused edge backward of one step: both edge_net evaluations' LN/relu/Linear2 backward
  * (message: gy = gaggr[dst]; edge update: gy = ge_next), gC = gz1m + gz1e,

@@ -296,3 +296,178 @@ extern "C" int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, cons
   PDG_CHECK_LAUNCH("pdg_node_bwd");
   return PDG_OK;
 }
+
+// ============================================================================ node P/Q pre-pass
+// x_t = LN(a2_prev) [+ x_prev] (loader waves, -> LDS + HBM), P = Wa x_t, Q = Wb x_t (compute
+// waves, weights Wa = W1[:, 0:128], Wb = W1[:, 128:256] of edge_net.0 held in registers).
+// Bitwise the results of pdg_node_pq (node_pq_kernel).
+namespace {
+
+template <bool RES>
+__device__ __forceinline__ void load_xt_tile(float* __restrict__ buf, int t, int N, int lt,
+                                             const float* __restrict__ a2p, const float* __restrict__ xres,
+                                             const LNStat& st, const float* __restrict__ g,
+                                             const float* __restrict__ b, float* __restrict__ xout) {
+  f32x4 av[2], rv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
+    const bool ok = node < N;
+    av[u] = ok ? reinterpret_cast<const f32x4*>(a2p + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (RES) rv[u] = ok ? reinterpret_cast<const f32x4*>(xres + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
+    const f32x4 gg = reinterpret_cast<const f32x4*>(g)[j], bb = reinterpret_cast<const f32x4*>(b)[j];
+    f32x4 y;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {   // ln_res_frag (pdg_fwd.hip), element by element
+      float v = div_den(av[u][e] - st.mean, st.den, st.rstd) * gg[e] + bb[e];
+      if (RES) v += rv[u][e];
+      y[e] = v;
+    }
+    *reinterpret_cast<f32x4*>(buf + rr * GS + 4 * j) = y;
+    if (node < N) reinterpret_cast<f32x4*>(xout + (size_t)node * L)[j] = y;
+  }
+}
+
+}  // namespace
+
+template <bool RES>
+__global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
+    int N, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
+    const float* __restrict__ lb, const float* __restrict__ xres, float* __restrict__ xout,
+    const float* __restrict__ W1, float* __restrict__ P, float* __restrict__ Q) {
+  __shared__ __attribute__((aligned(16))) float xt[2 * TILE * GS];
+  const int w = wave_id(), l = lane_id();
+  const bool loader = w >= NU_COMPUTE;
+  const int ntiles = tiles_of(N);
+  const int lt = threadIdx.x - 64 * NU_COMPUTE;
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const int r = l & 15, q = l >> 4;
+  const int oc = 16 * w + 4 * q;
+  f32x4 waf[8], wbf[8];
+  if (!loader) {
+    const float* pa = W1 + (size_t)(16 * w + r) * (3 * L) + 4 * q;
+#pragma unroll
+    for (int T = 0; T < 8; ++T) {
+      waf[T] = *reinterpret_cast<const f32x4*>(pa + 16 * T);
+      wbf[T] = *reinterpret_cast<const f32x4*>(pa + L + 16 * T);
+    }
+  }
+  if (loader && nu_tile(0) < ntiles) load_xt_tile<RES>(xt, nu_tile(0), N, lt, a2p, xres, st, lg, lb, xout);
+  __syncthreads();
+  for (int i = 0;; ++i) {
+    const int tile = nu_tile(i);
+    if (tile >= ntiles) break;   // uniform across the block
+    if (loader) {
+      const int nt = nu_tile(i + 1);
+      if (nt < ntiles) load_xt_tile<RES>(xt + ((i + 1) & 1) * TILE * GS, nt, N, lt, a2p, xres, st, lg, lb, xout);
+    } else {
+      const int row = tile * TILE + r;
+      f32x4 acc_p = {0.f, 0.f, 0.f, 0.f}, acc_q = {0.f, 0.f, 0.f, 0.f};
+      const float* xr = xt + (i & 1) * TILE * GS + r * GS + 4 * q;
+#pragma unroll
+      for (int T = 0; T < 8; ++T) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(xr + 16 * T);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          acc_p = __builtin_amdgcn_mfma_f32_16x16x4f32(waf[T][jj], bv[jj], acc_p, 0, 0, 0);
+          acc_q = __builtin_amdgcn_mfma_f32_16x16x4f32(wbf[T][jj], bv[jj], acc_q, 0, 0, 0);
+        }
+      }
+      if (row < N) {
+        *reinterpret_cast<f32x4*>(P + (size_t)row * L + oc) = acc_p;
+        *reinterpret_cast<f32x4*>(Q + (size_t)row * L + oc) = acc_q;
+      }
+    }
+    __syncthreads();   // tile i's buffer is free for the loaders of iteration i + 1
+  }
+}
+
+extern "C" int pdg_node_pq_rw(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                              const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
+                              float* Q, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_node_pq_rw: n_nodes must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(x_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) && PDG_ALIGNED(W1) &&
+                    PDG_ALIGNED(ln_g) && PDG_ALIGNED(ln_b) && PDG_ALIGNED(x_res),
+                "pdg_node_pq_rw: misaligned pointer");
+  const int tiles = tiles_of(n_nodes);
+  const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
+  const int grid = tiles < cap ? tiles : cap;
+  if (x_res)
+    hipLaunchKernelGGL(node_pq_rw_kernel<true>, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes,
+                       a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q);
+  else
+    hipLaunchKernelGGL(node_pq_rw_kernel<false>, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes,
+                       a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q);
+  PDG_CHECK_LAUNCH("pdg_node_pq_rw");
+  return PDG_OK;
+}
+
+// ============================================================================ summed transposed GEMMs
+// out = W0T in0 + W1T in1 [+ res] (the input gradient of x through P = Wa x, Q = Wb x plus the
+// node_net path), weights held in registers; bitwise pdg_gemm_sum2.
+__global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
+    int N, const float* __restrict__ in0, const float* __restrict__ in1, const float* __restrict__ W0T,
+    const float* __restrict__ W1T, const float* __restrict__ res, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float xin[2 * XBUF];
+  const int w = wave_id(), l = lane_id();
+  const bool loader = w >= NU_COMPUTE;
+  const int ntiles = tiles_of(N);
+  const int lt = threadIdx.x - 64 * NU_COMPUTE;
+  const int r = l & 15, q = l >> 4;
+  const int oc = 16 * w + 4 * q;
+  f32x4 wf[16];
+  if (!loader) {
+    const float* p0 = W0T + (size_t)(16 * w + r) * L + 4 * q;
+    const float* p1 = W1T + (size_t)(16 * w + r) * L + 4 * q;
+#pragma unroll
+    for (int T = 0; T < 8; ++T) {
+      wf[T] = *reinterpret_cast<const f32x4*>(p0 + 16 * T);
+      wf[8 + T] = *reinterpret_cast<const f32x4*>(p1 + 16 * T);
+    }
+  }
+  if (loader && nu_tile(0) < ntiles) load_tile(xin, nu_tile(0), N, lt, in0, in1);
+  __syncthreads();
+  for (int i = 0;; ++i) {
+    const int tile = nu_tile(i);
+    if (tile >= ntiles) break;   // uniform across the block
+    if (loader) {
+      const int nt = nu_tile(i + 1);
+      if (nt < ntiles) load_tile(xin + ((i + 1) & 1) * XBUF, nt, N, lt, in0, in1);
+    } else {
+      const int row = tile * TILE + r;
+      const int rc = row < N ? row : N - 1;
+      f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+      if (res) rv = *reinterpret_cast<const f32x4*>(res + (size_t)rc * L + oc);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* xr = xin + (i & 1) * XBUF + r * XS + 4 * q;
+#pragma unroll
+      for (int T = 0; T < 16; ++T) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(xr + 16 * T);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[T][jj], bv[jj], acc, 0, 0, 0);
+      }
+      if (res) acc += rv;
+      if (row < N) *reinterpret_cast<f32x4*>(out + (size_t)row * L + oc) = acc;
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
+                                const float* res, float* out, void* stream) {
+  PDG_CHECK_ARG(rows > 0, "pdg_gemm_sum2_rw: rows must be > 0");
+  PDG_CHECK_ARG(PDG_ALIGNED(in0) && PDG_ALIGNED(in1) && PDG_ALIGNED(out) && PDG_ALIGNED(W0T) && PDG_ALIGNED(W1T) &&
+                    PDG_ALIGNED(res),
+                "pdg_gemm_sum2_rw: misaligned pointer");
+  const int tiles = tiles_of(rows);
+  const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
+  const int grid = tiles < cap ? tiles : cap;
+  hipLaunchKernelGGL(gemm_sum2_rw_kernel, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, rows, in0, in1, W0T,
+                     W1T, res, out);
+  PDG_CHECK_LAUNCH("pdg_gemm_sum2_rw");
+  return PDG_OK;
+}

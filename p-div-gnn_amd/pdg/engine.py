@@ -165,8 +165,8 @@ class EPDEngine:
         for t in range(steps):
             i_m, i_e, i_n = 2 + 3 * t, 3 + 3 * t, 4 + 3 * t
             x_t = self._empty(N, L)
-            lib.pdg_node_pq(N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_t), _p(W1),
-                            _p(Pm), _p(Qm), s)
+            self._t("node_pq", lib.pdg_node_pq_rw, N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev),
+                    _p(x_prev), _p(x_t), _p(W1), _p(Pm), _p(Qm), s)
             # the last step's edge update has no consumer (models.py:316 decodes nodes only)
             eu = t < steps - 1
             e_t = self._empty(E, L)
@@ -298,7 +298,8 @@ class EPDEngine:
                     _p(gz2m), _p(gz1m), _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), s)
             self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
                     _p(plan.perm_src), _p(gz1m), _p(gz1e if eu else None), _p(gP), _p(gQ), s)
-            lib.pdg_gemm_sum2(N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part), _p(gx_t), s)
+            self._t("gemm_sum2", lib.pdg_gemm_sum2_rw, N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part),
+                    _p(gx_t), s)
             segs["W2"].append((gz2m, d["a1m"], E))
             if eu:
                 segs["W2"].append((gz2e, d["a1e"], E))

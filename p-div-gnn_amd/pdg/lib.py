@@ -28,6 +28,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_encoder_fwd": [I, I, P, P, P, P, P, P, P, P, P, P],
     "pdg_ln_finalize": [P, I, c_double, P, P],
     "pdg_node_pq": [I, P, P, P, P, P, P, P, P, P, P],
+    "pdg_node_pq_rw": [I, P, P, P, P, P, P, P, P, P, P],
     "pdg_edge_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
     "pdg_segment_sum": [I, P, P, P, P, P, P, P, P],
     "pdg_node_mlp1": [I, P, P, P, P, P, P],
@@ -43,6 +44,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_node_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdg_gemm_dual": [I, P, P, P, P, P, P, P, P],
     "pdg_gemm_sum2": [I, P, P, P, P, P, P, P],
+    "pdg_gemm_sum2_rw": [I, P, P, P, P, P, P, P],
     "pdg_edge_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "pdg_pq_scatter_bwd": [I, P, P, P, P, P, P, P, P],
     "pdg_wgrad_accum": [I, P, P, P, P, P, I, P],

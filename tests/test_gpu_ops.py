@@ -365,3 +365,40 @@ def test_node_bwd_matches_separate_kernels(env, N):
                             s) == 0
     for a, b in zip(outs0, outs1):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("N,res", [(7, True), (1031, False), (40328, True)])
+def test_register_weight_kernels_match_lds_kernels(env, N, res):
+    """pdg_node_pq_rw / pdg_gemm_sum2_rw (weights in registers) == pdg_node_pq / pdg_gemm_sum2
+    (weights in LDS) bitwise."""
+    import struct
+    lib, sh, _ = env
+    s = sh()
+    a2 = torch.relu(rnd(N, L))
+    xr = rnd(N, L) if res else None
+    g, b = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
+    W1, _ = lin(L, 3 * L)
+    r64 = a2.double()
+    mean, sd = float(r64.mean()), float(r64.std(unbiased=False))
+    den = float(torch.tensor(sd, dtype=torch.float32) + 1e-5)
+    st = torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, N * L)),
+                          dtype=torch.uint8).cuda()
+    outs = []
+    for fn in (lib.pdg_node_pq, lib.pdg_node_pq_rw):
+        x, P, Q = (torch.empty(N, L, device="cuda") for _ in range(3))
+        assert fn(N, a2.data_ptr(), st.data_ptr(), g.data_ptr(), b.data_ptr(), xr.data_ptr() if res else None,
+                  x.data_ptr(), W1.data_ptr(), P.data_ptr(), Q.data_ptr(), s) == 0
+        outs.append((x, P, Q))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+    i0, i1 = rnd(N, L), rnd(N, L)
+    W0T, _ = lin(L, L)
+    W1T, _ = lin(L, L)
+    rr = rnd(N, L) if res else None
+    o = []
+    for fn in (lib.pdg_gemm_sum2, lib.pdg_gemm_sum2_rw):
+        out = torch.empty(N, L, device="cuda")
+        assert fn(N, i0.data_ptr(), i1.data_ptr(), W0T.data_ptr(), W1T.data_ptr(), rr.data_ptr() if res else None,
+                  out.data_ptr(), s) == 0
+        o.append(out)
+    assert torch.equal(o[0], o[1])
