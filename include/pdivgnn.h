@@ -259,6 +259,22 @@ int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream);
 int pdg_adam(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
              float lr, float beta1, float beta2, float eps, int step, const int* skip_flag, void* stream);
 
+/* ---------------------------------------------------------------- device-side collate (§8f row 1) */
+/* One copy job: dst[i] = src[i] (+ add for the integer kinds), i < count.  `src`/`dst` are
+ * device pointers; the job table itself lives in device memory (40 bytes per job). */
+enum { PDG_COPY_F32 = 0, PDG_COPY_B32 = 1, PDG_COPY_B64 = 2 };
+typedef struct pdg_copy_job {
+  const void* src;
+  void* dst;
+  int64_t count;
+  int64_t add;
+  int32_t kind;
+  int32_t pad_;
+} pdg_copy_job;
+/* Assemble a minibatch from HBM-resident graphs (PyG collate, gnn_train.py:387-394): runs all
+ * jobs (njobs <= 65535, the largest count max_count) in one launch. */
+int pdg_collate(const pdg_copy_job* jobs, int njobs, long max_count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

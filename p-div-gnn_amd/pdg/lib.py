@@ -57,6 +57,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_div_bwd": [I, P, I, P, P, P, P, P, P, I, I, P, P],
     "pdg_transpose": [I, I, I, P, P, P],
     "pdg_nonfinite": [P, c_int64, P, P],
+    "pdg_collate": [P, I, ctypes.c_long, P],
     "pdg_adam": [c_int64, P, P, P, P, c_float, c_float, c_float, c_float, I, P, P],
 }
 _RESTYPES = {"pdg_last_error": ctypes.c_char_p}
