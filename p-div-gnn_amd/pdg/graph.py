@@ -179,3 +179,24 @@ class Batch(Data):
         out = super().to(device, non_blocking=non_blocking)
         out._data_list = self._data_list
         return out
+
+
+class DataLoader:
+    """PyG ``DataLoader`` subset used by the reference scripts (gnn_train.py:387-394,
+    gnn_inference.py:103-107): host collate of ``batch_size`` graphs, optional shuffle."""
+
+    def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False,
+                 generator: torch.Generator | None = None) -> None:
+        self.dataset = dataset
+        self.batch_size = int(batch_size)
+        self.shuffle = shuffle
+        self.generator = generator
+
+    def __len__(self) -> int:
+        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def __iter__(self):
+        n = len(self.dataset)
+        order = torch.randperm(n, generator=self.generator).tolist() if self.shuffle else list(range(n))
+        for i in range(0, n, self.batch_size):
+            yield Batch.from_data_list([self.dataset[j] for j in order[i:i + self.batch_size]])
