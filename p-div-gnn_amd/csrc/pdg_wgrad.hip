@@ -428,31 +428,30 @@ __device__ __forceinline__ int x6_addr(int r, int b) {
   return r * X6_ROWB + (b ^ (((r & 3) << 6) | (((r >> 2) & 3) << 4)));
 }
 
-// bf16 round-to-nearest-even of x, as the upper half of a float.
-__device__ __forceinline__ unsigned bf16_rne(float x) {
-  const unsigned u = __float_as_uint(x);
-  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
-}
-
-// x = hi + mid + lo exactly.
-__device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& lo) {
-  h = bf16_rne(x);
-  const float r1 = x - __uint_as_float(h << 16);
-  m = bf16_rne(r1);
-  lo = bf16_rne(r1 - __uint_as_float(m << 16));
+// (x0, x1) = hi + mid + lo exactly, per element: bf16 round-to-nearest-even of x, of the
+// remainder and of the rest, two elements per v_cvt_pk_bf16_f32 (a bf16 widens to float by
+// a 16-bit shift); each term comes out as a packed pair (x0 in the low half).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& h, unsigned& m, unsigned& lo) {
+  h = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, bf16x2));
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+  m = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
+  const float q0 = r0 - __uint_as_float(m << 16), q1 = r1 - __uint_as_float(m & 0xffff0000u);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){q0, q1}, bf16x2));
 }
 
 // Split 4 rows x 4 columns and write them: row i of this thread goes to image row 4 rg + i.
 __device__ __forceinline__ void x6_store(unsigned char* img, int cg, int rg, const f32x4 (&v)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    unsigned h[4], m[4], lo[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) split3(v[i][c], h[c], m[c], lo[c]);
+    unsigned h0, m0, l0, h1, m1, l1;
+    split3_pair(v[i][0], v[i][1], h0, m0, l0);
+    split3_pair(v[i][2], v[i][3], h1, m1, l1);
     const int off = x6_addr(4 * rg + i, 8 * cg);
-    *reinterpret_cast<u32x2*>(img + off) = u32x2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
-    *reinterpret_cast<u32x2*>(img + X6_TERM + off) = u32x2{m[0] | (m[1] << 16), m[2] | (m[3] << 16)};
-    *reinterpret_cast<u32x2*>(img + 2 * X6_TERM + off) = u32x2{lo[0] | (lo[1] << 16), lo[2] | (lo[3] << 16)};
+    *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
+    *reinterpret_cast<u32x2*>(img + X6_TERM + off) = u32x2{m0, m1};
+    *reinterpret_cast<u32x2*>(img + 2 * X6_TERM + off) = u32x2{l0, l1};
   }
 }
 
