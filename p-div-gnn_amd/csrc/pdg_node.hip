@@ -29,23 +29,33 @@ constexpr int XS = 2 * L + 8;                 // [aggr | x] tile row stride (flo
 constexpr int AS = L + 8;                     // layer-1 tile row stride: 136
 constexpr int XBUF = TILE * XS;               // floats per [aggr | x] buffer
 
-// Loader waves (256 lanes): copy rows 16 t .. 16 t + 15 of aggr and x into the
+// Loader waves (256 lanes): copy rows 16 t .. 16 t + 15 of aggr and x into a
 // tile buffer; lane (row lr = lane >> 5 (+8), chunk j = lane & 31), 4 independent
-// 16-B loads per lane.  Rows past N are zero.
-__device__ __forceinline__ void load_tile(float* __restrict__ xb, int t, int N, int lt,
-                                          const float* __restrict__ aggr, const float* __restrict__ x) {
-  const int j = lt & 31, lr = lt >> 5;
+// 16-B loads per lane.  Rows past N are zero.  Three buffers: the loads of tile
+// i + 2 are issued before the barrier of iteration i and written after it, so
+// their latency overlaps two compute phases.
+struct TileRegs {
   f32x4 v[4];
+};
+
+// Issue the loads of tile t (no wait: the registers are consumed after the next barrier).
+__device__ __forceinline__ void fetch_tile(TileRegs& tr, int t, int N, int lt, const float* __restrict__ aggr,
+                                           const float* __restrict__ x) {
+  const int j = lt & 31, lr = lt >> 5;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int r = lr + 8 * (u >> 1), node = t * TILE + r;
     const float* src = (u & 1) ? x : aggr;
-    v[u] = node < N ? reinterpret_cast<const f32x4*>(src + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    tr.v[u] = node < N ? reinterpret_cast<const f32x4*>(src + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+}
+
+__device__ __forceinline__ void store_tile(float* __restrict__ xb, int lt, const TileRegs& tr) {
+  const int j = lt & 31, lr = lt >> 5;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int r = lr + 8 * (u >> 1);
-    *reinterpret_cast<f32x4*>(xb + r * XS + (u & 1) * L + 4 * j) = v[u];
+    *reinterpret_cast<f32x4*>(xb + r * XS + (u & 1) * L + 4 * j) = tr.v[u];
   }
 }
 
@@ -57,7 +67,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
     int N, const float* __restrict__ aggr, const float* __restrict__ x, const float* __restrict__ W1,
     const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
     float* __restrict__ a1_out, float* __restrict__ a2_out, double* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float xin[2 * XBUF];
+  __shared__ __attribute__((aligned(16))) float xin[3 * XBUF];
   __shared__ __attribute__((aligned(16))) float a1t[2 * TILE * AS];   // double-buffered: one barrier per tile
   const int w = wave_id(), l = lane_id();
   const bool loader = w >= NU_COMPUTE;
@@ -75,18 +85,26 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
     for (int T = 0; T < 8; ++T) w2f[T] = *reinterpret_cast<const f32x4*>(w2r + 16 * T);
   }
   double s1 = 0, s2 = 0;
-  if (loader && nu_tile(0) < ntiles) load_tile(xin, nu_tile(0), N, lt, aggr, x);
+  TileRegs tr;
+  if (loader) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (nu_tile(k) < ntiles) {
+        fetch_tile(tr, nu_tile(k), N, lt, aggr, x);
+        store_tile(xin + k * XBUF, lt, tr);
+      }
+  }
   __syncthreads();
   for (int i = 0;; ++i) {
     const int tile = nu_tile(i);
     if (tile >= ntiles) break;   // uniform across the block
-    const float* xb = xin + (i & 1) * XBUF;
+    const float* xb = xin + (i % 3) * XBUF;
     const int row = tile * TILE + r;
     const bool valid = row < N;
+    const bool ahead = nu_tile(i + 2) < ntiles;
     f32x4 a1 = {0.f, 0.f, 0.f, 0.f};
     if (loader) {
-      const int nt = nu_tile(i + 1);
-      if (nt < ntiles) load_tile(xin + ((i + 1) & 1) * XBUF, nt, N, lt, aggr, x);
+      if (ahead) fetch_tile(tr, nu_tile(i + 2), N, lt, aggr, x);
     } else {
       // layer 1: a1 = relu(W1 [aggr | x] + b1), K = 256
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -105,7 +123,9 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
       if (valid && a1_out) *reinterpret_cast<f32x4*>(a1_out + (size_t)row * L + 16 * w + 4 * q) = a1;
     }
     __syncthreads();
-    if (!loader) {
+    if (loader) {
+      if (ahead) store_tile(xin + ((i + 2) % 3) * XBUF, lt, tr);   // last read in iteration i - 1
+    } else {
       // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       const float* ar = a1t + (i & 1) * TILE * AS + r * AS + 4 * q;
@@ -168,19 +188,25 @@ namespace {
 constexpr int GS = L + 8;                      // LDS row stride of the gz2 / gz1 tiles
 
 // Loader waves: tile t's gz2 rows into `buf` (and to HBM).  Lane lt covers chunks lt and
-// lt + 256 of the 16 x 32 (row, 16-B chunk) tile.
-__device__ __forceinline__ void load_gz2_tile(float* __restrict__ buf, int t, int N, int lt,
-                                              const float* __restrict__ gy, const float* __restrict__ a2,
-                                              const LNStat& st, const pdg_ln_bwd& lb,
-                                              const float* __restrict__ g, float* __restrict__ gz2_out) {
+// lt + 256 of the 16 x 32 (row, 16-B chunk) tile; loads issued one iteration ahead.
+struct Gz2Regs {
   f32x4 gv[2], av[2];
+};
+
+__device__ __forceinline__ void fetch_gz2(Gz2Regs& rg, int t, int N, int lt, const float* __restrict__ gy,
+                                          const float* __restrict__ a2) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
     const bool ok = node < N;
-    gv[u] = ok ? reinterpret_cast<const f32x4*>(gy + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-    av[u] = ok ? reinterpret_cast<const f32x4*>(a2 + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    rg.gv[u] = ok ? reinterpret_cast<const f32x4*>(gy + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    rg.av[u] = ok ? reinterpret_cast<const f32x4*>(a2 + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+}
+
+__device__ __forceinline__ void store_gz2(float* __restrict__ buf, int t, int N, int lt, const Gz2Regs& rg,
+                                          const LNStat& st, const pdg_ln_bwd& lb, const float* __restrict__ g,
+                                          float* __restrict__ gz2_out) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
@@ -188,9 +214,9 @@ __device__ __forceinline__ void load_gz2_tile(float* __restrict__ buf, int t, in
     f32x4 z;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {   // ln_relu_bwd (pdg_bwd.hip), element by element
-      const float xhat = div_den(av[u][e] - st.mean, st.den, st.rstd);
-      const float ga = st.rstd * (gg[e] * gv[u][e] - lb.c1) - xhat * lb.c2;
-      z[e] = av[u][e] > 0.f ? ga : 0.f;
+      const float xhat = div_den(rg.av[u][e] - st.mean, st.den, st.rstd);
+      const float ga = st.rstd * (gg[e] * rg.gv[u][e] - lb.c1) - xhat * lb.c2;
+      z[e] = rg.av[u][e] > 0.f ? ga : 0.f;
     }
     *reinterpret_cast<f32x4*>(buf + rr * GS + 4 * j) = z;
     if (node < N) reinterpret_cast<f32x4*>(gz2_out + (size_t)node * L)[j] = z;
@@ -205,7 +231,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
     const float* __restrict__ W2T, const float* __restrict__ W1aT, const float* __restrict__ W1bT,
     float* __restrict__ gz2_out, float* __restrict__ gz1_out, float* __restrict__ gaggr,
     float* __restrict__ gx_part) {
-  __shared__ __attribute__((aligned(16))) float gz2t[2 * TILE * GS];
+  __shared__ __attribute__((aligned(16))) float gz2t[3 * TILE * GS];
   __shared__ __attribute__((aligned(16))) float gz1t[2 * TILE * GS];
   const int w = wave_id(), l = lane_id();
   const bool loader = w >= NU_COMPUTE;
@@ -227,7 +253,15 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
       wbf[T] = *reinterpret_cast<const f32x4*>(pb + 16 * T);
     }
   }
-  if (loader && nu_tile(0) < ntiles) load_gz2_tile(gz2t, nu_tile(0), N, lt, gy, a2, st, lb, lg, gz2_out);
+  Gz2Regs rg;
+  if (loader) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (nu_tile(k) < ntiles) {
+        fetch_gz2(rg, nu_tile(k), N, lt, gy, a2);
+        store_gz2(gz2t + k * TILE * GS, nu_tile(k), N, lt, rg, st, lb, lg, gz2_out);
+      }
+  }
   __syncthreads();
   for (int i = 0;; ++i) {
     const int tile = nu_tile(i);
@@ -235,14 +269,14 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
     const int row = tile * TILE + r;
     const bool valid = row < N;
     const int rc = valid ? row : N - 1;
+    const bool ahead = nu_tile(i + 2) < ntiles;
     float* g1 = gz1t + (i & 1) * TILE * GS;
     if (loader) {
-      const int nt = nu_tile(i + 1);
-      if (nt < ntiles) load_gz2_tile(gz2t + ((i + 1) & 1) * TILE * GS, nt, N, lt, gy, a2, st, lb, lg, gz2_out);
+      if (ahead) fetch_gz2(rg, nu_tile(i + 2), N, lt, gy, a2);
     } else {
       const f32x4 a1v = *reinterpret_cast<const f32x4*>(a1 + (size_t)rc * L + oc);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* zr = gz2t + (i & 1) * TILE * GS + r * GS + 4 * q;
+      const float* zr = gz2t + (i % 3) * TILE * GS + r * GS + 4 * q;
 #pragma unroll
       for (int T = 0; T < 8; ++T) {
         const f32x4 bv = *reinterpret_cast<const f32x4*>(zr + 16 * T);
@@ -256,7 +290,9 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
       if (valid) *reinterpret_cast<f32x4*>(gz1_out + (size_t)row * L + oc) = z1;
     }
     __syncthreads();
-    if (!loader) {
+    if (loader) {
+      if (ahead) store_gz2(gz2t + ((i + 2) % 3) * TILE * GS, nu_tile(i + 2), N, lt, rg, st, lb, lg, gz2_out);
+    } else {
       const f32x4 res = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + oc);
       f32x4 acc_a = {0.f, 0.f, 0.f, 0.f}, acc_b = {0.f, 0.f, 0.f, 0.f};
       const float* zr = g1 + r * GS + 4 * q;
@@ -303,19 +339,26 @@ extern "C" int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, cons
 // Bitwise the results of pdg_node_pq (node_pq_kernel).
 namespace {
 
-template <bool RES>
-__device__ __forceinline__ void load_xt_tile(float* __restrict__ buf, int t, int N, int lt,
-                                             const float* __restrict__ a2p, const float* __restrict__ xres,
-                                             const LNStat& st, const float* __restrict__ g,
-                                             const float* __restrict__ b, float* __restrict__ xout) {
+struct XtRegs {
   f32x4 av[2], rv[2];
+};
+
+template <bool RES>
+__device__ __forceinline__ void fetch_xt(XtRegs& rg, int t, int N, int lt, const float* __restrict__ a2p,
+                                         const float* __restrict__ xres) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
     const bool ok = node < N;
-    av[u] = ok ? reinterpret_cast<const f32x4*>(a2p + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-    if (RES) rv[u] = ok ? reinterpret_cast<const f32x4*>(xres + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    rg.av[u] = ok ? reinterpret_cast<const f32x4*>(a2p + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (RES) rg.rv[u] = ok ? reinterpret_cast<const f32x4*>(xres + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+}
+
+template <bool RES>
+__device__ __forceinline__ void store_xt(float* __restrict__ buf, int t, int N, int lt, const XtRegs& rg,
+                                         const LNStat& st, const float* __restrict__ g,
+                                         const float* __restrict__ b, float* __restrict__ xout) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
@@ -323,8 +366,8 @@ __device__ __forceinline__ void load_xt_tile(float* __restrict__ buf, int t, int
     f32x4 y;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {   // ln_res_frag (pdg_fwd.hip), element by element
-      float v = div_den(av[u][e] - st.mean, st.den, st.rstd) * gg[e] + bb[e];
-      if (RES) v += rv[u][e];
+      float v = div_den(rg.av[u][e] - st.mean, st.den, st.rstd) * gg[e] + bb[e];
+      if (RES) v += rg.rv[u][e];
       y[e] = v;
     }
     *reinterpret_cast<f32x4*>(buf + rr * GS + 4 * j) = y;
@@ -339,7 +382,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
     int N, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ xres, float* __restrict__ xout,
     const float* __restrict__ W1, float* __restrict__ P, float* __restrict__ Q) {
-  __shared__ __attribute__((aligned(16))) float xt[2 * TILE * GS];
+  __shared__ __attribute__((aligned(16))) float xt[3 * TILE * GS];
   const int w = wave_id(), l = lane_id();
   const bool loader = w >= NU_COMPUTE;
   const int ntiles = tiles_of(N);
@@ -356,18 +399,26 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
       wbf[T] = *reinterpret_cast<const f32x4*>(pa + L + 16 * T);
     }
   }
-  if (loader && nu_tile(0) < ntiles) load_xt_tile<RES>(xt, nu_tile(0), N, lt, a2p, xres, st, lg, lb, xout);
+  XtRegs rg;
+  if (loader) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (nu_tile(k) < ntiles) {
+        fetch_xt<RES>(rg, nu_tile(k), N, lt, a2p, xres);
+        store_xt<RES>(xt + k * TILE * GS, nu_tile(k), N, lt, rg, st, lg, lb, xout);
+      }
+  }
   __syncthreads();
   for (int i = 0;; ++i) {
     const int tile = nu_tile(i);
     if (tile >= ntiles) break;   // uniform across the block
+    const bool ahead = nu_tile(i + 2) < ntiles;
     if (loader) {
-      const int nt = nu_tile(i + 1);
-      if (nt < ntiles) load_xt_tile<RES>(xt + ((i + 1) & 1) * TILE * GS, nt, N, lt, a2p, xres, st, lg, lb, xout);
+      if (ahead) fetch_xt<RES>(rg, nu_tile(i + 2), N, lt, a2p, xres);
     } else {
       const int row = tile * TILE + r;
       f32x4 acc_p = {0.f, 0.f, 0.f, 0.f}, acc_q = {0.f, 0.f, 0.f, 0.f};
-      const float* xr = xt + (i & 1) * TILE * GS + r * GS + 4 * q;
+      const float* xr = xt + (i % 3) * TILE * GS + r * GS + 4 * q;
 #pragma unroll
       for (int T = 0; T < 8; ++T) {
         const f32x4 bv = *reinterpret_cast<const f32x4*>(xr + 16 * T);
@@ -382,7 +433,9 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
         *reinterpret_cast<f32x4*>(Q + (size_t)row * L + oc) = acc_q;
       }
     }
-    __syncthreads();   // tile i's buffer is free for the loaders of iteration i + 1
+    __syncthreads();
+    if (loader && ahead)   // buffer (i + 2) % 3 was last read in iteration i - 1
+      store_xt<RES>(xt + ((i + 2) % 3) * TILE * GS, nu_tile(i + 2), N, lt, rg, st, lg, lb, xout);
   }
 }
 
@@ -412,7 +465,7 @@ extern "C" int pdg_node_pq_rw(int n_nodes, const float* a2_prev, const pdg_ln_st
 __global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
     int N, const float* __restrict__ in0, const float* __restrict__ in1, const float* __restrict__ W0T,
     const float* __restrict__ W1T, const float* __restrict__ res, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) float xin[2 * XBUF];
+  __shared__ __attribute__((aligned(16))) float xin[3 * XBUF];
   const int w = wave_id(), l = lane_id();
   const bool loader = w >= NU_COMPUTE;
   const int ntiles = tiles_of(N);
@@ -429,21 +482,29 @@ __global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
       wf[8 + T] = *reinterpret_cast<const f32x4*>(p1 + 16 * T);
     }
   }
-  if (loader && nu_tile(0) < ntiles) load_tile(xin, nu_tile(0), N, lt, in0, in1);
+  TileRegs tr;
+  if (loader) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (nu_tile(k) < ntiles) {
+        fetch_tile(tr, nu_tile(k), N, lt, in0, in1);
+        store_tile(xin + k * XBUF, lt, tr);
+      }
+  }
   __syncthreads();
   for (int i = 0;; ++i) {
     const int tile = nu_tile(i);
     if (tile >= ntiles) break;   // uniform across the block
+    const bool ahead = nu_tile(i + 2) < ntiles;
     if (loader) {
-      const int nt = nu_tile(i + 1);
-      if (nt < ntiles) load_tile(xin + ((i + 1) & 1) * XBUF, nt, N, lt, in0, in1);
+      if (ahead) fetch_tile(tr, nu_tile(i + 2), N, lt, in0, in1);
     } else {
       const int row = tile * TILE + r;
       const int rc = row < N ? row : N - 1;
       f32x4 rv = {0.f, 0.f, 0.f, 0.f};
       if (res) rv = *reinterpret_cast<const f32x4*>(res + (size_t)rc * L + oc);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* xr = xin + (i & 1) * XBUF + r * XS + 4 * q;
+      const float* xr = xin + (i % 3) * XBUF + r * XS + 4 * q;
 #pragma unroll
       for (int T = 0; T < 16; ++T) {
         const f32x4 bv = *reinterpret_cast<const f32x4*>(xr + 16 * T);
@@ -454,6 +515,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
       if (row < N) *reinterpret_cast<f32x4*>(out + (size_t)row * L + oc) = acc;
     }
     __syncthreads();
+    if (loader && ahead) store_tile(xin + ((i + 2) % 3) * XBUF, lt, tr);   // last read in iteration i - 1
   }
 }
 
