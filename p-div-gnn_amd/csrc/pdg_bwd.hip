@@ -403,8 +403,18 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_bwd_kern
     float* __restrict__ gz1m, float* __restrict__ gz2e, float* __restrict__ gz1e, float* __restrict__ gC,
     float* __restrict__ ge_out) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+#if PDG_EDGE_X6
+  load_wblock_swz(lds, WcT, L, 0);                                   // Wc^T (fp32)
+  unsigned char* w2p = reinterpret_cast<unsigned char*>(lds + 128 * 128);
+  load_wplanes(w2p, W2T, L, 0);                                      // W2^T as bf16 term planes
+#define PDG_GEMM_2(acc, v) gemm128_x6(acc, w2p, v)
+#define PDG_GEMM_C(acc, v) gemm128_swz(acc, lds, v)
+#else
   load_wblock(lds, W2T, L, 0);
   load_wblock(lds + WBLK, WcT, L, 0);
+#define PDG_GEMM_2(acc, v) PDG_GEMM_W2(acc, lds, v)
+#define PDG_GEMM_C(acc, v) gemm128(acc, lds + WBLK, v)
+#endif
   __syncthreads();
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
   const LNStat ste = *reinterpret_cast<const LNStat*>(EU ? ste_p : stm_p);
@@ -423,7 +433,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_bwd_kern
     ln_relu_bwd(v, a, stm, lbm, lg);
     if (valid) store_frag(gz2m + (size_t)row * L, v);
     zero_acc(acc);
-    gemm128(acc, lds, v);
+    PDG_GEMM_2(acc, v);
     load_frag(a, a1m + (size_t)rc * L);
     relu_mask_acc(v, acc, a);
     if (valid) store_frag(gz1m + (size_t)row * L, v);
@@ -436,7 +446,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_bwd_kern
       ln_relu_bwd(v, a, ste, lbe, lg);
       if (valid) store_frag(gz2e + (size_t)row * L, v);
       zero_acc(acc);
-      gemm128(acc, lds, v);
+      PDG_GEMM_2(acc, v);
       load_frag(a, a1e + (size_t)rc * L);
       relu_mask_acc(v, acc, a);
       if (valid) store_frag(gz1e + (size_t)row * L, v);
@@ -445,13 +455,15 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_bwd_kern
     // ---- ge_out = ge_next + Wc^T gC
     if (valid) store_frag(gC + (size_t)row * L, v);
     zero_acc(acc);
-    gemm128(acc, lds + WBLK, v);
+    PDG_GEMM_C(acc, v);
     if (EU) {
       load_frag(a, ge_next + (size_t)rc * L);
       PDG_FOR_FRAG(s) ACC(acc, s) += a[s];
     }
     if (valid) store_acc(ge_out + (size_t)row * L, acc);
   }
+#undef PDG_GEMM_2
+#undef PDG_GEMM_C
 }
 
 extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
@@ -469,12 +481,13 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
                 "pdg_edge_bwd: edge-update arguments missing or misaligned");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd: ge_out must not alias ge_next");
   const int grid = persistent_grid(n_edges, EDGE_WAVES, 1);
+  const size_t shm = PDG_EDGE_X6 ? (size_t)EDGE_LDS_BYTES : 2 * WBLK * sizeof(float);
   if (ge_next)
-    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(64 * EDGE_WAVES), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(64 * EDGE_WAVES), shm, (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
                        gz1m, gz2e, gz1e, gC, ge_out);
   else
-    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(64 * EDGE_WAVES), 2 * WBLK * sizeof(float), (hipStream_t)stream,
+    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(64 * EDGE_WAVES), shm, (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, WcT, gz2m,
                        gz1m, gz2e, gz1e, gC, ge_out);
   PDG_CHECK_LAUNCH("pdg_edge_bwd");

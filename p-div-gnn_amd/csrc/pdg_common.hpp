@@ -37,7 +37,10 @@ constexpr int WBLK = 128 * WPAD;        // floats per weight block in LDS (69,63
 #ifndef PDG_EDGE_WAVES
 #define PDG_EDGE_WAVES 12
 #endif
-constexpr int EDGE_WAVES = PDG_EDGE_WAVES;  // waves per block of the fused edge kernels (one block per CU)
+constexpr int EDGE_WAVES = PDG_EDGE_WAVES;
+#ifndef PDG_EDGE_X6
+#define PDG_EDGE_X6 1   // edge kernels: W2 GEMMs as bf16x6 (0: fp32 MFMA, padded LDS images)
+#endif  // waves per block of the fused edge kernels (one block per CU)
 constexpr float LN_EPS = 1e-5f;         // torch_geometric LayerNorm default eps
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -168,6 +171,155 @@ __device__ __forceinline__ void gemm128(Acc& acc, const float* __restrict__ wl, 
       }
     }
     PDG_FENCE();
+  }
+}
+
+// Timing experiments only (results are wrong): drop the W2 GEMMs of the edge kernels.
+#ifdef PDG_DIAG_NOW2
+#define PDG_GEMM_W2(acc, w, v) ((acc).b[0][0] += (v)[0])
+#else
+#define PDG_GEMM_W2(acc, w, v) gemm128(acc, w, v)
+#endif
+
+// ----------------------------------------------------------------------------- edge-kernel weights
+// The fused edge kernels hold two weights in LDS: Wc (or Wc^T) in fp32 and W2 (or W2^T) as
+// three bf16 term planes for the bf16x6 product below; 64 KB + 96 KB = the whole 160 KB,
+// so neither image is padded: 16-byte chunks are XOR-swizzled by the row's low 4 bits.
+// Both layouts make every ds_read_b128 lane group of the A reads hit 16 distinct slots.
+constexpr int EDGE_LDS_BYTES = 128 * 128 * 4 + 3 * 128 * 128 * 2;   // 163,840
+
+// fp32 image, unpadded: element (o, c) at float o*128 + 4*((c >> 2) ^ (o & 15)) + (c & 3).
+__device__ __forceinline__ void load_wblock_swz(float* __restrict__ lds, const float* __restrict__ W, int ld,
+                                                int col0) {
+  for (int idx = threadIdx.x; idx < 128 * 32; idx += blockDim.x) {
+    const int o = idx >> 5, c4 = idx & 31;
+    const f32x4 val = *reinterpret_cast<const f32x4*>(W + (size_t)o * ld + col0 + 4 * c4);
+    *reinterpret_cast<f32x4*>(lds + o * 128 + 4 * (c4 ^ (o & 15))) = val;
+  }
+}
+
+// gemm128 on the swizzled fp32 image (same MFMA order and pipelining, so the same results).
+__device__ __forceinline__ void gemm128_swz(Acc& acc, const float* __restrict__ wl, const float (&v)[FRAG]) {
+  const int l = lane_id(), i = l & 15, q = l >> 4;
+  // chunk (4t + q) ^ i = 4 (t ^ (i >> 2)) + (q ^ (i & 3))
+  const float* base = wl + opaque(i * 128 + 4 * (q ^ (i & 3)));
+  const int ti = i >> 2;
+  f32x4 a0[2], a1[2];
+  a0[0] = *reinterpret_cast<const f32x4*>(base + 0 * 16 * 128 + 16 * (0 ^ ti));
+  a0[1] = *reinterpret_cast<const f32x4*>(base + 1 * 16 * 128 + 16 * (0 ^ ti));
+#pragma unroll
+  for (int it = 0; it < 32; it += 2) {
+    {
+      const int nt = (it + 1) >> 2, np = (it + 1) & 3;
+      a1[0] = *reinterpret_cast<const f32x4*>(base + (2 * np) * 16 * 128 + 16 * (nt ^ ti));
+      a1[1] = *reinterpret_cast<const f32x4*>(base + (2 * np + 1) * 16 * 128 + 16 * (nt ^ ti));
+      const int t = it >> 2, p = it & 3;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc.b[2 * p] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[0][j], v[4 * t + j], acc.b[2 * p], 0, 0, 0);
+        acc.b[2 * p + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[1][j], v[4 * t + j], acc.b[2 * p + 1], 0, 0, 0);
+      }
+    }
+    PDG_FENCE();
+    {
+      if (it + 2 < 32) {
+        const int nt = (it + 2) >> 2, np = (it + 2) & 3;
+        a0[0] = *reinterpret_cast<const f32x4*>(base + (2 * np) * 16 * 128 + 16 * (nt ^ ti));
+        a0[1] = *reinterpret_cast<const f32x4*>(base + (2 * np + 1) * 16 * 128 + 16 * (nt ^ ti));
+      }
+      const int t = (it + 1) >> 2, p = (it + 1) & 3;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc.b[2 * p] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0][j], v[4 * t + j], acc.b[2 * p], 0, 0, 0);
+        acc.b[2 * p + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[1][j], v[4 * t + j], acc.b[2 * p + 1], 0, 0, 0);
+      }
+    }
+    PDG_FENCE();
+  }
+}
+
+// bf16x6 product on the matrix cores, fp32 accuracy: W = W0 + W1 + W2 and v = v0 + v1 + v2
+// split exactly into bf16 terms (round-to-nearest, 24 significant bits), six products
+// Wi vj (i + j <= 2) summed in fp32 smallest first (dropped terms < 2^-24 |W||v|).
+// v_mfma_f32_16x16x32_bf16, K chunk m sums the lane's fragment elements v[8m .. 8m+7]
+// (features 32m + 4q + {0..3} and 32m + 16 + 4q + {0..3}); the plane images store each
+// 32-feature block of a weight row permuted to match: position 8q + 4 half + e.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3_pair_u(float x0, float x1, unsigned& h, unsigned& m, unsigned& lo) {
+  h = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){x0, x1}, bf16x2_t));
+  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
+  m = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){r0, r1}, bf16x2_t));
+  const float q0 = r0 - __uint_as_float(m << 16), q1 = r1 - __uint_as_float(m & 0xffff0000u);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2_t){q0, q1}, bf16x2_t));
+}
+
+constexpr int PLANE_BYTES = 128 * 128 * 2;
+
+// Byte offset of weight (o, f) in a plane image.
+__device__ __forceinline__ int plane_off(int o, int f) {
+  const int m = f >> 5, fl = f & 31, half = fl >> 4, qq = (fl & 15) >> 2, e = fl & 3;
+  const int chunk = 4 * m + qq;
+  return o * 256 + 16 * (chunk ^ (o & 15)) + 2 * (4 * half + e);
+}
+
+// Build the three term planes of W[o][col0 + f] (row stride ld) at `planes` (bytes).
+__device__ __forceinline__ void load_wplanes(unsigned char* __restrict__ planes, const float* __restrict__ W,
+                                             int ld, int col0) {
+  for (int idx = threadIdx.x; idx < 128 * 64; idx += blockDim.x) {
+    const int o = idx >> 6, f = 2 * (idx & 63);   // features f, f + 1 (same chunk, adjacent positions)
+    const float* wr = W + (size_t)o * ld + col0 + f;
+    unsigned h, m, lo;
+    split3_pair_u(wr[0], wr[1], h, m, lo);
+    const int off = plane_off(o, f);
+    *reinterpret_cast<unsigned*>(planes + off) = h;
+    *reinterpret_cast<unsigned*>(planes + PLANE_BYTES + off) = m;
+    *reinterpret_cast<unsigned*>(planes + 2 * PLANE_BYTES + off) = lo;
+  }
+}
+
+__device__ __forceinline__ void gemm128_x6(Acc& acc, const unsigned char* __restrict__ planes,
+                                           const float (&v)[FRAG]) {
+  const int l = lane_id(), i = l & 15, q = l >> 4;
+  // chunk (4m + q) ^ i = 4 (m ^ (i >> 2)) + (q ^ (i & 3))
+  const unsigned char* base = planes + opaque(i * 256 + 16 * (q ^ (i & 3)));
+  const int mi = i >> 2;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    unsigned h[4], md[4], lo[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) split3_pair_u(v[8 * m + 2 * p], v[8 * m + 2 * p + 1], h[p], md[p], lo[p]);
+    const bf16x8_t B0 = __builtin_bit_cast(bf16x8_t, (u32x4_t){h[0], h[1], h[2], h[3]});
+    const bf16x8_t B1 = __builtin_bit_cast(bf16x8_t, (u32x4_t){md[0], md[1], md[2], md[3]});
+    const bf16x8_t B2 = __builtin_bit_cast(bf16x8_t, (u32x4_t){lo[0], lo[1], lo[2], lo[3]});
+    const int co = 64 * (m ^ mi);
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {   // output blocks 2pr, 2pr+1: two independent chains
+      bf16x8_t A[2][3];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const unsigned char* a = base + (2 * pr + u) * 16 * 256 + co;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) A[u][pl] = *reinterpret_cast<const bf16x8_t*>(a + pl * PLANE_BYTES);
+      }
+      f32x4 t0 = acc.b[2 * pr], t1 = acc.b[2 * pr + 1];
+      t0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][2], B0, t0, 0, 0, 0);
+      t1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1][2], B0, t1, 0, 0, 0);
+      t0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][1], B1, t0, 0, 0, 0);
+      t1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1][1], B1, t1, 0, 0, 0);
+      t0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][0], B2, t0, 0, 0, 0);
+      t1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1][0], B2, t1, 0, 0, 0);
+      t0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][1], B0, t0, 0, 0, 0);
+      t1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1][1], B0, t1, 0, 0, 0);
+      t0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][0], B1, t0, 0, 0, 0);
+      t1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1][0], B1, t1, 0, 0, 0);
+      acc.b[2 * pr] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[0][0], B0, t0, 0, 0, 0);
+      acc.b[2 * pr + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A[1][0], B0, t1, 0, 0, 0);
+      PDG_FENCE();
+    }
   }
 }
 

@@ -381,8 +381,18 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kern
     float* __restrict__ a2m, float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m,
     double* __restrict__ part_e) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+#if PDG_EDGE_X6
+  load_wblock_swz(lds, W1, 3 * L, 2 * L);   // W_c (fp32): edge-feature block
+  unsigned char* w2p = reinterpret_cast<unsigned char*>(lds + 128 * 128);
+  load_wplanes(w2p, W2, L, 0);             // W2 as three bf16 term planes
+#define PDG_GEMM_C(acc, v) gemm128_swz(acc, lds, v)
+#define PDG_GEMM_2(acc, v) gemm128_x6(acc, w2p, v)
+#else
   load_wblock(lds, W1, 3 * L, 2 * L);   // W_c: edge-feature block
   load_wblock(lds + WBLK, W2, L, 0);
+#define PDG_GEMM_C(acc, v) gemm128(acc, lds, v)
+#define PDG_GEMM_2(acc, v) PDG_GEMM_W2(acc, lds + WBLK, v)
+#endif
   __syncthreads();
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const int l = lane_id();
@@ -399,7 +409,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kern
     // C = W_c e_t + b1 (shared by both edge_net evaluations)
     Acc C;
     zero_acc(C);
-    gemm128(C, lds, v);
+    PDG_GEMM_C(C, v);
     {
       const float* bp = b1 + lane_col();
 #pragma unroll
@@ -413,7 +423,7 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kern
     if (valid && a1m) store_frag(a1m + (size_t)row * L, v);   // a1m / a1e: kept for the backward only
     Acc Z;
     zero_acc(Z);
-    gemm128(Z, lds + WBLK, v);
+    PDG_GEMM_2(Z, v);
     bias_relu(v, Z, b2);
     if (valid) store_frag(a2m + (size_t)row * L, v);
     accum_stats(v, valid, sm1, sm2);
@@ -423,14 +433,28 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kern
       load_frag(ve, a1e + (size_t)(valid ? row : rc) * L);
 #endif
       zero_acc(Z);
-      gemm128(Z, lds + WBLK, ve);
+      PDG_GEMM_2(Z, ve);
       bias_relu(v, Z, b2);
       if (valid) store_frag(a2e + (size_t)row * L, v);
       accum_stats(v, valid, se1, se2);
     }
   }
-  write_partials(sm1, sm2, part_m);
-  if (EU) write_partials(se1, se2, part_e);
+#undef PDG_GEMM_C
+#undef PDG_GEMM_2
+  // the weight images are dead once every wave has passed block_sum2's first barrier
+  double* red = reinterpret_cast<double*>(lds);
+  block_sum2(sm1, sm2, red);
+  if (threadIdx.x == 0) {
+    part_m[2 * blockIdx.x] = sm1;
+    part_m[2 * blockIdx.x + 1] = sm2;
+  }
+  if (EU) {
+    block_sum2(se1, se2, red + 32);
+    if (threadIdx.x == 0) {
+      part_e[2 * blockIdx.x] = se1;
+      part_e[2 * blockIdx.x + 1] = se2;
+    }
+  }
 }
 
 extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
@@ -445,7 +469,7 @@ extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat
   PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd: edge-update outputs missing or misaligned");
   const int grid = persistent_grid(n_edges, EDGE_WAVES, 1);
-  const size_t shm = 2 * WBLK * sizeof(float);
+  const size_t shm = PDG_EDGE_X6 ? (size_t)EDGE_LDS_BYTES : 2 * WBLK * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
 #define PDG_EDGE_FWD(R, U)                                                                                     \
   hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(64 * EDGE_WAVES), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \
