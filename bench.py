@@ -117,6 +117,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--dp-mode", default="replica", choices=["replica", "sync"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     args = ap.parse_args()
@@ -153,7 +154,8 @@ def main():
     torch.manual_seed(69)
     model = EncodeProcessDecode(input_edges_features_size=1, message_passing_steps=cfg["steps"], latent_size=L,
                                 input_nodes_features_size=6, output_nodes_features_size=3, **stats).to(device)
-    trainer = Trainer(model, lr=1e-3, divergence=cfg["divergence"], divergence_penalty=10.0, process_group=pg)
+    trainer = Trainer(model, lr=1e-3, divergence=cfg["divergence"], divergence_penalty=10.0, process_group=pg,
+                      dp_mode=args.dp_mode)
     plan = plan_for(batch)
     N, E = plan.n_nodes, plan.n_edges
 
@@ -262,7 +264,7 @@ def main():
             "config": {"workload": cfg["workload"], "graphs_per_gpu": cfg["graphs"], "nodes_per_gpu": N,
                        "edges_per_gpu": E, "global_batch": cfg["graphs"] * world,
                        "message_passing_steps": cfg["steps"], "latent": L, "divergence": cfg["divergence"],
-                       "parallelism": f"graph-DP x{world}", "final_loss": round(loss, 6)},
+                       "parallelism": f"graph-DP x{world}" + ("" if args.dp_mode == "replica" else " (sync-LN)"), "final_loss": round(loss, 6)},
             "roofline": roof(dominant),
             "roofline_gather_scatter": [roof(k) for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
             "roofline_node_net": roof("node_net") if "node_net" in kt else None,

@@ -74,6 +74,11 @@ int pdg_encoder_fwd(int rows, int in_features, const float* x_in, const float* W
 
 /* Reduce LayerNorm partials -> statistics (mean, std_pop + eps). */
 int pdg_ln_finalize(const double* partials, int nparts, double count, pdg_ln_stat* out, void* stream);
+/* Exact data-parallel LayerNorm (optional "sync" DP mode): reduce the
+ * per-block partials to out2 = {sum, sumsq} (device, 2 doubles) for an all-reduce over
+ * ranks, then pdg_ln_finalize(out2, 1, global_count, ...).  New in this build: the
+ * reference LayerNorm (models.py:42-55) runs on one device and needs no exchange. */
+int pdg_ln_partials_sum(const double* partials, int nparts, double* out2, void* stream);
 
 /* Processor node pre-pass (models.py:221/236 re-associated): x_t = LN(a2_prev) [+ x_res];
  * P = W1[:, 0:128] x_t, Q = W1[:, 128:256] x_t  (W1 = processor.edge_net.0.weight, 128 x 384). */
@@ -156,6 +161,9 @@ int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* rowptr, cons
 int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g,
                            const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
                            void* stream);
+/* Sync DP mode, backward: after lb->S1 and lb->S2 were all-reduced over ranks, recompute
+ * lb->c1 = S1/M and lb->c2 = S2/(M std) with the global statistics in st. */
+int pdg_ln_bwd_rescale(const pdg_ln_stat* st, pdg_ln_bwd* lb, void* stream);
 
 /* MLP tail backward (LN -> relu -> Linear2 -> relu): ga2 = LNbwd(gy); gz2 = ga2 * [a2 > 0];
  * gz1 = (W2^T gz2) * [a1 > 0].  gy row k = gy_rows[gidx ? gidx[k] : k]. */

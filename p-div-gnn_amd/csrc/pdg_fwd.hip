@@ -247,6 +247,25 @@ extern "C" int pdg_ln_finalize(const double* partials, int nparts, double count,
   return PDG_OK;
 }
 
+// Exact data-parallel LayerNorm ("sync" mode): each rank reduces its
+// per-block partials to one (sum, sumsq) pair, the pairs are all-reduced over the
+// process group, and pdg_ln_finalize(pair, 1, global_count) yields the statistics of
+// the whole minibatch, as the reference computes them on one device (models.py:42-55).
+__global__ void ln_partials_sum_kernel(const double* __restrict__ part, int n, double* __restrict__ out2) {
+  __shared__ double red[2 * 16];
+  double a = 0, b = 0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) { a += part[2 * i]; b += part[2 * i + 1]; }
+  block_sum2(a, b, red);
+  if (threadIdx.x == 0) { out2[0] = a; out2[1] = b; }
+}
+
+extern "C" int pdg_ln_partials_sum(const double* partials, int nparts, double* out2, void* stream) {
+  PDG_CHECK_ARG(nparts > 0 && out2, "pdg_ln_partials_sum: empty");
+  hipLaunchKernelGGL(ln_partials_sum_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partials, nparts, out2);
+  PDG_CHECK_LAUNCH("pdg_ln_partials_sum");
+  return PDG_OK;
+}
+
 // ============================================================================ node P/Q pre-pass
 template <bool RES>
 __global__ __launch_bounds__(768, 3) void node_pq_kernel(int N, const float* __restrict__ a2p,

@@ -97,6 +97,8 @@ class EPDEngine:
         self._nparts = ctypes.c_int(0)
         # one weight-gradient slab per block of pdg_wgrad_segments: three blocks per CU
         self._nslabs = 3 * torch.cuda.get_device_properties(self.device).multi_processor_count
+        self._pair = torch.zeros(2, **f64)
+        self.sync = None
         # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
         self.timed: dict | None = None
 
@@ -117,8 +119,29 @@ class EPDEngine:
     def _empty(self, *shape):
         return torch.empty(*shape, dtype=torch.float32, device=self.device)
 
-    def _finalize(self, part, count: int, out_ptr: int, s) -> None:
-        lib.pdg_ln_finalize(part.data_ptr(), self._nparts.value, float(count), out_ptr, s)
+    def _finalize(self, part, count: int, out_ptr: int, s, edges: bool = False) -> None:
+        if self.sync is None:
+            lib.pdg_ln_finalize(part.data_ptr(), self._nparts.value, float(count), out_ptr, s)
+            return
+        # exact DP LayerNorm: statistics of the whole minibatch over all ranks
+        group, n_glob, e_glob = self.sync
+        lib.pdg_ln_partials_sum(part.data_ptr(), self._nparts.value, self._pair.data_ptr(), s)
+        torch.distributed.all_reduce(self._pair, group=group)
+        lib.pdg_ln_finalize(self._pair.data_ptr(), 1, float((e_glob if edges else n_glob) * L), out_ptr, s)
+
+    def _sync_bwd(self, lb_buf: "_StatBuf", i: int, st_ptr: int, s) -> None:
+        """Sync mode: all-reduce S1/S2 of backward scalar set i, then recompute c1/c2."""
+        if self.sync is None:
+            return
+        o = i * lb_buf.nbytes + 8               # pdg_ln_bwd: {float c1, c2; double S1, S2}
+        torch.distributed.all_reduce(lb_buf.buf[o:o + 16].view(torch.float64), group=self.sync[0])
+        lib.pdg_ln_bwd_rescale(st_ptr, lb_buf[i], s)
+
+    def set_sync(self, group, n_nodes_global: int = 0, n_edges_global: int = 0) -> None:
+        """Enable (group given) or disable (None) the exact data-parallel LayerNorm: every
+        graph-LayerNorm of forward and backward uses the statistics of the global minibatch
+        of n_nodes_global / n_edges_global rows, as one device running all of it would."""
+        self.sync = None if group is None else (group, int(n_nodes_global), int(n_edges_global))
 
     # ------------------------------------------------------------------ forward
     def forward(self, P: dict, stats8: torch.Tensor, plan: GraphPlan, pos, mean_stress, nodes_types,
@@ -147,7 +170,7 @@ class EPDEngine:
         lib.pdg_encoder_fwd(E, 1, _p(e_in), _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]),
                             _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]), _p(a1_ee), _p(a2_ee),
                             _p(self._part_a), np_, s)
-        self._finalize(self._part_a, E * L, st[1], s)
+        self._finalize(self._part_a, E * L, st[1], s, True)
         if need_grad:
             ctx.x_in, ctx.e_in, ctx.a1_ne, ctx.a2_ne, ctx.a1_ee, ctx.a2_ee = x_in, e_in, a1_ne, a2_ne, a1_ee, a2_ee
 
@@ -177,9 +200,9 @@ class EPDEngine:
             self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
                     _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
                     _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
-            self._finalize(self._part_a, E * L, st[i_m], s)
+            self._finalize(self._part_a, E * L, st[i_m], s, True)
             if eu:
-                self._finalize(self._part_b, E * L, st[i_e], s)
+                self._finalize(self._part_b, E * L, st[i_e], s, True)
             # aggregation (models.py:215-217) and node_net (:240-243)
             aggr = self._empty(N, L)
             xs = self._empty(N, L) if need_grad else None
@@ -248,10 +271,11 @@ class EPDEngine:
         lb = _StatBuf(4, LN_BWD_BYTES, self.device)
         segs: dict[str, list] = {k: [] for k in ("W2", "Wc", "Wa", "Wb", "Wn2", "Wn1a", "Wn1b", "d1", "ne2", "ee2")}
 
-        def colsum(rows, gy_rows, gidx, a2, st_ptr, gname, bname, lb_ptr):
+        def colsum(rows, gy_rows, gidx, a2, st_ptr, gname, bname, lb_i):
             lib.pdg_ln_colsum(rows, _p(gy_rows), _p(gidx), _p(a2), st_ptr, _p(self._part_col), np_, s)
             lib.pdg_ln_colsum_finalize(_p(self._part_col), self._nparts.value, _p(P[gname]), st_ptr,
-                                       _p(G[gname]), _p(G[bname]), lb_ptr, s)
+                                       _p(G[gname]), _p(G[bname]), lb[lb_i], s)
+            self._sync_bwd(lb, lb_i, st_ptr, s)
 
         gy = gy.contiguous()
         if ctx.scale_output:
@@ -279,7 +303,7 @@ class EPDEngine:
             ge_out = ge_bufs[t % 2]
             # node_net tail: n_t = LN_n(a2n_t), gy = gx_next   (x_{t+1} = n_t + x_t)
             colsum(N, gx_next, None, d["a2n"], st[d["i_n"]], "processor.node_net.4.weight",
-                   "processor.node_net.4.bias", lb[0])
+                   "processor.node_net.4.bias", 0)
             self._t("node_bwd", lib.pdg_node_bwd, N, _p(gx_next), _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], lb[0],
                     _p(P["processor.node_net.4.weight"]), _p(T["Wn2T"]), _p(T["Wn1aT"]), _p(T["Wn1bT"]),
                     _p(gz2n), _p(gz1n), _p(gaggr), _p(gx_part), s)
@@ -289,9 +313,10 @@ class EPDEngine:
             lib.pdg_ln_colsum_finalize(_p(self._part_col), self._nparts.value, _p(P["processor.edge_net.4.weight"]),
                                        st[d["i_m"]], _p(G["processor.edge_net.4.weight"]),
                                        _p(G["processor.edge_net.4.bias"]), lb[1], s)
+            self._sync_bwd(lb, 1, st[d["i_m"]], s)
             if eu:
                 colsum(E, ge_next, None, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
-                       "processor.edge_net.4.bias", lb[2])
+                       "processor.edge_net.4.bias", 2)
             self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr), _p(ge_next), _p(d["a2m"]),
                     _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]], st[d["i_e"]] if eu else None, lb[1],
                     lb[2] if eu else None, _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]),
@@ -313,14 +338,14 @@ class EPDEngine:
             ge_next = ge_out
         # encoders
         gz2, gz1 = self._empty(N, L), self._empty(N, L)
-        colsum(N, gx_next, None, ctx.a2_ne, st[0], "node_encoder.4.weight", "node_encoder.4.bias", lb[3])
+        colsum(N, gx_next, None, ctx.a2_ne, st[0], "node_encoder.4.weight", "node_encoder.4.bias", 3)
         lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], lb[3],
                          _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), s)
         segs["ne2"].append((gz2, ctx.a1_ne, N))
         lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
                              _p(G["node_encoder.0.bias"]), None, s)
         gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
-        colsum(E, ge_next, None, ctx.a2_ee, st[1], "edge_encoder.4.weight", "edge_encoder.4.bias", lb[3])
+        colsum(E, ge_next, None, ctx.a2_ee, st[1], "edge_encoder.4.weight", "edge_encoder.4.bias", 3)
         lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], lb[3],
                          _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), s)
         segs["ee2"].append((gz2e_, ctx.a1_ee, E))

@@ -6,7 +6,11 @@ Per step (one minibatch already resident in HBM):
   loss     sum_g NMSE_g / B  [+ lambda * sum_g div_g / B]                  (:168-197)
   backward                                                                 (:205)
   DP       one all-reduce (mean) of the flat fp32 gradient bucket over RCCL (graph-batch data
-           parallelism across GPUs; new in this build)
+           parallelism across GPUs; new in this build).  dp_mode="sync" instead
+           reproduces one device running the whole global minibatch: every graph-LayerNorm
+           all-reduces its (sum, sumsq) pair in the forward and its (S1, S2) pair in the
+           backward, the loss is divided by the GLOBAL number of graphs and the gradient
+           bucket is summed, not averaged (2 x 47 sixteen-byte collectives more per step).
   update   Adam(lr, betas=(0.9, 0.999), eps=1e-8) on the flat parameter buffer (:118, :206)
 
 Parameters and gradients live in one flat buffer each (the model's Parameters
@@ -26,7 +30,10 @@ from .plan import plan_for
 
 class Trainer:
     def __init__(self, model, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 divergence: bool = False, divergence_penalty: float = 1.0, process_group=None) -> None:
+                 divergence: bool = False, divergence_penalty: float = 1.0, process_group=None,
+                 dp_mode: str = "replica") -> None:
+        if dp_mode not in ("replica", "sync"):
+            raise ValueError("dp_mode must be 'replica' or 'sync'")
         dev = next(model.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("Trainer needs the model on a HIP device")
@@ -37,6 +44,7 @@ class Trainer:
         self.divergence = divergence
         self.penalty = float(divergence_penalty)
         self.pg = process_group
+        self.sync = dp_mode == "sync" and process_group is not None
         sizes = [int(torch.Size(s).numel()) for _, s in PARAM_SHAPES]
         total = sum(sizes)
         self.flat_p = torch.empty(total, dtype=torch.float32, device=dev)
@@ -66,24 +74,38 @@ class Trainer:
         return self._gt_cache[key]
 
     def step(self, batch) -> dict:
-        """One optimisation step; returns device scalars (no host sync)."""
+        """One optimisation step; returns device scalars (no host sync, except one read of the
+        global row counts in dp_mode="sync")."""
         m = self.model
         s = stream_handle(self.device)
         plan = plan_for(batch)
         stats8 = m.stats_tensor(self.device)
+        B, N = plan.n_graphs, plan.n_nodes
+        f32 = dict(dtype=torch.float32, device=self.device)
+        Bn = B                                      # loss normaliser (gnn_train.py:193/196)
+        if self.sync:
+            cnt = torch.tensor([N, plan.n_edges, B], dtype=torch.float64, device=self.device)
+            torch.distributed.all_reduce(cnt, group=self.pg)
+            n_g, e_g, Bn = (int(v) for v in cnt.tolist())
+            self.engine.set_sync(self.pg, n_g, e_g)
+        try:
+            return self._step(batch, plan, stats8, B, N, Bn, f32, s)
+        finally:
+            self.engine.set_sync(None)
+
+    def _step(self, batch, plan, stats8, B, N, Bn, f32, s) -> dict:
+        m = self.model
         y, ctx = self.engine.forward(self.P, stats8, plan, batch.pos, batch.mean_stress,
                                      batch.nodes_types.reshape(-1).contiguous(), batch.edge_attr.reshape(-1),
                                      m.message_passing_steps, True, False, True)
         gt = self._gt(batch)
-        B, N = plan.n_graphs, plan.n_nodes
-        f32 = dict(dtype=torch.float32, device=self.device)
         loss_g, den = torch.empty(B, **f32), torch.empty(B, 3, **f32)
         lib.pdg_nmse_fwd(B, plan.ptr.data_ptr(), gt.data_ptr(), y.data_ptr(), loss_g.data_ptr(), den.data_ptr(), s)
-        scale = torch.full((1,), 1.0 / B, **f32)
+        scale = torch.full((1,), 1.0 / Bn, **f32)
         gy = torch.empty(N, 3, **f32)
         lib.pdg_nmse_bwd(B, plan.ptr.data_ptr(), N, gt.data_ptr(), y.data_ptr(), den.data_ptr(), scale.data_ptr(), 0,
                          gy.data_ptr(), s)
-        out = {"nmse": loss_g.sum() / B}
+        out = {"nmse": loss_g.sum() / Bn}
         if self.divergence:
             types = batch.surfaces_nodes_for_div if batch.surfaces_nodes_for_div is not None else batch.nodes_types
             types = types.reshape(-1).to(torch.int64).contiguous()
@@ -92,17 +114,24 @@ class Trainer:
             lib.pdg_div_fwd(B, plan.ptr.data_ptr(), plan.a_rowptr.data_ptr(), plan.a_col.data_ptr(),
                             plan.a_val.data_ptr(), types.data_ptr(), y.data_ptr(), 0, div.data_ptr(),
                             loss_d.data_ptr(), s)
-            sd = torch.full((1,), self.penalty / B, **f32)
+            sd = torch.full((1,), self.penalty / Bn, **f32)
             lib.pdg_div_bwd(B, plan.ptr.data_ptr(), N, plan.at_rowptr.data_ptr(), plan.at_row.data_ptr(),
                             plan.at_comp.data_ptr(), plan.at_val.data_ptr(), div.data_ptr(), sd.data_ptr(), 0, 1,
                             gy.data_ptr(), s)
-            out["div"] = loss_d.sum() * (self.penalty / B)
+            out["div"] = loss_d.sum() * (self.penalty / Bn)
         self.flat_g.zero_()
         self.engine.backward(self.P, ctx, gy, self.G)
         del ctx
         if self.pg is not None:
             torch.distributed.all_reduce(self.flat_g, group=self.pg)
-            self.flat_g.mul_(1.0 / torch.distributed.get_world_size(self.pg))
+            if self.sync:                           # per-rank shares of the global-batch loss: sum
+                parts = torch.stack([out["nmse"], out.get("div", torch.zeros((), **f32))])
+                torch.distributed.all_reduce(parts, group=self.pg)
+                out["nmse"] = parts[0]
+                if "div" in out:
+                    out["div"] = parts[1]
+            else:
+                self.flat_g.mul_(1.0 / torch.distributed.get_world_size(self.pg))
         self.step_count += 1
         lib.pdg_nonfinite(self.flat_g.data_ptr(), self.flat_g.numel(), self._skip.data_ptr(), s)
         lib.pdg_adam(self.flat_p.numel(), self.flat_p.data_ptr(), self.flat_g.data_ptr(), self.exp_avg.data_ptr(),

@@ -3,8 +3,10 @@
 Both ranks run pdg.trainer.Trainer on cuda:0 with a gloo process group (RCCL
 refuses two ranks on one device; the Trainer's collective is the same
 `all_reduce` either way).  Checked: the all-reduced flat gradient bucket equals
-the mean of the per-shard fp64 oracle gradients, and the parameters stay
-bit-identical across ranks after several Adam steps.
+the mean of the per-shard fp64 oracle gradients (dp_mode "replica") or the fp64
+oracle gradient of the whole global minibatch on one device (dp_mode "sync",
+graph-LayerNorm statistics exchanged), and the parameters stay bit-identical
+across ranks after several Adam steps.
 """
 import os
 import socket
@@ -43,10 +45,10 @@ def _oracle_grads(P0, samples, idx):
     total, _, _ = O.batch_loss(pred, gt, b.ptr, [d.op_div_matrix.double() for d in datas], b.nodes_types,
                                True, 10.0)
     total.backward()
-    return torch.cat([P[n].grad.reshape(-1) for n in PARAM_NAMES])
+    return torch.cat([P[n].grad.reshape(-1) for n in PARAM_NAMES]), float(total.detach())
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, mode):
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
@@ -69,10 +71,12 @@ def _worker(rank, world, port, q):
                                     input_nodes_features_size=6, output_nodes_features_size=3,
                                     **{k: torch.tensor(v) for k, v in STATS.items()}).to(dev)
         P0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
-        tr = Trainer(model, lr=1e-3, divergence=True, divergence_penalty=10.0, process_group=dist.group.WORLD)
-        tr.step(batch)
+        tr = Trainer(model, lr=1e-3, divergence=True, divergence_penalty=10.0, process_group=dist.group.WORLD,
+                     dp_mode=mode)
+        out = tr.step(batch)
         torch.cuda.synchronize()
         g = tr.flat_g.detach().double().cpu()
+        loss = float(out["total"])
         for _ in range(3):
             tr.step(batch)
         torch.cuda.synchronize()
@@ -80,23 +84,31 @@ def _worker(rank, world, port, q):
         ps = [torch.empty_like(p) for _ in range(world)]
         dist.all_gather(ps, p)
         if rank == 0:
-            ref = sum(_oracle_grads(P0, samples, s) for s in shards) / world
-            q.put((float((g - ref).norm() / ref.norm()), max(float((x - ps[0]).abs().max()) for x in ps)))
+            if mode == "sync":
+                ref, ref_loss = _oracle_grads(P0, samples, sorted(i for s in shards for i in s))
+            else:
+                rs = [_oracle_grads(P0, samples, s) for s in shards]
+                ref = sum(r[0] for r in rs) / world
+                ref_loss = rs[0][1]                    # replica: rank 0 reports its own shard's loss
+            q.put((float((g - ref).norm() / ref.norm()), max(float((x - ps[0]).abs().max()) for x in ps),
+                   abs(loss - ref_loss) / abs(ref_loss)))
         dist.barrier()
     finally:
         dist.destroy_process_group()
 
 
-def test_trainer_dp_world2_on_one_gpu():
+@pytest.mark.parametrize("mode", ["replica", "sync"])
+def test_trainer_dp_world2_on_one_gpu(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
-    gerr, pdiff = q.get(timeout=400)
+    gerr, pdiff, lerr = q.get(timeout=400)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     assert gerr < 1e-4, gerr
+    assert lerr < 1e-5, lerr
     assert pdiff == 0.0, pdiff
