@@ -31,6 +31,22 @@ __device__ __forceinline__ void ln_relu_bwd(float (&gy)[FRAG], const float (&a2)
   }
 }
 
+// ln_relu_bwd with the LayerNorm weight as a FeatVec (no vector-memory access).
+__device__ __forceinline__ void ln_relu_bwd_fv(float (&gy)[FRAG], const float (&a2)[FRAG], const LNStat& st,
+                                               const pdg_ln_bwd& lb, const FeatVec& g) {
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const f32x4 gg = featvec_chunk(g, t);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int s = 4 * t + j;
+      const float xhat = div_den(a2[s] - st.mean, st.den, st.rstd);
+      const float ga = st.rstd * (gg[j] * gy[s] - lb.c1) - xhat * lb.c2;
+      gy[s] = a2[s] > 0.f ? ga : 0.f;
+    }
+  }
+}
+
 __device__ __forceinline__ void relu_mask_acc(float (&v)[FRAG], const Acc& acc, const float (&a)[FRAG]) {
   PDG_FOR_FRAG(s) v[s] = a[s] > 0.f ? ACC(acc, s) : 0.f;
 }
@@ -411,8 +427,21 @@ extern "C" int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const
 }
 
 // ============================================================================ fused edge backward
+// Memory-order discipline as in edge_fwd_kernel (pdg_fwd.hip): vmcnt counts loads and
+// stores together in issue order, so each row a later step needs is loaded before
+// the stores that precede that step (a1m before gz2m is stored, ge_next / a2e before
+// gz1m, a1e before gz2e, ge_next as the ge_out accumulator before gz1e), and the
+// next tile's gathered gaggr row and a2m row before this tile's last store.
+#ifndef PDG_EDGE_BWD_WAVES
+#define PDG_EDGE_BWD_WAVES PDG_EDGE_WAVES
+#endif
+constexpr int EB_WAVES = PDG_EDGE_BWD_WAVES;
+#ifndef PDG_EB_EARLY_A1E
+#define PDG_EB_EARLY_A1E 0
+#endif
+
 template <bool EU>
-__global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_bwd_kernel(
+__global__ __launch_bounds__(64 * EB_WAVES, EB_WAVES / 4) void edge_bwd_kernel(
     int E, const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
     const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
     const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ stm_p, const pdg_ln_stat* __restrict__ ste_p,
@@ -433,52 +462,84 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_bwd_kern
 #define PDG_GEMM_2(acc, v) PDG_GEMM_W2(acc, lds, v)
 #define PDG_GEMM_C(acc, v) gemm128(acc, lds + WBLK, v)
 #endif
+  const FeatVec fg = load_featvec(lg);
   __syncthreads();
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
   const LNStat ste = *reinterpret_cast<const LNStat*>(EU ? ste_p : stm_p);
   const pdg_ln_bwd lbm = *lbm_p, lbe = *(EU ? lbe_p : lbm_p);
   const int l = lane_id();
-  PDG_TILE_LOOP(E) {
+  const int lc = lane_col();
+  const int nw = blockDim.x >> 6, ntiles = tiles_of(E), stride = gridDim.x * nw;
+  int tile = xcd_block() * nw + wave_id();
+  // rows are clamped, so the prefetches below are unconditional (never live across the loop)
+  auto rowc = [&](int t) {
+    const int r = t * TILE + (l & 15);
+    return r < E ? r : E - 1;
+  };
+  float gm[FRAG], a[FRAG];   // this tile's gaggr[dst] and a2m rows
+  {
+    const int rc = rowc(tile);
+    load_frag(gm, gaggr + (size_t)dst[rc] * L);
+    load_frag(a, a2m + (size_t)rc * L);
+  }
+  int d_next = dst[rowc(tile + stride)];
+  for (; tile < ntiles; tile += stride) {
     const int row = tile * TILE + (l & 15);
     const bool valid = row < E;
     const int rc = valid ? row : E - 1;
-    const int d_node = dst[rc];
-    float v[FRAG], a[FRAG];
-    Acc acc;
+    float A[FRAG];
+    Acc Z;
     // ---- message path: gy = gaggr[dst]   (scatter_add_ backward = gather)
-    load_frag(v, gaggr + (size_t)d_node * L);
-    load_frag(a, a2m + (size_t)rc * L);
-    ln_relu_bwd(v, a, stm, lbm, lg);
-    if (valid) store_frag(gz2m + (size_t)row * L, v);
-    zero_acc(acc);
-    PDG_GEMM_2(acc, v);
-    load_frag(a, a1m + (size_t)rc * L);
-    relu_mask_acc(v, acc, a);
-    if (valid) store_frag(gz1m + (size_t)row * L, v);
+    ln_relu_bwd_fv(gm, a, stm, lbm, fg);                   // gm := gz2m
+    load_frag(A, a1m + (size_t)rc * L);
+    if (valid) store_frag(gz2m + (size_t)row * L, gm);
+    zero_acc(Z);
+    PDG_GEMM_2(Z, gm);
+    float v[FRAG];
+    relu_mask_acc(v, Z, A);                                // v := gz1m
     if (EU) {
-      float m[FRAG];
-      PDG_FOR_FRAG(s) m[s] = v[s];   // keep gz1m for gC
       // ---- edge-update path: gy = ge_next
-      load_frag(v, ge_next + (size_t)rc * L);
-      load_frag(a, a2e + (size_t)rc * L);
-      ln_relu_bwd(v, a, ste, lbe, lg);
-      if (valid) store_frag(gz2e + (size_t)row * L, v);
-      zero_acc(acc);
-      PDG_GEMM_2(acc, v);
-      load_frag(a, a1e + (size_t)rc * L);
-      relu_mask_acc(v, acc, a);
-      if (valid) store_frag(gz1e + (size_t)row * L, v);
-      PDG_FOR_FRAG(s) v[s] = m[s] + v[s];   // gC = gz1m + gz1e
+      float G[FRAG];
+      load_frag(G, ge_next + (size_t)rc * L);
+      load_frag(A, a2e + (size_t)rc * L);
+      if (valid) store_frag(gz1m + (size_t)row * L, v);
+      ln_relu_bwd_fv(G, A, ste, lbe, fg);                  // G := gz2e
+#if PDG_EB_EARLY_A1E
+      load_frag(A, a1e + (size_t)rc * L);
+      if (valid) store_frag(gz2e + (size_t)row * L, G);
+      zero_acc(Z);
+      PDG_GEMM_2(Z, G);
+#else
+      zero_acc(Z);
+      PDG_GEMM_2(Z, G);
+      load_frag(A, a1e + (size_t)rc * L);
+      if (valid) store_frag(gz2e + (size_t)row * L, G);
+#endif
+      relu_mask_acc(G, Z, A);                              // G := gz1e
+      // ge_out = ge_next + Wc^T gC: the accumulator starts as ge_next
+      {
+        const float* gp = ge_next + (size_t)rc * L + lc;
+#pragma unroll
+        for (int T = 0; T < 8; ++T) Z.b[T] = ld4(gp, T);
+      }
+      if (valid) store_frag(gz1e + (size_t)row * L, G);
+      PDG_FOR_FRAG(s) v[s] = v[s] + G[s];                  // gC = gz1m + gz1e
+    } else {
+      if (valid) store_frag(gz1m + (size_t)row * L, v);
+      zero_acc(Z);
     }
-    // ---- ge_out = ge_next + Wc^T gC
+    // ---- ge_out = [ge_next +] Wc^T gC
     if (valid) store_frag(gC + (size_t)row * L, v);
-    zero_acc(acc);
-    PDG_GEMM_C(acc, v);
-    if (EU) {
-      load_frag(a, ge_next + (size_t)rc * L);
-      PDG_FOR_FRAG(s) ACC(acc, s) += a[s];
+    PDG_GEMM_C(Z, v);
+    // next tile's rows before this tile's last store
+    {
+      const int rcn = rowc(tile + stride);
+      load_frag(gm, gaggr + (size_t)d_next * L);
+      load_frag(a, a2m + (size_t)rcn * L);
+      d_next = dst[rowc(tile + 2 * stride)];
     }
-    if (valid) store_acc(ge_out + (size_t)row * L, acc);
+    PDG_FENCE();
+    if (valid) store_acc(ge_out + (size_t)row * L, Z);
   }
 #undef PDG_GEMM_2
 #undef PDG_GEMM_C
@@ -498,14 +559,14 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
                              PDG_ALIGNED(gz1e) && st_e && lb_e),
                 "pdg_edge_bwd: edge-update arguments missing or misaligned");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd: ge_out must not alias ge_next");
-  const int grid = persistent_grid(n_edges, EDGE_WAVES, 1);
+  const int grid = persistent_grid(n_edges, EB_WAVES, 1);
   const size_t shm = PDG_EDGE_X6 ? (size_t)EDGE_LDS_BYTES : 2 * WBLK * sizeof(float);
   if (ge_next)
-    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(64 * EDGE_WAVES), shm, (hipStream_t)stream,
+    hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(64 * EB_WAVES), shm, (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
                        gz1m, gz2e, gz1e, gC, ge_out);
   else
-    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(64 * EDGE_WAVES), shm, (hipStream_t)stream,
+    hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(64 * EB_WAVES), shm, (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, WcT, gz2m,
                        gz1m, gz2e, gz1e, gC, ge_out);
   PDG_CHECK_LAUNCH("pdg_edge_bwd");

@@ -126,6 +126,33 @@ __device__ __forceinline__ void zero_acc(Acc& acc) {
   for (int ob = 0; ob < 8; ++ob) acc.b[ob] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
+// A loop-invariant per-feature vector (bias, LayerNorm weight / bias) kept in two
+// VGPRs: lane l holds p[l] and p[64 + l].  Chunk T of the fragment layout (features
+// 16T + 4q + j of lane quarter q) is fetched with ds_bpermute through the LDS
+// crossbar: no LDS allocation and no vector-memory counter, so reading it never
+// waits for this wave's outstanding global stores (vmcnt counts loads and stores
+// together on CDNA, in issue order).
+struct FeatVec {
+  float lo, hi;
+};
+__device__ __forceinline__ FeatVec load_featvec(const float* __restrict__ p) {
+  const int l = lane_id();
+  return FeatVec{p[l], p[64 + l]};
+}
+__device__ __forceinline__ f32x4 featvec_chunk(const FeatVec& fv, int T) {
+  const int addr = opaque(4 * (16 * (T & 3) + 4 * (lane_id() >> 4)));   // kept inside the tile loop
+  const int src = __float_as_int(T < 4 ? fv.lo : fv.hi);
+  f32x4 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = __int_as_float(__builtin_amdgcn_ds_bpermute(addr + 4 * j, src));
+  return r;
+}
+// acc = per-feature bias (the accumulator is then the bias plus the GEMM).
+__device__ __forceinline__ void bias_acc(Acc& acc, const FeatVec& b) {
+#pragma unroll
+  for (int ob = 0; ob < 8; ++ob) acc.b[ob] = featvec_chunk(b, ob);
+}
+
 // acc += W * v over K = 128: 8 input groups t x 4 output-block pairs x 8 MFMAs
 // (256 MFMAs).  The A fragments of the next (t, pair) are read from LDS while
 // the current pair's 8 MFMAs issue; the two accumulators of a pair alternate so

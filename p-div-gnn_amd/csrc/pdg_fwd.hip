@@ -320,18 +320,31 @@ extern "C" int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat*
 // ============================================================================ fused edge pass
 // First layer of both edge_net evaluations from the shared C = W_c e + b1, in
 // four chunks of 8 features (each accumulator block pair dies as its chunk is
-// consumed); the gathered P/Q rows of chunk q+1 are in flight while chunk q is
-// computed:
-//   edge update: relu(C + P[src] + Q[dst]) -> ve (kept for layer 2, stored to a1e)
-//   message:     relu(C + P[dst] + Q[src]) -> v  (stored to a1m by the caller)
-// Registers (<= 168 for 3 waves/SIMD) allow one of: the next chunk's gathers in
-// flight, or the edge-update layer-1 output kept for layer 2 instead of re-read;
-// measured, keeping it is faster (edge_fwd -5 %, prefetching -1.5 %).
+// consumed):
+//   edge update: relu(C + P[src] + Q[dst]) -> ve (kept for layer 2)
+//   message:     relu(C + P[dst] + Q[src]) -> v
+// Chunk 0's gathers are issued before the W_c GEMM so their latency hides behind
+// it; with PDG_EF_PREFETCH chunk q+1's are in flight while chunk q is computed.
+//
+// Memory-order discipline of the tile loop: vmcnt counts loads and stores together
+// and in issue order, so a load issued after a store cannot be waited for without
+// also waiting for the store.  Every per-tile load is therefore issued before the
+// stores it would otherwise queue behind: the next tile's rows and indices before
+// this tile's last store, the gathers before a1m / a1e are stored, and the
+// loop-invariant vectors (b1, b2, LayerNorm weight and bias) never touch vector
+// memory inside the loop (FeatVec, ds_bpermute).
 #ifndef PDG_EF_PREFETCH
-#define PDG_EF_PREFETCH 0
+#define PDG_EF_PREFETCH 1
 #endif
-#ifndef PDG_EF_KEEP_A1E
-#define PDG_EF_KEEP_A1E 1
+#ifndef PDG_EDGE_FWD_WAVES
+#define PDG_EDGE_FWD_WAVES 8   // 2 waves per SIMD, 256 VGPRs: room for the prefetches (measured)
+#endif
+constexpr int EF_WAVES = PDG_EDGE_FWD_WAVES;
+#ifndef PDG_EF_EARLY
+#define PDG_EF_EARLY 1
+#endif
+#ifndef PDG_EF_NEXT
+#define PDG_EF_NEXT 1
 #endif
 struct Gather8 {
   f32x4 xs[2], yd[2], xd[2], ys[2];
@@ -352,46 +365,68 @@ __device__ __forceinline__ void gather_chunk(Gather8& g, int q, const float* __r
   }
 }
 
+// ps/qd/pd/qs already offset by lane_col(); g0 holds chunk 0, already issued.
 template <bool EU>
-__device__ __forceinline__ void first_layers(float (&v)[FRAG], float (&ve)[FRAG], const Acc& C,
+__device__ __forceinline__ void first_layers(float (&v)[FRAG], float (&ve)[FRAG], const Acc& C, Gather8 g0,
                                              const float* __restrict__ ps, const float* __restrict__ qd,
-                                             const float* __restrict__ pd, const float* __restrict__ qs,
-                                             float* __restrict__ a1e_row, bool valid) {
-  const int lc = lane_col();
-  ps += lc; qd += lc; pd += lc; qs += lc;
-#if PDG_EF_PREFETCH
-  Gather8 g[2];
-  gather_chunk<EU>(g[0], 0, ps, qd, pd, qs);
-#else
-  Gather8 g[1];
+                                             const float* __restrict__ pd, const float* __restrict__ qs) {
+  Gather8 cur = g0;
+#if !PDG_EF_EARLY
+  gather_chunk<EU>(cur, 0, ps, qd, pd, qs);
 #endif
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
 #if PDG_EF_PREFETCH
-    if (q < 3) gather_chunk<EU>(g[(q + 1) & 1], q + 1, ps, qd, pd, qs);
-    const Gather8& c8 = g[q & 1];
+    Gather8 nxt;
+    if (q < 3) gather_chunk<EU>(nxt, q + 1, ps, qd, pd, qs);
 #else
-    gather_chunk<EU>(g[0], q, ps, qd, pd, qs);
-    const Gather8& c8 = g[0];
+    if (q > 0) gather_chunk<EU>(cur, q, ps, qd, pd, qs);
 #endif
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      f32x4 e;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float c = C.b[2 * q + t][j];
-        if (EU) e[j] = fmaxf((c + c8.xs[t][j]) + c8.yd[t][j], 0.f);
-        v[8 * q + 4 * t + j] = fmaxf((c + c8.xd[t][j]) + c8.ys[t][j], 0.f);
-        if (EU && PDG_EF_KEEP_A1E) ve[8 * q + 4 * t + j] = e[j];
+        if (EU) ve[8 * q + 4 * t + j] = fmaxf((c + cur.xs[t][j]) + cur.yd[t][j], 0.f);
+        v[8 * q + 4 * t + j] = fmaxf((c + cur.xd[t][j]) + cur.ys[t][j], 0.f);
       }
-      if (EU && valid && a1e_row) st4(a1e_row + lc, 2 * q + t, e);
     }
+#if PDG_EF_PREFETCH
+    if (q < 3) cur = nxt;
+#endif
     PDG_FENCE();
   }
 }
 
+// v = LN(x) [+ r] from rows already in registers (models.py:225 residual).
+template <bool RES>
+__device__ __forceinline__ void ln_apply(float (&v)[FRAG], const float (&x)[FRAG], const float (&r)[FRAG],
+                                         const LNStat& st, const FeatVec& g, const FeatVec& b) {
+#pragma unroll
+  for (int T = 0; T < 8; ++T) {
+    const f32x4 gg = featvec_chunk(g, T), bb = featvec_chunk(b, T);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float y = div_den(x[4 * T + j] - st.mean, st.den, st.rstd) * gg[j] + bb[j];
+      if (RES) y += r[4 * T + j];
+      v[4 * T + j] = y;
+    }
+  }
+}
+
+// v = relu(acc + bias); the bias is added after the GEMM so that the accumulator
+// starts as the MFMA's inline zero and occupies no registers before the GEMM.
+__device__ __forceinline__ void bias_relu_fv(float (&v)[FRAG], const Acc& acc, const FeatVec& b) {
+#pragma unroll
+  for (int T = 0; T < 8; ++T) {
+    const f32x4 bb = featvec_chunk(b, T);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[4 * T + j] = fmaxf(acc.b[T][j] + bb[j], 0.f);
+  }
+}
+
 template <bool RES, bool EU>
-__global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kernel(
+__global__ __launch_bounds__(64 * EF_WAVES, EF_WAVES / 4) void edge_fwd_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
     const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ P,
@@ -412,51 +447,74 @@ __global__ __launch_bounds__(64 * EDGE_WAVES, EDGE_WAVES / 4) void edge_fwd_kern
 #define PDG_GEMM_C(acc, v) gemm128(acc, lds, v)
 #define PDG_GEMM_2(acc, v) PDG_GEMM_W2(acc, lds + WBLK, v)
 #endif
+  const FeatVec fg = load_featvec(lg), fb = load_featvec(lb), fb1 = load_featvec(b1), fb2 = load_featvec(b2);
   __syncthreads();
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const int l = lane_id();
+  const int lc = lane_col();
   double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
-  PDG_TILE_LOOP(E) {
+  const int nw = blockDim.x >> 6, ntiles = tiles_of(E), stride = gridDim.x * nw;
+  int tile = xcd_block() * nw + wave_id();
+  // raw inputs of the current tile: LayerNorm input row, residual row, endpoints
+  float xa[FRAG], xr[FRAG];
+  int s_node = 0, d_node = 0;
+  auto issue = [&](int t) {
+    const int r = t * TILE + (l & 15);
+    const int rc = r < E ? r : E - 1;
+    s_node = src[rc];
+    d_node = dst[rc];
+    load_frag(xa, a2p + (size_t)rc * L);
+    if (RES) load_frag(xr, eres + (size_t)rc * L);
+  };
+  issue(tile);   // unconditional (rows clamped), so the buffers are not live across the whole loop
+  for (; tile < ntiles; tile += stride) {
     const int row = tile * TILE + (l & 15);
     const bool valid = row < E;
-    const int rc = valid ? row : E - 1;
-    const int s_node = src[rc], d_node = dst[rc];
+    const float* ps = P + (size_t)s_node * L + lc;
+    const float* qd = Q + (size_t)d_node * L + lc;
+    const float* pd = P + (size_t)d_node * L + lc;
+    const float* qs = Q + (size_t)s_node * L + lc;
+    Gather8 g0;
+#if PDG_EF_EARLY
+    gather_chunk<EU>(g0, 0, ps, qd, pd, qs);
+#endif
     float v[FRAG];
     // e_t = LN(a2_prev) + e_res   (models.py:225 residual of the previous step)
-    ln_res_frag<RES>(v, a2p + (size_t)rc * L, RES ? eres + (size_t)rc * L : nullptr, st, lg, lb);
-    if (valid) store_frag(eout + (size_t)row * L, v);
+    ln_apply<RES>(v, xa, xr, st, fg, fb);
     // C = W_c e_t + b1 (shared by both edge_net evaluations)
     Acc C;
     zero_acc(C);
+    if (valid) store_frag(eout + (size_t)row * L, v);
     PDG_GEMM_C(C, v);
-    {
-      const float* bp = b1 + lane_col();
 #pragma unroll
-      for (int t = 0; t < 8; ++t) C.b[t] += ld4(bp, t);
-    }
+    for (int T = 0; T < 8; ++T) C.b[T] += featvec_chunk(fb1, T);
     // layer 1 of the edge update (models.py:219-222, x[row] = x[src], x[col] = x[dst]) and of
     // the message (models.py:233-238, x_i = x[dst], x_j = x[src])
     float ve[FRAG];
-    first_layers<EU>(v, ve, C, P + (size_t)s_node * L, Q + (size_t)d_node * L, P + (size_t)d_node * L,
-                     Q + (size_t)s_node * L, (EU && a1e) ? a1e + (size_t)row * L : nullptr, valid);
-    if (valid && a1m) store_frag(a1m + (size_t)row * L, v);   // a1m / a1e: kept for the backward only
+    first_layers<EU>(v, ve, C, g0, ps, qd, pd, qs);
     Acc Z;
     zero_acc(Z);
+    if (valid && a1m) store_frag(a1m + (size_t)row * L, v);   // a1m / a1e: kept for the backward only
+    if (EU && valid && a1e) store_frag(a1e + (size_t)row * L, ve);
     PDG_GEMM_2(Z, v);
-    bias_relu(v, Z, b2);
-    if (valid) store_frag(a2m + (size_t)row * L, v);
+    bias_relu_fv(v, Z, fb2);
     accum_stats(v, valid, sm1, sm2);
     if (EU) {
       // edge-update layer 2
-#if !PDG_EF_KEEP_A1E
-      load_frag(ve, a1e + (size_t)(valid ? row : rc) * L);
-#endif
       zero_acc(Z);
+      if (valid) store_frag(a2m + (size_t)row * L, v);
       PDG_GEMM_2(Z, ve);
-      bias_relu(v, Z, b2);
-      if (valid) store_frag(a2e + (size_t)row * L, v);
+      bias_relu_fv(v, Z, fb2);
       accum_stats(v, valid, se1, se2);
     }
+#if PDG_EF_NEXT
+    issue(tile + stride);   // before this tile's last store
+    PDG_FENCE();
+    if (valid) store_frag((EU ? a2e : a2m) + (size_t)row * L, v);
+#else
+    if (valid) store_frag((EU ? a2e : a2m) + (size_t)row * L, v);
+    if (tile + stride < ntiles) issue(tile + stride);
+#endif
   }
 #undef PDG_GEMM_C
 #undef PDG_GEMM_2
@@ -487,11 +545,11 @@ extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat
                 "pdg_edge_fwd: misaligned pointer");
   PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd: edge-update outputs missing or misaligned");
-  const int grid = persistent_grid(n_edges, EDGE_WAVES, 1);
+  const int grid = persistent_grid(n_edges, EF_WAVES, 1);
   const size_t shm = PDG_EDGE_X6 ? (size_t)EDGE_LDS_BYTES : 2 * WBLK * sizeof(float);
   hipStream_t s = (hipStream_t)stream;
 #define PDG_EDGE_FWD(R, U)                                                                                     \
-  hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(64 * EDGE_WAVES), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \
+  hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(64 * EF_WAVES), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \
                      e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e)
   if (e_res) {
     if (with_edge_update) PDG_EDGE_FWD(true, true); else PDG_EDGE_FWD(true, false);
