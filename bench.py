@@ -38,7 +38,8 @@ import torch.distributed as dist  # noqa: E402
 PMC_FILE = ROOT / "profiles" / "r01_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
 PMC_NAMES = {"edge_fwd": "void edge_fwd_kernel<true, true>", "edge_bwd": "void edge_bwd_kernel<true>",
              "segment_sum": "segment_sum_kernel", "node_net": "node_net_kernel", "pq_scatter_bwd": "pq_scatter_bwd_kernel",
-             "wgrad_W2": "wgrad_x6_kernel"}
+             "wgrad_W2": "wgrad_x6_kernel", "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
+             "edge_gout": "void edge_gout_wc_kernel<true>"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
 PEAK_HBM = 8.0e12           # MI355X HBM3E spec bandwidth (same guide; 6.3 TB/s measured copy)
 L = 128
@@ -173,8 +174,9 @@ def main():
     eng = trainer.engine
     # HIP events bracket the timed kernels' launches in the last `ev_steps` steps of the timed
     # region (each event pair costs a few us of queue time; sampling keeps the region clean)
-    timed_kernels = ["edge_fwd", "edge_bwd", "wgrad_W2", "segment_sum", "node_net", "node_bwd", "node_pq",
-                     "gemm_sum2", "pq_scatter_bwd"]
+    timed_kernels = ["edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2", "segment_sum", "node_net", "node_bwd",
+                     "node_pq", "gemm_sum2", "pq_scatter_bwd"]
+    fused = eng.fused_edge_wgrad
     ev_steps = min(args.steps, 3)
     if pg is not None:
         dist.barrier()
@@ -200,15 +202,21 @@ def main():
     kt = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) * 1e-3 for k, v in ev.items()}
     ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
     S = cfg["steps"]
+    nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
     # algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops and the bytes the
     # kernel must read/write (inputs once, outputs once, int32 indices)
     work = {
         # 3 (128x128) GEMMs per edge; reads a2e_prev, e_prev, 4 gathered P/Q rows, src, dst;
         # writes e_t, a1m, a2m, a1e, a2e
         "edge_fwd": (E * 3 * 2 * L * L, E * (11 * 4 * L + 8)),
-        # 3 GEMMs per edge; reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst;
-        # writes gz2m, gz1m, gz2e, gz1e, gC, ge_out
-        "edge_bwd": (E * 3 * 2 * L * L, E * (12 * 4 * L + 4)),
+        # fused (pdg_edge_bwd_w2): 2 GEMMs + 2 weight-gradient products per edge; reads gaggr[dst],
+        # ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gz1e, gC; one slab read+write per block.
+        # unfused (pdg_edge_bwd): 3 GEMMs; writes gz2m, gz1m, gz2e, gz1e, gC, ge_out
+        "edge_bwd": ((E * 4 * 2 * L * L, E * (9 * 4 * L + 4) + 2 * nslab_bytes) if fused
+                     else (E * 3 * 2 * L * L, E * (12 * 4 * L + 4))),
+        # fused Wc path (pdg_edge_gout_wc): GEMM + weight-gradient product; reads gC, e, ge_next,
+        # writes ge_out; one slab read+write per block
+        "edge_gout": (E * 2 * 2 * L * L, E * 4 * 4 * L + 2 * nslab_bytes),
         # all steps' W2 segments: 2E rows per step of (G, X) 512-byte rows, one 64 KB slab per block
         "wgrad_W2": (S * 2 * E * 2 * L * L, S * 2 * E * 2 * 4 * L + 512 * (L * L + L) * 4),
         # dst-segment sum of LN(a2m): reads a2m (E rows) and rowptr, writes aggr (+ x-hat sums)
@@ -222,6 +230,8 @@ def main():
     if PMC_FILE.exists() and args.config == 2:
         data = json.loads(PMC_FILE.read_text())
         for k, prefix in PMC_NAMES.items():
+            if fused and k == "edge_bwd":
+                prefix = PMC_NAMES["edge_bwd_w2"]
             hit = [v for name, v in data.items() if name.startswith(prefix)]
             if hit:
                 pmc[k] = round(hit[0]["total"])
@@ -245,7 +255,7 @@ def main():
                 "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4), "frac_hbm": round(f_hbm, 4),
                 "avg_launch_ms": round(t * 1e3, 4), "share_of_step": round(ktot[k] / el, 4)}
 
-    dominant = max([k for k in ("edge_fwd", "edge_bwd", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])
+    dominant = max([k for k in ("edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])
     if rank == 0:
         res = {
             "metric": ("mesh-nodes/sec (inference) on periodic FEM graphs" if infer

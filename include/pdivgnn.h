@@ -202,6 +202,23 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
                  float* gz2m, float* gz1m, float* gz2e, float* gz1e, float* gC, float* ge_out,
                  void* stream);
 
+/* Edge backward with the shared-weight gradients fused (pdg_ebw.hip), replacing
+ * pdg_edge_bwd + the W2 / Wc passes of pdg_wgrad_segments (gnn_local_stress/models.py:194-208,
+ * backward).  Weights stationary in registers, 32-row operand images in LDS; one block per
+ * slab, `nslabs` blocks (the same value for every call of a backward pass: the block ->
+ * slab map is fixed and the slabs accumulate, reduced once by pdg_wgrad_reduce).
+ *   pdg_edge_bwd_w2:  gz1m/gz1e/gC as pdg_edge_bwd; slabs (zeroed before the first call)
+ *                     += gz2m^T a1m + gz2e^T a1e and the b2 column sums; gz2m/gz2e are not
+ *                     materialised.  ge_next == NULL: message branch only, gC = gz1m.
+ *   pdg_edge_gout_wc: ge_out = [ge_next +] WcT gC; slabs += gC^T e and the b1 column sums. */
+int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
+                    const float* a2m, const float* a1m, const float* a2e, const float* a1e,
+                    const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
+                    const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
+                    float* gz1e, float* gC, float* slabs, int nslabs, void* stream);
+int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next,
+                     const float* WcT, float* ge_out, float* slabs, int nslabs, void* stream);
+
 /* Backward of the P/Q gathers: gP[v] = sum_{dst-seg(v)} gz1m + sum_{src-seg(v)} gz1e,
  * gQ[v] = sum_{src-seg(v)} gz1m + sum_{dst-seg(v)} gz1e.  src-seg uses rowptr_src and
  * perm_src (positions of the dst-sorted edges grouped by src).  gz1e may be NULL (no

@@ -1,0 +1,436 @@
+// Edge backward with the shared-weight gradients fused in (models.py:194-208 edge_net,
+// backward of one message-passing step; SURVEY §8 rows a5/a6 and the weight gradients).
+//
+// The plain edge backward (pdg_edge_bwd, pdg_bwd.hip) keeps W2^T and Wc^T in LDS, so
+// the weight gradients dW2 = sum gz2^T a1 and dWc = sum gC^T e need a second pass
+// (pdg_wgrad_segments) that re-reads gz2 / a1 / gC / e from HBM.  Here the weights
+// are STATIONARY IN REGISTERS (wave w of 8 owns output features [16w, 16w + 16) of
+// the product, 48 VGPRs of bf16 terms) and LDS holds the 32-row images of the
+// operands instead: the same images feed the activation GEMM (straight 16-B reads)
+// and the weight-gradient MFMAs (transposed reads), so the gradients cost no HBM
+// traffic and gz2m / gz2e are never written.  Two kernels, one per weight:
+//
+//   pdg_edge_bwd_w2:  gz2 = LN_bwd(gy) [a2 > 0] for the message (gy = gaggr[dst]) and the
+//                     edge update (gy = ge_next); gz1 = (W2^T gz2) [a1 > 0]; gC = gz1m + gz1e;
+//                     slab += gz2m^T a1m + gz2e^T a1e (and the b2 sums).
+//   pdg_edge_gout_wc: ge_out = ge_next + Wc^T gC; slab += gC^T e (and the b1 sums).
+//
+// All products are bf16x6 (fp32-accurate).  Rows are split into one contiguous range per
+// block (one block of 8 waves per CU); a block's 128x128 (+128) fp32 slab is
+// read-modified-written once at the end, so slabs accumulate over the steps of a
+// backward pass and are reduced once by pdg_wgrad_reduce (deterministic).
+//
+// Per 32-row round: stage (loads -> LN backward / split -> images) | barrier | next
+// round's loads issued | weight-gradient MFMAs | activation MFMAs | stores | barrier.
+// Every load of a round is issued before the previous round's stores (vmcnt counts
+// loads and stores together, in issue order).
+#include "pdg_common.hpp"
+#include "pdg_runtime.hpp"
+#include "pdg_x6.hpp"
+
+using namespace pdg;
+
+namespace {
+
+constexpr int EBW_WAVES = 8;
+constexpr int EBW_THREADS = 64 * EBW_WAVES;
+constexpr int EBW_IMG = 3 * X6_TERM;        // one bf16x6 image of 32 rows (24 KB)
+constexpr int EBW_MASK = X6_ROWS * L;       // relu mask bytes of 32 rows
+constexpr int WSLAB = L * L + L;            // floats per slab (weight + bias sums)
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// A operand of rows 16w .. 16w+15 of a 128x128 matrix WT (o' x k, row-major), K chunk ks
+// (k = 32 ks + 8 (l >> 4) + 0..7), three bf16 terms.
+struct WSlice {
+  bf16x8 a[4][3];
+};
+
+__device__ __forceinline__ void load_wslice(WSlice& ws, const float* __restrict__ WT, int w) {
+  const int l = lane_id();
+  const float* row = WT + (size_t)(16 * w + (l & 15)) * L + 8 * (l >> 4);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const f32x4 x0 = *reinterpret_cast<const f32x4*>(row + 32 * ks);
+    const f32x4 x1 = *reinterpret_cast<const f32x4*>(row + 32 * ks + 4);
+    unsigned h[4], m[4], lo[4];
+    split3_pair(x0[0], x0[1], h[0], m[0], lo[0]);
+    split3_pair(x0[2], x0[3], h[1], m[1], lo[1]);
+    split3_pair(x1[0], x1[1], h[2], m[2], lo[2]);
+    split3_pair(x1[2], x1[3], h[3], m[3], lo[3]);
+    ws.a[ks][0] = __builtin_bit_cast(bf16x8, (u32x4){h[0], h[1], h[2], h[3]});
+    ws.a[ks][1] = __builtin_bit_cast(bf16x8, (u32x4){m[0], m[1], m[2], m[3]});
+    ws.a[ks][2] = __builtin_bit_cast(bf16x8, (u32x4){lo[0], lo[1], lo[2], lo[3]});
+  }
+}
+
+// Columns 4cg .. 4cg+3 of image row r, split into the three terms.
+__device__ __forceinline__ void img_store4(unsigned char* img, int r, int cg, const f32x4& v) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split3_pair(v[0], v[1], h0, m0, l0);
+  split3_pair(v[2], v[3], h1, m1, l1);
+  const int off = x6_addr(r, 8 * cg);
+  *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
+  *reinterpret_cast<u32x2*>(img + X6_TERM + off) = u32x2{m0, m1};
+  *reinterpret_cast<u32x2*>(img + 2 * X6_TERM + off) = u32x2{l0, l1};
+}
+
+__device__ __forceinline__ unsigned relu_mask4(const f32x4& a) {
+  return (a[0] > 0.f ? 0x1u : 0u) | (a[1] > 0.f ? 0x100u : 0u) | (a[2] > 0.f ? 0x10000u : 0u) |
+         (a[3] > 0.f ? 0x1000000u : 0u);
+}
+
+// gz2 = LN_bwd(gy) * [a2 > 0] for 4 features (ln_relu_bwd, pdg_bwd.hip, element by element).
+__device__ __forceinline__ f32x4 ln_relu_bwd4(const f32x4& gy, const f32x4& a2, const LNStat& st,
+                                              const pdg_ln_bwd& lb, const f32x4& g) {
+  f32x4 z;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float xhat = div_den(a2[e] - st.mean, st.den, st.rstd);
+    const float ga = st.rstd * (g[e] * gy[e] - lb.c1) - xhat * lb.c2;
+    z[e] = a2[e] > 0.f ? ga : 0.f;
+  }
+  return z;
+}
+
+// slab += G^T X over the 32 staged rows (K = rows): wave w owns o in 32 (w & 3) + [0, 32),
+// i in 64 (w >> 2) + [0, 64) as two 32x32 accumulators (wgrad_x6_kernel's operand reads).
+__device__ __forceinline__ void wgrad_round(f32x16 (&acc)[2], const unsigned char* gimg, const unsigned char* ximg) {
+  const int l = lane_id(), w = wave_id(), h = l >> 5;
+  const int ob = 32 * (w & 3), ib = 64 * (w >> 2);
+  const int lrow = 8 * h + ((l & 15) >> 2);
+  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    const int row = 16 * ks + lrow;
+    bf16x8 A[3], B[2][3];
+    const int g0 = x6_addr(row, lcolb + 2 * ob), g1 = x6_addr(row + 4, lcolb + 2 * ob);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) A[p] = x6_operand(gimg + p * X6_TERM, g0, g1);
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int x0 = x6_addr(row, lcolb + 2 * (ib + 32 * b)), x1 = x6_addr(row + 4, lcolb + 2 * (ib + 32 * b));
+#pragma unroll
+      for (int p = 0; p < 3; ++p) B[b][p] = x6_operand(ximg + p * X6_TERM, x0, x1);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      f32x16 t = acc[b];
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[b][0], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[b][1], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[b][2], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[b][0], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[b][1], t, 0, 0, 0);
+      acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[b][0], t, 0, 0, 0);
+    }
+  }
+}
+
+// d[nb] = (W^T-slice x image rows 16 nb .. 16 nb + 15): D row = output feature 16w + 4(l >> 4) + j,
+// column = staged row 16 nb + (l & 15).  NI images share the weight operands.
+template <int NI>
+__device__ __forceinline__ void gemm_round(f32x4 (&d)[NI][2], const WSlice& ws, const unsigned char* const (&img)[NI]) {
+  const int l = lane_id(), n = l & 15, kg = l >> 4;
+#pragma unroll
+  for (int u = 0; u < NI; ++u)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) d[u][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+#pragma unroll
+    for (int u = 0; u < NI; ++u)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int off = x6_addr(16 * nb + n, 64 * ks + 16 * kg);
+        bf16x8 B[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(img[u] + p * X6_TERM + off);
+        f32x4 t = d[u][nb];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][2], B[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][1], B[1], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][0], B[2], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][1], B[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][0], B[1], t, 0, 0, 0);
+        d[u][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][0], B[0], t, 0, 0, 0);
+      }
+  }
+}
+
+// Block's row range: contiguous, a multiple of 32 rows except at the end.
+__device__ __forceinline__ void block_rows(int M, int& r0, int& r1) {
+  const int nb = gridDim.x;
+  int per = (M + nb - 1) / nb;
+  per = (per + X6_ROWS - 1) / X6_ROWS * X6_ROWS;
+  r0 = min(M, per * (int)blockIdx.x);
+  r1 = min(M, per * ((int)blockIdx.x + 1));
+}
+
+// slab += acc (the block's own slab, fixed block -> slab map) and the bias sums:
+// thread (cg, rg) holds column sums of columns 4cg .. 4cg+3 over its rows; reduced over
+// the 16 row groups in order through LDS (`red`, 8 KB, the images being dead).
+__device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const f32x16 (&acc)[2], const f32x4& bsum,
+                                                float* red) {
+  const int l = lane_id(), w = wave_id(), h = l >> 5, c = l & 31;
+  const int ob = 32 * (w & 3), ib = 64 * (w >> 2);
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h, i = ib + 32 * b + c;
+      slab[o * L + i] += acc[b][r];
+    }
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  *reinterpret_cast<f32x4*>(red + rg * L + 4 * cg) = bsum;
+  __syncthreads();
+  if (threadIdx.x < L) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s += red[g * L + threadIdx.x];
+    slab[L * L + threadIdx.x] += s;
+  }
+}
+
+__device__ __forceinline__ int clamp_row(int r, int r1) { return r < r1 ? r : r1 - 1; }
+
+}  // namespace
+
+// ============================================================================ W2 path
+template <bool EU>
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
+    const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
+    const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
+    const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ stm_p, const pdg_ln_stat* __restrict__ ste_p,
+    const pdg_ln_bwd* __restrict__ lbm_p, const pdg_ln_bwd* __restrict__ lbe_p, const float* __restrict__ lg,
+    const float* __restrict__ W2T, float* __restrict__ gz1m, float* __restrict__ gz1e, float* __restrict__ gC,
+    float* __restrict__ slabs, int E) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img_gm = sm;                                  // gz2m
+  unsigned char* img_am = sm + EBW_IMG;                        // a1m
+  unsigned char* img_ge = sm + 2 * EBW_IMG;                    // gz2e (EU)
+  unsigned char* img_ae = sm + 3 * EBW_IMG;                    // a1e (EU)
+  unsigned char* msk_m = sm + (EU ? 4 : 2) * EBW_IMG;          // [a1m > 0]
+  unsigned char* msk_e = msk_m + EBW_MASK;                     // [a1e > 0] (EU)
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  int r0, r1;
+  block_rows(E, r0, r1);
+  WSlice ws;
+  load_wslice(ws, W2T, w);
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+  const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
+  const LNStat ste = *reinterpret_cast<const LNStat*>(EU ? ste_p : stm_p);
+  const pdg_ln_bwd lbm = *lbm_p, lbe = *(EU ? lbe_p : lbm_p);
+  f32x16 acc[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
+  // prefetched rows of the next round: thread rows rg and rg + 16, columns 4cg .. 4cg+3
+  f32x4 pg[2], pa2[2], pa1[2], pge[2], pa2e[2], pa1e[2];
+  int dnext[2] = {0, 0};
+  auto issue = [&](int base, const int (&dn)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
+      pg[u] = *reinterpret_cast<const f32x4*>(gaggr + (size_t)dn[u] * L + 4 * cg);
+      pa2[u] = *reinterpret_cast<const f32x4*>(a2m + rc);
+      pa1[u] = *reinterpret_cast<const f32x4*>(a1m + rc);
+      if (EU) {
+        pge[u] = *reinterpret_cast<const f32x4*>(ge_next + rc);
+        pa2e[u] = *reinterpret_cast<const f32x4*>(a2e + rc);
+        pa1e[u] = *reinterpret_cast<const f32x4*>(a1e + rc);
+      }
+    }
+  };
+  if (r0 < r1) {
+    int d0[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      d0[u] = dst[clamp_row(r0 + rg + 16 * u, r1)];
+      dnext[u] = dst[clamp_row(r0 + X6_ROWS + rg + 16 * u, r1)];
+    }
+    issue(r0, d0);
+  }
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    // ---- stage: gz2 (LN + relu backward), a1 and its relu mask into the images
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const bool ok = base + r < r1;
+      const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 zm = ok ? ln_relu_bwd4(pg[u], pa2[u], stm, lbm, g4) : zero;
+      const f32x4 am = ok ? pa1[u] : zero;
+      bsum += zm;
+      img_store4(img_gm, r, cg, zm);
+      img_store4(img_am, r, cg, am);
+      *reinterpret_cast<unsigned*>(msk_m + r * L + 4 * cg) = relu_mask4(am);
+      if (EU) {
+        const f32x4 ze = ok ? ln_relu_bwd4(pge[u], pa2e[u], ste, lbe, g4) : zero;
+        const f32x4 ae = ok ? pa1e[u] : zero;
+        bsum += ze;
+        img_store4(img_ge, r, cg, ze);
+        img_store4(img_ae, r, cg, ae);
+        *reinterpret_cast<unsigned*>(msk_e + r * L + 4 * cg) = relu_mask4(ae);
+      }
+    }
+    __syncthreads();
+    // ---- next round's loads, ahead of this round's stores
+    if (base + X6_ROWS < r1) {
+      const int dcur[2] = {dnext[0], dnext[1]};
+#pragma unroll
+      for (int u = 0; u < 2; ++u) dnext[u] = dst[clamp_row(base + 2 * X6_ROWS + rg + 16 * u, r1)];
+      issue(base + X6_ROWS, dcur);
+    }
+    // ---- dW2 += gz2m^T a1m (+ gz2e^T a1e)
+    wgrad_round(acc, img_gm, img_am);
+    if (EU) wgrad_round(acc, img_ge, img_ae);
+    // ---- gz1 = (W2^T gz2) [a1 > 0], gC = gz1m + gz1e
+    constexpr int NI = EU ? 2 : 1;
+    f32x4 d[NI][2];
+    const unsigned char* imgs[NI];
+    imgs[0] = img_gm;
+    if (EU) imgs[NI - 1] = img_ge;
+    gemm_round<NI>(d, ws, imgs);
+    const int oc = 16 * w + 4 * (l >> 4);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = 16 * nb + (l & 15);
+      const int row = base + r;
+      const unsigned mm = *reinterpret_cast<const unsigned*>(msk_m + r * L + oc);
+      f32x4 zm;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) zm[j] = (mm >> (8 * j)) & 1u ? d[0][nb][j] : 0.f;
+      f32x4 c = zm;
+      if (EU) {
+        const unsigned me = *reinterpret_cast<const unsigned*>(msk_e + r * L + oc);
+        f32x4 ze;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ze[j] = (me >> (8 * j)) & 1u ? d[NI - 1][nb][j] : 0.f;
+        c = zm + ze;
+        if (row < r1) *reinterpret_cast<f32x4*>(gz1e + (size_t)row * L + oc) = ze;
+      }
+      if (row < r1) {
+        *reinterpret_cast<f32x4*>(gz1m + (size_t)row * L + oc) = zm;
+        *reinterpret_cast<f32x4*>(gC + (size_t)row * L + oc) = c;
+      }
+    }
+    __syncthreads();   // the images are rewritten by the next round
+  }
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+}
+
+// ============================================================================ Wc path
+template <bool RES>
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
+    const float* __restrict__ gC, const float* __restrict__ e, const float* __restrict__ ge_next,
+    const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs, int E) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img_c = sm;              // gC
+  unsigned char* img_e = sm + EBW_IMG;    // e
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(E, r0, r1);
+  WSlice ws;
+  load_wslice(ws, WcT, w);
+  f32x16 acc[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 pc[2], pe[2], pres[2];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
+      pc[u] = *reinterpret_cast<const f32x4*>(gC + rc);
+      pe[u] = *reinterpret_cast<const f32x4*>(e + rc);
+      // residual in the D layout of the GEMM (row 16u + (l & 15), features oc .. oc+3)
+      if (RES) pres[u] = *reinterpret_cast<const f32x4*>(ge_next + (size_t)clamp_row(base + 16 * u + (l & 15), r1) * L + oc);
+    }
+  };
+  if (r0 < r1) issue(r0);
+  for (int base = r0; base < r1; base += X6_ROWS) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const bool ok = base + r < r1;
+      const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4 c = ok ? pc[u] : zero;
+      bsum += c;
+      img_store4(img_c, r, cg, c);
+      img_store4(img_e, r, cg, ok ? pe[u] : zero);
+    }
+    f32x4 res[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) res[u] = RES ? pres[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    // ---- dWc += gC^T e
+    wgrad_round(acc, img_c, img_e);
+    // ---- ge_out = ge_next + Wc^T gC
+    f32x4 d[1][2];
+    const unsigned char* imgs[1] = {img_c};
+    gemm_round<1>(d, ws, imgs);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int row = base + 16 * nb + (l & 15);
+      if (row < r1) *reinterpret_cast<f32x4*>(ge_out + (size_t)row * L + oc) = RES ? res[nb] + d[0][nb] : d[0][nb];
+    }
+    __syncthreads();
+  }
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+}
+
+// ============================================================================ C ABI
+extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
+                               const float* a2m, const float* a1m, const float* a2e, const float* a1e,
+                               const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
+                               const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
+                               float* gz1e, float* gC, float* slabs, int nslabs, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_w2: n_edges must be > 0");
+  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_bwd_w2: bad slabs");
+  PDG_CHECK_ARG(dst && gaggr && a2m && a1m && st_m && lb_m && ln_g && W2T && gz1m && gC,
+                "pdg_edge_bwd_w2: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(ln_g) &&
+                    PDG_ALIGNED(W2T) && PDG_ALIGNED(gz1m) && PDG_ALIGNED(gC) && PDG_ALIGNED(slabs),
+                "pdg_edge_bwd_w2: misaligned pointer");
+  const bool eu = ge_next != nullptr;
+  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && gz1e && st_e && lb_e && PDG_ALIGNED(a2e) &&
+                        PDG_ALIGNED(a1e) && PDG_ALIGNED(gz1e)),
+                "pdg_edge_bwd_w2: edge-update arguments missing or misaligned");
+  const size_t shm = eu ? 4 * EBW_IMG + 2 * EBW_MASK : 2 * EBW_IMG + EBW_MASK;
+  if (eu)
+    hipLaunchKernelGGL(edge_bwd_w2_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, dst,
+                       gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, gz1m, gz1e, gC, slabs,
+                       n_edges);
+  else
+    hipLaunchKernelGGL(edge_bwd_w2_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, dst,
+                       gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, gz1m, gz1e, gC, slabs,
+                       n_edges);
+  PDG_CHECK_LAUNCH("pdg_edge_bwd_w2");
+  return PDG_OK;
+}
+
+extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
+                                float* ge_out, float* slabs, int nslabs, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_gout_wc: n_edges must be > 0");
+  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_gout_wc: bad slabs");
+  PDG_CHECK_ARG(gC && e && WcT && ge_out, "pdg_edge_gout_wc: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(gC) && PDG_ALIGNED(e) && PDG_ALIGNED(WcT) && PDG_ALIGNED(ge_out) &&
+                    PDG_ALIGNED(slabs) && (!ge_next || PDG_ALIGNED(ge_next)),
+                "pdg_edge_gout_wc: misaligned pointer");
+  PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_gout_wc: ge_out must not alias ge_next");
+  const size_t shm = 2 * EBW_IMG;
+  if (ge_next)
+    hipLaunchKernelGGL(edge_gout_wc_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
+                       ge_next, WcT, ge_out, slabs, n_edges);
+  else
+    hipLaunchKernelGGL(edge_gout_wc_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
+                       ge_next, WcT, ge_out, slabs, n_edges);
+  PDG_CHECK_LAUNCH("pdg_edge_gout_wc");
+  return PDG_OK;
+}

@@ -13,11 +13,11 @@
 // owns outputs o in [32w, 32w+32) and all 128 inputs (4 accumulators).
 #include "pdg_common.hpp"
 #include "pdg_runtime.hpp"
+#include "pdg_x6.hpp"
 
 using namespace pdg;
 
 constexpr int SLAB = L * L + L;   // floats per slab
-typedef float f32x16 __attribute__((ext_vector_type(16)));   // v_mfma_f32_32x32x2_f32 accumulator
 
 __device__ __forceinline__ void zero_acc16(f32x16 (&acc)[4]) {
 #pragma unroll
@@ -415,32 +415,6 @@ __global__ __launch_bounds__(256, 2) void wgrad_segments_kernel(WgradSegs sg, lo
 // are XOR-swizzled by ((r & 3) << 2 | (r >> 2) & 3): both the writes and each
 // 32-lane half of the transposed reads then hit 64 distinct banks.  Wave w owns the 64x64
 // output quadrant (o in 64(w>>1) + [0,64), i in 64(w&1) + [0,64)).
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-constexpr int X6_ROWS = 32;                       // rows staged per round
-constexpr int X6_ROWB = 256;                      // bytes per row of one term image
-constexpr int X6_TERM = X6_ROWS * X6_ROWB;        // bytes per term image (8 KB)
-
-// Byte address of byte `b` (0..255) of image row `r`.
-__device__ __forceinline__ int x6_addr(int r, int b) {
-  return r * X6_ROWB + (b ^ (((r & 3) << 6) | (((r >> 2) & 3) << 4)));
-}
-
-// (x0, x1) = hi + mid + lo exactly, per element: bf16 round-to-nearest-even of x, of the
-// remainder and of the rest, two elements per v_cvt_pk_bf16_f32 (a bf16 widens to float by
-// a 16-bit shift); each term comes out as a packed pair (x0 in the low half).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void split3_pair(float x0, float x1, unsigned& h, unsigned& m, unsigned& lo) {
-  h = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, bf16x2));
-  const float r0 = x0 - __uint_as_float(h << 16), r1 = x1 - __uint_as_float(h & 0xffff0000u);
-  m = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){r0, r1}, bf16x2));
-  const float q0 = r0 - __uint_as_float(m << 16), q1 = r1 - __uint_as_float(m & 0xffff0000u);
-  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){q0, q1}, bf16x2));
-}
-
 // Split 4 rows x 4 columns and write them: row i of this thread goes to image row 4 rg + i.
 __device__ __forceinline__ void x6_store(unsigned char* img, int cg, int rg, const f32x4 (&v)[4]) {
 #pragma unroll
@@ -470,19 +444,6 @@ __device__ __forceinline__ void x6_load(const WgTable* tb, int nseg, long base, 
       xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
-}
-
-// MFMA operand of columns col0 + (l & 31), rows 16 ks + 8 (l >> 5) + 0..7, from term image `img`:
-// two transposed reads of 4 rows each, at the lane's addresses ofs0 / ofs1 (row
-// 16 ks + 8 (l >> 5) + ((l & 15) >> 2) [+ 4], columns col0 + 16 ((l >> 4) & 1) + 4 (l & 3) .. +3).
-__device__ __forceinline__ bf16x8 x6_operand(const unsigned char* img, int ofs0, int ofs1) {
-  typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-  const s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + ofs0));
-  const s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + ofs1));
-  s16x4 v0 = a, v1 = b;
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  const s16x8 r = s16x8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-  return __builtin_bit_cast(bf16x8, r);
 }
 
 __global__ __launch_bounds__(256, 3) void wgrad_x6_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {

@@ -23,6 +23,7 @@ producer and the consumer of each normalised tensor.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -99,6 +100,11 @@ class EPDEngine:
         self._nslabs = 3 * torch.cuda.get_device_properties(self.device).multi_processor_count
         self._pair = torch.zeros(2, **f64)
         self.sync = None
+        # edge backward with the W2 / Wc weight gradients fused (pdg_edge_bwd_w2 / pdg_edge_gout_wc);
+        # False selects pdg_edge_bwd + deferred pdg_wgrad_segments passes (kept for A/B and tests)
+        self.fused_edge_wgrad = os.environ.get("PDG_FUSED_EDGE_WGRAD", "1") != "0"
+        self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
+                             lib.pdg_max_blocks())
         # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
         self.timed: dict | None = None
 
@@ -270,6 +276,11 @@ class EPDEngine:
         st = ctx.stats
         lb = _StatBuf(4, LN_BWD_BYTES, self.device)
         segs: dict[str, list] = {k: [] for k in ("W2", "Wc", "Wa", "Wb", "Wn2", "Wn1a", "Wn1b", "d1", "ne2", "ee2")}
+        fused = self.fused_edge_wgrad
+        if fused:
+            nse = self._nslabs_e
+            slabs_w2 = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
+            slabs_wc = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
 
         def colsum(rows, gy_rows, gidx, a2, st_ptr, gname, bname, lb_i):
             lib.pdg_ln_colsum(rows, _p(gy_rows), _p(gidx), _p(a2), st_ptr, _p(self._part_col), np_, s)
@@ -292,14 +303,16 @@ class EPDEngine:
         gaggr, gx_part, gx_t = (self._empty(N, L) for _ in range(3))
         gz1m, gz1e = self._empty(E, L), self._empty(E, L)
         ge_bufs = [self._empty(E, L), self._empty(E, L)]
+        gC_fused = self._empty(E, L) if fused else None
         gx_next = gx
         for t in reversed(range(ctx.steps)):
             d = ctx.per_step[t]
             eu = d["eu"]
             assert eu == (ge_next is not None)
             gz2n, gz1n, gP, gQ = (self._empty(N, L) for _ in range(4))
-            gz2m, gC = self._empty(E, L), self._empty(E, L)
-            gz2e = self._empty(E, L) if eu else None
+            gC = gC_fused if fused else self._empty(E, L)   # fused: consumed within the step
+            gz2m = None if fused else self._empty(E, L)
+            gz2e = self._empty(E, L) if (eu and not fused) else None
             ge_out = ge_bufs[t % 2]
             # node_net tail: n_t = LN_n(a2n_t), gy = gx_next   (x_{t+1} = n_t + x_t)
             colsum(N, gx_next, None, d["a2n"], st[d["i_n"]], "processor.node_net.4.weight",
@@ -317,18 +330,29 @@ class EPDEngine:
             if eu:
                 colsum(E, ge_next, None, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
                        "processor.edge_net.4.bias", 2)
-            self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr), _p(ge_next), _p(d["a2m"]),
-                    _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]], st[d["i_e"]] if eu else None, lb[1],
-                    lb[2] if eu else None, _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]),
-                    _p(gz2m), _p(gz1m), _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), s)
+            if fused:
+                self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
+                        _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
+                        st[d["i_e"]] if eu else None, lb[1], lb[2] if eu else None,
+                        _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(gz1m), _p(gz1e if eu else None),
+                        _p(gC), _p(slabs_w2), nse, s)
+                self._t("edge_gout", lib.pdg_edge_gout_wc, E, _p(gC), _p(d["e"]), _p(ge_next), _p(T["WcT"]),
+                        _p(ge_out), _p(slabs_wc), nse, s)
+            else:
+                self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr),
+                        _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
+                        st[d["i_e"]] if eu else None, lb[1], lb[2] if eu else None,
+                        _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]), _p(gz2m), _p(gz1m),
+                        _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), s)
             self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
                     _p(plan.perm_src), _p(gz1m), _p(gz1e if eu else None), _p(gP), _p(gQ), s)
             self._t("gemm_sum2", lib.pdg_gemm_sum2_rw, N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part),
                     _p(gx_t), s)
-            segs["W2"].append((gz2m, d["a1m"], E))
-            if eu:
-                segs["W2"].append((gz2e, d["a1e"], E))
-            segs["Wc"].append((gC, d["e"], E))
+            if not fused:
+                segs["W2"].append((gz2m, d["a1m"], E))
+                if eu:
+                    segs["W2"].append((gz2e, d["a1e"], E))
+                segs["Wc"].append((gC, d["e"], E))
             segs["Wa"].append((gP, d["x"], N))
             segs["Wb"].append((gQ, d["x"], N))
             segs["Wn2"].append((gz2n, d["a1n"], N))
@@ -377,3 +401,8 @@ class EPDEngine:
                 rw = (ctypes.c_int * n)(*[r for _, _, r in chunk])
                 self._t("wgrad_" + key, lib.pdg_wgrad_segments, n, gp, xp, rw, _p(self._slabs), ns, s)
                 lib.pdg_wgrad_reduce(_p(self._slabs), ns, _p(G[wname]), ld, col0, _p(G[bname]) if bname else None, s)
+        if fused:   # the slabs of the fused edge backward, accumulated over all steps
+            lib.pdg_wgrad_reduce(_p(slabs_w2), nse, _p(G["processor.edge_net.2.weight"]), L, 0,
+                                 _p(G["processor.edge_net.2.bias"]), s)
+            lib.pdg_wgrad_reduce(_p(slabs_wc), nse, _p(G["processor.edge_net.0.weight"]), 3 * L, 2 * L,
+                                 _p(G["processor.edge_net.0.bias"]), s)

@@ -171,3 +171,28 @@ def test_isolated_node_and_ragged_batch():
     ref = O.epd_forward(P, st, b.pos.cpu(), b.mean_stress.cpu(), b.nodes_types.cpu(), b.edge_index.cpu(),
                         b.edge_attr.cpu(), 3, scale_output=True)
     assert rel(out, ref) < OUT_TOL
+
+
+@pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
+def test_fused_edge_weight_gradients_match_separate_passes(nmesh, ngraph, steps):
+    """pdg_edge_bwd_w2 + pdg_edge_gout_wc (weight gradients fused into the edge backward,
+    slabs accumulated over the steps) against pdg_edge_bwd + pdg_wgrad_segments: every
+    parameter gradient and the input-gradient chain agree to fp32 summation-order noise.
+    (41, 3): ~15k edges, several 32-row rounds per block and a ragged last round;
+    (9, 1): fewer edges than blocks x 32 (empty blocks)."""
+    from gnn_local_stress import losses
+    from pdg import meshgen
+    samples = meshgen.make_dataset(ngraph, n=nmesh, hole_radius=(0.15, 0.3), seed=7)
+    batch = make_batch(samples)
+    stats = {k: float(v) for k, v in dataset_stats(batch).items()}
+    grads = {}
+    for fused in (True, False):
+        model = _model(steps, stats)
+        model._engine_for(batch.pos.device).fused_edge_wgrad = fused
+        pred = model(batch, scale_output=False).local_stress
+        gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
+        total, _, _ = losses.batch_loss(pred, batch, gt, divergence=True, divergence_penalty=10.0)
+        total.backward()
+        grads[fused] = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    for name, g in grads[True].items():
+        assert rel(g, grads[False][name]) < 1e-5, (name, rel(g, grads[False][name]))
