@@ -210,14 +210,19 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
  *   pdg_edge_bwd_w2:  gz1m/gz1e/gC as pdg_edge_bwd; slabs (zeroed before the first call)
  *                     += gz2m^T a1m + gz2e^T a1e and the b2 column sums; gz2m/gz2e are not
  *                     materialised.  ge_next == NULL: message branch only, gC = gz1m.
- *   pdg_edge_gout_wc: ge_out = [ge_next +] WcT gC; slabs += gC^T e and the b1 column sums. */
+ *   pdg_edge_gout_wc: ge_out = [ge_next +] WcT gC; slabs += gC^T e and the b1 column sums.
+ *                     a2ln != NULL: also the column sums of the backward of the LayerNorm that
+ *                     produced e (input a2ln, statistics st_ln, upstream gradient ge_out), as
+ *                     pdg_ln_colsum partials: nslabs rows of 256 doubles in ln_partials (one
+ *                     spare row after them for pdg_ln_colsum_finalize). */
 int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                     const float* a2m, const float* a1m, const float* a2e, const float* a1e,
                     const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
                     const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
                     float* gz1e, float* gC, float* slabs, int nslabs, void* stream);
 int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next,
-                     const float* WcT, float* ge_out, float* slabs, int nslabs, void* stream);
+                     const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
+                     const pdg_ln_stat* st_ln, double* ln_partials, void* stream);
 
 /* Backward of the P/Q gathers: gP[v] = sum_{dst-seg(v)} gz1m + sum_{src-seg(v)} gz1e,
  * gQ[v] = sum_{src-seg(v)} gz1m + sum_{dst-seg(v)} gz1e.  src-seg uses rowptr_src and

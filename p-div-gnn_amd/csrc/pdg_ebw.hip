@@ -324,10 +324,16 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
 template <bool RES>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
     const float* __restrict__ gC, const float* __restrict__ e, const float* __restrict__ ge_next,
-    const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs, int E) {
+    const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs,
+    const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, double* __restrict__ part, int E) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img_c = sm;              // gC
   unsigned char* img_e = sm + EBW_IMG;    // e
+  double* colsum = reinterpret_cast<double*>(sm + 2 * EBW_IMG);   // [sum gy (128) | sum gy*xhat (128)]
+  const bool ln = a2ln != nullptr;
+  LNStat stln;
+  if (ln) stln = *reinterpret_cast<const LNStat*>(stln_p);
+  for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) colsum[i] = 0.0;
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
@@ -341,48 +347,90 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
   f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 pc[2], pe[2], pres[2];
-  auto issue = [&](int base) {
+  // prefetched rows of the next round (a second slot, loads two rounds ahead, measured no faster)
+  struct Slot {
+    f32x4 c[2], e[2], res[2], a2[2];
+  };
+  Slot sa;
+  auto issue = [&](int base, Slot& sl) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
-      pc[u] = *reinterpret_cast<const f32x4*>(gC + rc);
-      pe[u] = *reinterpret_cast<const f32x4*>(e + rc);
+      sl.c[u] = *reinterpret_cast<const f32x4*>(gC + rc);
+      sl.e[u] = *reinterpret_cast<const f32x4*>(e + rc);
       // residual in the D layout of the GEMM (row 16u + (l & 15), features oc .. oc+3)
-      if (RES) pres[u] = *reinterpret_cast<const f32x4*>(ge_next + (size_t)clamp_row(base + 16 * u + (l & 15), r1) * L + oc);
+      const size_t rd = (size_t)clamp_row(base + 16 * u + (l & 15), r1) * L + oc;
+      if (RES) sl.res[u] = *reinterpret_cast<const f32x4*>(ge_next + rd);
+      // LayerNorm input of e (D layout) for the column sums of its backward
+      if (ln) sl.a2[u] = *reinterpret_cast<const f32x4*>(a2ln + rd);
     }
   };
-  if (r0 < r1) issue(r0);
-  for (int base = r0; base < r1; base += X6_ROWS) {
+  auto round = [&](int base, Slot& sl) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
       const bool ok = base + r < r1;
       const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 c = ok ? pc[u] : zero;
+      const f32x4 c = ok ? sl.c[u] : zero;
       bsum += c;
       img_store4(img_c, r, cg, c);
-      img_store4(img_e, r, cg, ok ? pe[u] : zero);
+      img_store4(img_e, r, cg, ok ? sl.e[u] : zero);
     }
-    f32x4 res[2];
+    f32x4 res[2], a2[2];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) res[u] = RES ? pres[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < 2; ++u) {
+      res[u] = RES ? sl.res[u] : f32x4{0.f, 0.f, 0.f, 0.f};
+      a2[u] = sl.a2[u];
+    }
     __syncthreads();
-    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS, sl);
     // ---- dWc += gC^T e
     wgrad_round(acc, img_c, img_e);
     // ---- ge_out = ge_next + Wc^T gC
     f32x4 d[1][2];
     const unsigned char* imgs[1] = {img_c};
     gemm_round<1>(d, ws, imgs);
+    f32x4 sg = f32x4{0.f, 0.f, 0.f, 0.f}, sx = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
       const int row = base + 16 * nb + (l & 15);
-      if (row < r1) *reinterpret_cast<f32x4*>(ge_out + (size_t)row * L + oc) = RES ? res[nb] + d[0][nb] : d[0][nb];
+      const f32x4 go = RES ? res[nb] + d[0][nb] : d[0][nb];
+      if (row < r1) {
+        *reinterpret_cast<f32x4*>(ge_out + (size_t)row * L + oc) = go;
+        if (ln) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            sg[j] += go[j];
+            sx[j] += go[j] * div_den(a2[nb][j] - stln.mean, stln.den, stln.rstd);
+          }
+        }
+      }
+    }
+    if (ln) {
+      // LayerNorm column sums (ln_colsum_kernel, pdg_bwd.hip) of this round: the 16 lanes of a
+      // quarter hold the rows of features oc .. oc+3, which no other lane of the block owns
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          sg[j] += __shfl_xor(sg[j], o);
+          sx[j] += __shfl_xor(sx[j], o);
+        }
+      if ((l & 15) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          colsum[oc + j] += (double)sg[j];
+          colsum[L + oc + j] += (double)sx[j];
+        }
+      }
     }
     __syncthreads();
-  }
+  };
+  if (r0 < r1) issue(r0, sa);
+  for (int base = r0; base < r1; base += X6_ROWS) round(base, sa);
   slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+  if (ln)
+    for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) part[(size_t)blockIdx.x * 2 * L + i] = colsum[i];
 }
 
 // ============================================================================ C ABI
@@ -416,7 +464,8 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
 }
 
 extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
-                                float* ge_out, float* slabs, int nslabs, void* stream) {
+                                float* ge_out, float* slabs, int nslabs, const float* a2ln, const pdg_ln_stat* st_ln,
+                                double* ln_partials, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_gout_wc: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_gout_wc: bad slabs");
   PDG_CHECK_ARG(gC && e && WcT && ge_out, "pdg_edge_gout_wc: null argument");
@@ -424,13 +473,14 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
                     PDG_ALIGNED(slabs) && (!ge_next || PDG_ALIGNED(ge_next)),
                 "pdg_edge_gout_wc: misaligned pointer");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_gout_wc: ge_out must not alias ge_next");
-  const size_t shm = 2 * EBW_IMG;
+  PDG_CHECK_ARG(!a2ln || (PDG_ALIGNED(a2ln) && st_ln && ln_partials), "pdg_edge_gout_wc: LayerNorm column-sum arguments");
+  const size_t shm = 2 * EBW_IMG + 2 * L * sizeof(double);
   if (ge_next)
     hipLaunchKernelGGL(edge_gout_wc_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, n_edges);
+                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges);
   else
     hipLaunchKernelGGL(edge_gout_wc_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, n_edges);
+                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges);
   PDG_CHECK_LAUNCH("pdg_edge_gout_wc");
   return PDG_OK;
 }

@@ -281,11 +281,22 @@ class EPDEngine:
             nse = self._nslabs_e
             slabs_w2 = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
             slabs_wc = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
+            part_e = torch.empty((nse + 1) * 2 * L, dtype=torch.float64, device=self.device)
 
         def colsum(rows, gy_rows, gidx, a2, st_ptr, gname, bname, lb_i):
             lib.pdg_ln_colsum(rows, _p(gy_rows), _p(gidx), _p(a2), st_ptr, _p(self._part_col), np_, s)
             lib.pdg_ln_colsum_finalize(_p(self._part_col), self._nparts.value, _p(P[gname]), st_ptr,
                                        _p(G[gname]), _p(G[bname]), lb[lb_i], s)
+            self._sync_bwd(lb, lb_i, st_ptr, s)
+
+        def colsum_e(rows, gy_rows, a2, st_ptr, gname, bname, lb_i):
+            """Column sums of the LayerNorm that produced an edge state e: fused mode takes the
+            partials pdg_edge_gout_wc wrote while producing gy_rows = d loss / d e."""
+            if not fused:
+                colsum(rows, gy_rows, None, a2, st_ptr, gname, bname, lb_i)
+                return
+            lib.pdg_ln_colsum_finalize(_p(part_e), nse, _p(P[gname]), st_ptr, _p(G[gname]), _p(G[bname]),
+                                       lb[lb_i], s)
             self._sync_bwd(lb, lb_i, st_ptr, s)
 
         gy = gy.contiguous()
@@ -328,16 +339,19 @@ class EPDEngine:
                                        _p(G["processor.edge_net.4.bias"]), lb[1], s)
             self._sync_bwd(lb, 1, st[d["i_m"]], s)
             if eu:
-                colsum(E, ge_next, None, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
-                       "processor.edge_net.4.bias", 2)
+                colsum_e(E, ge_next, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
+                         "processor.edge_net.4.bias", 2)
             if fused:
                 self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
                         _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                         st[d["i_e"]] if eu else None, lb[1], lb[2] if eu else None,
                         _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(gz1m), _p(gz1e if eu else None),
                         _p(gC), _p(slabs_w2), nse, s)
+                # + the column sums of the LayerNorm that produced e_t (LN_e of step t-1, or the encoder's)
+                a2ln, st_ln = ((ctx.per_step[t - 1]["a2e"], st[ctx.per_step[t - 1]["i_e"]]) if t > 0
+                               else (ctx.a2_ee, st[1]))
                 self._t("edge_gout", lib.pdg_edge_gout_wc, E, _p(gC), _p(d["e"]), _p(ge_next), _p(T["WcT"]),
-                        _p(ge_out), _p(slabs_wc), nse, s)
+                        _p(ge_out), _p(slabs_wc), nse, _p(a2ln), st_ln, _p(part_e), s)
             else:
                 self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr),
                         _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
@@ -369,7 +383,7 @@ class EPDEngine:
         lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
                              _p(G["node_encoder.0.bias"]), None, s)
         gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
-        colsum(E, ge_next, None, ctx.a2_ee, st[1], "edge_encoder.4.weight", "edge_encoder.4.bias", 3)
+        colsum_e(E, ge_next, ctx.a2_ee, st[1], "edge_encoder.4.weight", "edge_encoder.4.bias", 3)
         lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], lb[3],
                          _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), s)
         segs["ee2"].append((gz2e_, ctx.a1_ee, E))

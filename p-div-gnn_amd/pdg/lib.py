@@ -52,7 +52,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_accum": [I, P, P, P, P, P, I, P],
     "pdg_wgrad_reduce": [P, I, P, I, I, P, P],
     "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P],
-    "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P],
+    "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P],
     "pdg_wgrad_segments": [I, P, P, P, P, I, P],
     "pdg_wgrad_narrow": [I, P, P, I, I, P, P, P, P, P],
     "pdg_nmse_fwd": [I, P, P, P, P, P, P],
