@@ -41,6 +41,8 @@ PMC_NAMES = {"edge_fwd": "void edge_fwd_kernel<true, true>", "edge_bwd": "void e
              "wgrad_W2": "wgrad_x6_kernel", "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
              "edge_gout": "void edge_gout_wc_kernel<true>"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
+PEAK_BF16_MFMA = 16 * PEAK_FP32_MFMA   # dense bf16 MFMA (2.5 PF; the fp32 rate is 1/16 of it, same guide)
+X6 = 6                      # bf16x6: six bf16 products per fp32-accurate product
 PEAK_HBM = 8.0e12           # MI355X HBM3E spec bandwidth (same guide; 6.3 TB/s measured copy)
 L = 128
 
@@ -205,25 +207,29 @@ def main():
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
     # algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops and the bytes the
     # kernel must read/write (inputs once, outputs once, int32 indices)
+    # per kernel: ([(executed MFMA flops, the peak of that instruction type)], bytes); an fp32-accurate
+    # 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA, or 6x that in bf16 (bf16x6)
+    g = 2 * L * L
     work = {
-        # 3 (128x128) GEMMs per edge; reads a2e_prev, e_prev, 4 gathered P/Q rows, src, dst;
-        # writes e_t, a1m, a2m, a1e, a2e
-        "edge_fwd": (E * 3 * 2 * L * L, E * (11 * 4 * L + 8)),
-        # fused (pdg_edge_bwd_w2): 2 GEMMs + 2 weight-gradient products per edge; reads gaggr[dst],
-        # ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gz1e, gC; one slab read+write per block.
-        # unfused (pdg_edge_bwd): 3 GEMMs; writes gz2m, gz1m, gz2e, gz1e, gC, ge_out
-        "edge_bwd": ((E * 4 * 2 * L * L, E * (9 * 4 * L + 4) + 2 * nslab_bytes) if fused
-                     else (E * 3 * 2 * L * L, E * (12 * 4 * L + 4))),
-        # fused Wc path (pdg_edge_gout_wc): GEMM + weight-gradient product; reads gC, e, ge_next,
-        # writes ge_out; one slab read+write per block
-        "edge_gout": (E * 2 * 2 * L * L, E * 4 * 4 * L + 2 * nslab_bytes),
+        # W_c product (fp32 MFMA) + 2 W2 products (bf16x6) per edge; reads a2e_prev, e_prev, 4 gathered
+        # P/Q rows, src, dst; writes e_t, a1m, a2m, a1e, a2e
+        "edge_fwd": ([(E * g, PEAK_FP32_MFMA), (E * 2 * g * X6, PEAK_BF16_MFMA)], E * (11 * 4 * L + 8)),
+        # fused (pdg_edge_bwd_w2): 2 W2^T products + 2 weight-gradient products per edge (bf16x6);
+        # reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gz1e, gC; one slab
+        # read+write per block.  unfused (pdg_edge_bwd): W2^T x2 (bf16x6) + Wc^T (fp32); writes
+        # gz2m, gz1m, gz2e, gz1e, gC, ge_out
+        "edge_bwd": (([(E * 4 * g * X6, PEAK_BF16_MFMA)], E * (9 * 4 * L + 4) + 2 * nslab_bytes) if fused
+                     else ([(E * 2 * g * X6, PEAK_BF16_MFMA), (E * g, PEAK_FP32_MFMA)], E * (12 * 4 * L + 4))),
+        # fused Wc path (pdg_edge_gout_wc): Wc^T product + weight-gradient product (bf16x6); reads gC,
+        # e, ge_next and the LayerNorm input of e (column sums), writes ge_out; one slab read+write
+        "edge_gout": ([(E * 2 * g * X6, PEAK_BF16_MFMA)], E * 5 * 4 * L + 2 * nslab_bytes),
         # all steps' W2 segments: 2E rows per step of (G, X) 512-byte rows, one 64 KB slab per block
-        "wgrad_W2": (S * 2 * E * 2 * L * L, S * 2 * E * 2 * 4 * L + 512 * (L * L + L) * 4),
+        "wgrad_W2": ([(S * 2 * E * g * X6, PEAK_BF16_MFMA)], S * 2 * E * 2 * 4 * L + 512 * (L * L + L) * 4),
         # dst-segment sum of LN(a2m): reads a2m (E rows) and rowptr, writes aggr (+ x-hat sums)
-        "segment_sum": (0, 4 * L * E + 4 * (N + 1) + (1 if infer else 2) * 4 * L * N),
-        # node_net, 2 GEMMs (K = 256, 128) per node: reads aggr, x; writes a2n (+ a1n)
-        "node_net": (N * 2 * L * (2 * L + L), 2 * 4 * L * N + (1 if infer else 2) * 4 * L * N),
-        "pq_scatter_bwd": (0, 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
+        "segment_sum": ([], 4 * L * E + 4 * (N + 1) + (1 if infer else 2) * 4 * L * N),
+        # node_net, 2 fp32 GEMMs (K = 256, 128) per node: reads aggr, x; writes a2n (+ a1n)
+        "node_net": ([(N * 2 * L * (2 * L + L), PEAK_FP32_MFMA)], 2 * 4 * L * N + (1 if infer else 2) * 4 * L * N),
+        "pq_scatter_bwd": ([], 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
     }
 
     pmc = {}
@@ -237,13 +243,15 @@ def main():
                 pmc[k] = round(hit[0]["total"])
 
     def roof(k):
-        flops, nbytes = work[k]
+        terms, nbytes = work[k]
         t = kt[k]
-        f_mfma = flops / t / PEAK_FP32_MFMA
+        flops = sum(f for f, _ in terms)
+        t_peak = sum(f / pk for f, pk in terms)     # matrix-core time at peak rate
+        f_mfma = t_peak / t
         f_hbm = nbytes / t / PEAK_HBM
         bound = "mfma" if f_mfma >= f_hbm else "hbm"
-        if bound == "mfma":
-            ach, peak, unit = flops / t / 1e12, PEAK_FP32_MFMA / 1e12, "TFLOP/s"
+        if bound == "mfma":   # executed flops / time against the flop-weighted peak of the mix
+            ach, peak, unit = flops / t / 1e12, flops / t_peak / 1e12, "TFLOP/s"
         else:
             ach, peak, unit = nbytes / t / 1e9, PEAK_HBM / 1e9, "GB/s"
         return {"kernel": k, "bound": bound, "achieved": round(ach, 2), "peak": round(peak, 1), "unit": unit,
