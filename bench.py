@@ -212,8 +212,9 @@ def main():
     g = 2 * L * L
     work = {
         # W_c product (fp32 MFMA) + 2 W2 products (bf16x6) per edge; reads a2e_prev, e_prev, 4 gathered
-        # P/Q rows, src, dst; writes e_t, a1m, a2m, a1e, a2e
-        "edge_fwd": ([(E * g, PEAK_FP32_MFMA), (E * 2 * g * X6, PEAK_BF16_MFMA)], E * (11 * 4 * L + 8)),
+        # P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e
+        "edge_fwd": ([(E * g, PEAK_FP32_MFMA), (E * 2 * g * X6, PEAK_BF16_MFMA)],
+                     E * ((9 if infer else 11) * 4 * L + 8)),
         # fused (pdg_edge_bwd_w2): 2 W2^T products + 2 weight-gradient products per edge (bf16x6);
         # reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gz1e, gC; one slab
         # read+write per block.  unfused (pdg_edge_bwd): W2^T x2 (bf16x6) + Wc^T (fp32); writes
