@@ -224,6 +224,21 @@ int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* 
                      const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
                      const pdg_ln_stat* st_ln, double* ln_partials, void* stream);
 
+/* Mesh graph on the device (pdg_graph.hip): FaceToEdge of a triangle
+ * mesh (convert_utils.py:47-60), edge lengths (datasets.py:182-188) and, when `periodic`,
+ * compute_periodic_graph (datasets.py:39-119), coalesced (rows ascending, columns ascending
+ * within a row; attribute = the length for a mesh edge, 0 for a periodic-only pair).
+ * points: (n_nodes, dim) fp32, dim 2 or 3 (sides from the first two coordinates); faces:
+ * (n_faces, 3) int64.  Outputs edge_rows / edge_cols (int64) / edge_attr (fp32) of
+ * `capacity` >= 6 n_faces (+ 4 PDG_SIDE_MAX + 4 when periodic) entries; *n_edges (device
+ * int) receives the edge count, or -1 for invalid periodic geometry (opposite sides of
+ * different lengths, a corner that is not exactly one node, a side longer than
+ * PDG_SIDE_MAX = 4096).  scratch: pdg_mesh_graph_scratch_bytes(n_nodes, n_faces) bytes. */
+long pdg_mesh_graph_scratch_bytes(int n_nodes, int n_faces);
+int pdg_mesh_graph(int n_nodes, const float* points, int dim, int n_faces, const int64_t* faces,
+                   int periodic, int64_t* edge_rows, int64_t* edge_cols, float* edge_attr,
+                   long capacity, int* n_edges, void* scratch, long scratch_bytes, void* stream);
+
 /* Backward of the P/Q gathers: gP[v] = sum_{dst-seg(v)} gz1m + sum_{src-seg(v)} gz1e,
  * gQ[v] = sum_{src-seg(v)} gz1m + sum_{dst-seg(v)} gz1e.  src-seg uses rowptr_src and
  * perm_src (positions of the dst-sorted edges grouped by src).  gz1e may be NULL (no

@@ -78,13 +78,28 @@ def von_mises_stress(sx, sy, sxy):
     return np.sqrt(0.5 * ((sx - sy) ** 2 + sx ** 2 + sy ** 2 + 6 * sxy ** 2))
 
 
-def load_sample(mesh_filename: str | Path, data_filename: str | Path, periodic_graph: bool = True) -> Data:
-    """One dataset sample exactly as datasets.py:247-281 builds it."""
+def load_sample(mesh_filename: str | Path, data_filename: str | Path, periodic_graph: bool = True,
+                device=None) -> Data:
+    """One dataset sample exactly as datasets.py:247-281 builds it.  With a HIP ``device`` the
+    graph (FaceToEdge, lengths, periodic connections, coalesce) is built there by
+    ``pdg.devgraph.mesh_graph`` (the same edges, and bitwise the same lengths
+    for single-precision VTK points -- double-precision points are rounded to fp32 first, where
+    the reference takes the lengths in fp64 and rounds them: within 1 ulp) and the sample's
+    tensors stay on the host until the caller moves them."""
     points, faces = read_legacy_vtk(mesh_filename)
-    graph = mesh_to_graph(points, faces)
-    graph.edge_attr = compute_node_distances_as_edge_weights(graph).float()
-    if periodic_graph:
-        graph = compute_periodic_graph(graph)
+    if device is not None and torch.device(device).type == "cuda":
+        from pdg.devgraph import mesh_graph
+        if faces.shape[1] != 3:
+            raise ValueError("only triangle meshes are supported (quad meshes: convert_utils.py:63-80)")
+        ei, ea = mesh_graph(torch.from_numpy(np.ascontiguousarray(points, np.float32)).to(device),
+                            torch.from_numpy(np.ascontiguousarray(faces, np.int64)).to(device), periodic_graph)
+        graph = Data(pos=torch.from_numpy(np.ascontiguousarray(points)), edge_index=ei.cpu(), edge_attr=ea.cpu(),
+                     face=torch.from_numpy(np.ascontiguousarray(faces.T)))
+    else:
+        graph = mesh_to_graph(points, faces)
+        graph.edge_attr = compute_node_distances_as_edge_weights(graph).float()
+        if periodic_graph:
+            graph = compute_periodic_graph(graph)
     graph.is_periodic = periodic_graph
     with np.load(data_filename, allow_pickle=False) as mesh_data:
         stress_field = torch.from_numpy(mesh_data["stress_field"]).float()
@@ -103,10 +118,10 @@ class MeshStressFieldDatasetInMemory:
     """datasets.py:232-311 without PyG: ``len``, indexing, the eight scalar
     standardisation constants of the whole set (:283-291) and the collated data."""
 
-    def __init__(self, dataframe, transform=None, periodic_graph: bool = True) -> None:
+    def __init__(self, dataframe, transform=None, periodic_graph: bool = True, device=None) -> None:
         self.dataframe = dataframe
         self.transform = transform
-        self.graphs = [load_sample(m, d, periodic_graph)
+        self.graphs = [load_sample(m, d, periodic_graph, device)
                        for m, d in zip(dataframe["mesh_filename"], dataframe["data_filename"])]
         data = Batch.from_data_list(self.graphs)
         self.mean_pos = data.pos.mean()

@@ -53,6 +53,8 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_reduce": [P, I, P, I, I, P, P],
     "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P],
     "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P],
+    "pdg_mesh_graph": [I, P, I, I, P, I, P, P, P, ctypes.c_long, P, P, ctypes.c_long, P],
+    "pdg_mesh_graph_scratch_bytes": [I, I],
     "pdg_wgrad_segments": [I, P, P, P, P, I, P],
     "pdg_wgrad_narrow": [I, P, P, I, I, P, P, P, P, P],
     "pdg_nmse_fwd": [I, P, P, P, P, P, P],
@@ -64,7 +66,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_collate": [P, I, ctypes.c_long, P],
     "pdg_adam": [c_int64, P, P, P, P, c_float, c_float, c_float, c_float, I, P, P],
 }
-_RESTYPES = {"pdg_last_error": ctypes.c_char_p}
+_RESTYPES = {"pdg_last_error": ctypes.c_char_p, "pdg_mesh_graph_scratch_bytes": ctypes.c_long}
 
 LN_STAT_BYTES = 40   # sizeof(pdg_ln_stat)
 LN_BWD_BYTES = 24    # sizeof(pdg_ln_bwd)

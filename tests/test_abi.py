@@ -12,7 +12,7 @@ HEADER = ROOT / "include" / "pdivgnn.h"
 def _decls():
     text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
     out = {}
-    for m in re.finditer(r"\b(?:int|const char\*)\s+(pdg_\w+)\s*\(([^)]*)\)\s*;", text, re.S):
+    for m in re.finditer(r"\b(?:int|long|const char\*)\s+(pdg_\w+)\s*\(([^)]*)\)\s*;", text, re.S):
         args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
         out[m.group(1)] = args
     return out
@@ -46,6 +46,11 @@ def test_library_reports_errors_without_gpu():
     with pytest.raises(PdgError, match="rows must be > 0"):
         lib.pdg_mlp2_fwd(0, None, None, None, None, None, None, None)
     assert lib.pdg_max_blocks() >= 256
+    # mesh-graph scratch sizing is host arithmetic; argument checks precede any HIP call
+    assert lib.pdg_mesh_graph_scratch_bytes(100, 150) > 4 * (6 * 150)
+    assert lib.pdg_mesh_graph_scratch_bytes(0, 1) < 0
+    with pytest.raises(PdgError, match="bad sizes"):
+        lib.pdg_mesh_graph(10, None, 4, 0, None, 1, None, None, None, 0, None, None, 0, None)
 
 
 def test_struct_sizes_match_header():
