@@ -37,6 +37,12 @@ constexpr int EBW_THREADS = 64 * EBW_WAVES;
 constexpr int EBW_IMG = 3 * X6_TERM;        // one bf16x6 image of 32 rows (24 KB)
 constexpr int EBW_MASK = X6_ROWS * L;       // relu mask bytes of 32 rows
 constexpr int WSLAB = L * L + L;            // floats per slab (weight + bias sums)
+// fp32 row tile in LDS that turns the product's output layout (16 rows x 64 B per wave
+// instruction: 25 % below whole-row access in an isolated stream, tools/membench.hip) into
+// row-major global accesses: 32 rows, stride 132 floats (the 16-row column writes of the
+// output layout then hit 64 distinct banks).  Used by pdg_edge_gout_wc (-2 %); in
+// pdg_edge_bwd_w2 the three extra tiles measured +2 % and are not used.
+constexpr int OT_STRIDE = L + 4;
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
@@ -327,13 +333,12 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
     const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs,
     const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, double* __restrict__ part, int E) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  unsigned char* img_c = sm;              // gC
-  unsigned char* img_e = sm + EBW_IMG;    // e
-  double* colsum = reinterpret_cast<double*>(sm + 2 * EBW_IMG);   // [sum gy (128) | sum gy*xhat (128)]
+  unsigned char* img_c = sm;                                         // gC
+  unsigned char* img_e = sm + EBW_IMG;                               // e
+  float* t_o = reinterpret_cast<float*>(sm + 2 * EBW_IMG);           // Wc^T gC rows
   const bool ln = a2ln != nullptr;
   LNStat stln;
   if (ln) stln = *reinterpret_cast<const LNStat*>(stln_p);
-  for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) colsum[i] = 0.0;
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
@@ -347,90 +352,92 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
   f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  // prefetched rows of the next round (a second slot, loads two rounds ahead, measured no faster)
-  struct Slot {
-    f32x4 c[2], e[2], res[2], a2[2];
-  };
-  Slot sa;
-  auto issue = [&](int base, Slot& sl) {
+  // LayerNorm column sums of this thread's columns 4cg .. 4cg+3 (ln_colsum_kernel, pdg_bwd.hip)
+  double cs_g[4] = {0, 0, 0, 0}, cs_x[4] = {0, 0, 0, 0};
+  // prefetched rows of the next round, all whole-row (a second slot measured no faster)
+  f32x4 pc[2], pe[2], pres[2], pa2[2];
+  auto issue = [&](int base) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
-      sl.c[u] = *reinterpret_cast<const f32x4*>(gC + rc);
-      sl.e[u] = *reinterpret_cast<const f32x4*>(e + rc);
-      // residual in the D layout of the GEMM (row 16u + (l & 15), features oc .. oc+3)
-      const size_t rd = (size_t)clamp_row(base + 16 * u + (l & 15), r1) * L + oc;
-      if (RES) sl.res[u] = *reinterpret_cast<const f32x4*>(ge_next + rd);
-      // LayerNorm input of e (D layout) for the column sums of its backward
-      if (ln) sl.a2[u] = *reinterpret_cast<const f32x4*>(a2ln + rd);
+      pc[u] = *reinterpret_cast<const f32x4*>(gC + rc);
+      pe[u] = *reinterpret_cast<const f32x4*>(e + rc);
+      if (RES) pres[u] = *reinterpret_cast<const f32x4*>(ge_next + rc);
+      if (ln) pa2[u] = *reinterpret_cast<const f32x4*>(a2ln + rc);   // LayerNorm input of e
     }
   };
-  auto round = [&](int base, Slot& sl) {
+  if (r0 < r1) issue(r0);
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    f32x4 res[2], a2[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
       const bool ok = base + r < r1;
       const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 c = ok ? sl.c[u] : zero;
+      const f32x4 c = ok ? pc[u] : zero;
       bsum += c;
       img_store4(img_c, r, cg, c);
-      img_store4(img_e, r, cg, ok ? sl.e[u] : zero);
-    }
-    f32x4 res[2], a2[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      res[u] = RES ? sl.res[u] : f32x4{0.f, 0.f, 0.f, 0.f};
-      a2[u] = sl.a2[u];
+      img_store4(img_e, r, cg, ok ? pe[u] : zero);
+      res[u] = RES ? pres[u] : zero;
+      a2[u] = ln ? pa2[u] : zero;
     }
     __syncthreads();
-    if (base + X6_ROWS < r1) issue(base + X6_ROWS, sl);
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
     // ---- dWc += gC^T e
     wgrad_round(acc, img_c, img_e);
-    // ---- ge_out = ge_next + Wc^T gC
+    // ---- Wc^T gC in the product's output layout -> row tile
     f32x4 d[1][2];
     const unsigned char* imgs[1] = {img_c};
     gemm_round<1>(d, ws, imgs);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+      *reinterpret_cast<f32x4*>(t_o + (16 * nb + (l & 15)) * OT_STRIDE + oc) = d[0][nb];
+    __syncthreads();   // tile complete; the images are free for the next round
+    // ---- ge_out = ge_next + Wc^T gC, whole rows; column sums of the LayerNorm that produced e
     f32x4 sg = f32x4{0.f, 0.f, 0.f, 0.f}, sx = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int row = base + 16 * nb + (l & 15);
-      const f32x4 go = RES ? res[nb] + d[0][nb] : d[0][nb];
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const int row = base + r;
       if (row < r1) {
-        *reinterpret_cast<f32x4*>(ge_out + (size_t)row * L + oc) = go;
+        const f32x4 dv = *reinterpret_cast<const f32x4*>(t_o + r * OT_STRIDE + 4 * cg);
+        const f32x4 go = RES ? res[u] + dv : dv;
+        *reinterpret_cast<f32x4*>(ge_out + (size_t)row * L + 4 * cg) = go;
         if (ln) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             sg[j] += go[j];
-            sx[j] += go[j] * div_den(a2[nb][j] - stln.mean, stln.den, stln.rstd);
+            sx[j] += go[j] * div_den(a2[u][j] - stln.mean, stln.den, stln.rstd);
           }
         }
       }
     }
     if (ln) {
-      // LayerNorm column sums (ln_colsum_kernel, pdg_bwd.hip) of this round: the 16 lanes of a
-      // quarter hold the rows of features oc .. oc+3, which no other lane of the block owns
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          sg[j] += __shfl_xor(sg[j], o);
-          sx[j] += __shfl_xor(sx[j], o);
-        }
-      if ((l & 15) == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          colsum[oc + j] += (double)sg[j];
-          colsum[L + oc + j] += (double)sx[j];
-        }
+      for (int j = 0; j < 4; ++j) {
+        cs_g[j] += (double)sg[j];
+        cs_x[j] += (double)sx[j];
       }
     }
-    __syncthreads();
-  };
-  if (r0 < r1) issue(r0, sa);
-  for (int base = r0; base < r1; base += X6_ROWS) round(base, sa);
+  }
+  __syncthreads();   // the last round's tile reads precede the LDS reuse below
   slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
-  if (ln)
-    for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) part[(size_t)blockIdx.x * 2 * L + i] = colsum[i];
+  if (ln) {
+    // block partial = the 16 row groups' column sums, reduced in order through LDS
+    double* red = reinterpret_cast<double*>(sm + 2 * EBW_IMG);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[rg * 2 * L + 4 * cg + j] = cs_g[j];
+      red[rg * 2 * L + L + 4 * cg + j] = cs_x[j];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) {
+      double v = 0;
+      for (int g = 0; g < EBW_THREADS / 32; ++g) v += red[g * 2 * L + i];
+      part[(size_t)blockIdx.x * 2 * L + i] = v;
+    }
+  }
 }
 
 // ============================================================================ C ABI
@@ -474,7 +481,7 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
                 "pdg_edge_gout_wc: misaligned pointer");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_gout_wc: ge_out must not alias ge_next");
   PDG_CHECK_ARG(!a2ln || (PDG_ALIGNED(a2ln) && st_ln && ln_partials), "pdg_edge_gout_wc: LayerNorm column-sum arguments");
-  const size_t shm = 2 * EBW_IMG + 2 * L * sizeof(double);
+  const size_t shm = 2 * EBW_IMG + (size_t)EBW_THREADS / 32 * 2 * L * sizeof(double);   // >= the row tile
   if (ge_next)
     hipLaunchKernelGGL(edge_gout_wc_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
                        ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges);
