@@ -227,6 +227,10 @@ __device__ __forceinline__ void load_wblock_swz(float* __restrict__ lds, const f
 
 // gemm128 on the swizzled fp32 image (same MFMA order and pipelining, so the same results).
 __device__ __forceinline__ void gemm128_swz(Acc& acc, const float* __restrict__ wl, const float (&v)[FRAG]) {
+#ifdef PDG_DIAG_NOMFMA   // timing experiment only: results are wrong
+  acc.b[0][0] += v[0];
+  return;
+#endif
   const int l = lane_id(), i = l & 15, q = l >> 4;
   // chunk (4t + q) ^ i = 4 (t ^ (i >> 2)) + (q ^ (i & 3))
   const float* base = wl + opaque(i * 128 + 4 * (q ^ (i & 3)));
@@ -310,6 +314,10 @@ __device__ __forceinline__ void load_wplanes(unsigned char* __restrict__ planes,
 
 __device__ __forceinline__ void gemm128_x6(Acc& acc, const unsigned char* __restrict__ planes,
                                            const float (&v)[FRAG]) {
+#ifdef PDG_DIAG_NOMFMA
+  acc.b[0][0] += v[0];
+  return;
+#endif
   const int l = lane_id(), i = l & 15, q = l >> 4;
   // chunk (4m + q) ^ i = 4 (m ^ (i >> 2)) + (q ^ (i & 3))
   const unsigned char* base = planes + opaque(i * 256 + 16 * (q ^ (i & 3)));
