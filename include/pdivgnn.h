@@ -44,13 +44,10 @@ typedef struct pdg_ln_stat {
   double mean_d, std_d, count; /* fp64 copies and the element count M */
 } pdg_ln_stat;
 
-/* Backward scalars of one graph-LayerNorm call.  `ticket` is the arrival counter of
- * pdg_ln_colsum_finalize's single launch: zero when the struct is allocated, left zero by
- * every call. */
+/* Backward scalars of one graph-LayerNorm call. */
 typedef struct pdg_ln_bwd {
   float c1, c2;
   double S1, S2;
-  unsigned ticket, pad_;
 } pdg_ln_bwd;
 
 /* ---------------------------------------------------------------- library */
@@ -160,9 +157,7 @@ int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* rowptr, cons
 
 /* Reduce colsum partials: grad_b += sum gy, grad_g += sum gy*xhat, and the call's
  * backward scalars (S1 = sum g*gy, S2 = sum g*gy*xhat).  Row nparts of `partials`
- * (256 doubles after the last partial) is used as scratch.  One launch: a block per
- * column; the last block to arrive (out->ticket, agent-scope acq_rel) finalises, so
- * calls sharing one `out` must not run concurrently. */
+ * (256 doubles after the last partial) is used as scratch. */
 int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g,
                            const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
                            void* stream);

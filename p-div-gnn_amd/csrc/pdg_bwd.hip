@@ -206,8 +206,8 @@ extern "C" int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* r
 }
 
 // Two-level reduction of the per-block partials (P x 256 doubles): one block per
-// column sums its P partials with 256 threads and a fixed-order tree; the last block
-// to arrive turns the 256 column sums into parameter gradients and S1/S2 (one launch).
+// column sums its P partials with 256 threads and a fixed-order tree, then a
+// single block turns the 256 column sums into parameter gradients and S1/S2.
 __device__ __forceinline__ double block_tree_sum(double x, double* red) {
   red[threadIdx.x] = x;
   __syncthreads();
@@ -218,50 +218,38 @@ __device__ __forceinline__ double block_tree_sum(double x, double* red) {
   return red[0];
 }
 
-__global__ __launch_bounds__(256) void ln_colsum_finalize_kernel(const double* __restrict__ part, int n,
-                                                                 double* __restrict__ cols,
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const double* __restrict__ part, int n, int width,
+                                                            double* __restrict__ out) {
+  __shared__ double red[256];
+  const int col = blockIdx.x;
+  double s = 0;
+  for (int b = threadIdx.x; b < n; b += blockDim.x) s += part[(size_t)b * width + col];
+  const double t = block_tree_sum(s, red);
+  if (threadIdx.x == 0) out[col] = t;
+}
+
+__global__ __launch_bounds__(128) void ln_colsum_finalize_kernel(const double* __restrict__ cols,
                                                                  const float* __restrict__ g,
                                                                  const pdg_ln_stat* __restrict__ stp,
                                                                  float* __restrict__ grad_g,
                                                                  float* __restrict__ grad_b,
                                                                  pdg_ln_bwd* __restrict__ out) {
-  __shared__ double red[256];
-  __shared__ int last;
-  const int col = blockIdx.x;
-  double s = 0;
-  for (int b = threadIdx.x; b < n; b += blockDim.x) s += part[(size_t)b * 256 + col];
-  const double t = block_tree_sum(s, red);
-  if (threadIdx.x == 0) {
-    cols[col] = t;
-    // releases cols[col]; the last arrival acquires every other block's column (agent scope: all XCDs)
-    const unsigned prev = __hip_atomic_fetch_add(&out->ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __shared__ double red2[2 * 16];
   const int c = threadIdx.x;
-  double s1 = 0, s2 = 0;
-  if (c < 128) {
-    unsigned long long* cu = reinterpret_cast<unsigned long long*>(cols);
-    const double sg = __longlong_as_double(
-        (long long)__hip_atomic_load(cu + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    const double sx = __longlong_as_double(
-        (long long)__hip_atomic_load(cu + 128 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if (grad_b) grad_b[c] += (float)sg;
-    if (grad_g) grad_g[c] += (float)sx;
-    s1 = (double)g[c] * sg;
-    s2 = (double)g[c] * sx;
-  }
-  block_sum2(s1, s2, red);   // waves 2 and 3 add zeros: the sums of the former 128-thread finalize
+  const double sg = cols[c], sx = cols[128 + c];
+  if (grad_b) grad_b[c] += (float)sg;
+  if (grad_g) grad_g[c] += (float)sx;
+  double s1 = (double)g[c] * sg, s2 = (double)g[c] * sx;
+  block_sum2(s1, s2, red2);
   if (threadIdx.x == 0) {
     const double M = stp->count;
     const double sd = stp->std_d;
-    out->S1 = s1;
-    out->S2 = s2;
-    out->c1 = (float)(s1 / M);
-    out->c2 = sd > 0 ? (float)(s2 / (M * sd)) : 0.f;
-    out->ticket = 0;   // ready for the next call (visible after the kernel boundary)
+    pdg_ln_bwd r;
+    r.S1 = s1;
+    r.S2 = s2;
+    r.c1 = (float)(s1 / M);
+    r.c2 = sd > 0 ? (float)(s2 / (M * sd)) : 0.f;
+    *out = r;
   }
 }
 
@@ -269,11 +257,12 @@ extern "C" int pdg_ln_colsum_finalize(const double* partials, int nparts, const 
                                       const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
                                       void* stream) {
   PDG_CHECK_ARG(nparts > 0 && nparts < MAX_BLOCKS, "pdg_ln_colsum_finalize: bad nparts");
-  PDG_CHECK_ARG(out && st && ln_g, "pdg_ln_colsum_finalize: null argument");
   // the 256 column sums go into the row right after the last partial (see the header)
   double* cols = const_cast<double*>(partials) + (size_t)nparts * 256;
-  hipLaunchKernelGGL(ln_colsum_finalize_kernel, dim3(256), dim3(256), 0, (hipStream_t)stream, partials, nparts,
-                     cols, ln_g, st, grad_g, grad_b, out);
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(256), dim3(256), 0, (hipStream_t)stream, partials, nparts, 256, cols);
+  PDG_CHECK_LAUNCH("pdg_ln_colsum_finalize(reduce)");
+  hipLaunchKernelGGL(ln_colsum_finalize_kernel, dim3(1), dim3(128), 0, (hipStream_t)stream, cols, ln_g, st, grad_g,
+                     grad_b, out);
   PDG_CHECK_LAUNCH("pdg_ln_colsum_finalize");
   return PDG_OK;
 }

@@ -69,7 +69,7 @@ SIGNATURES: dict[str, list] = {
 _RESTYPES = {"pdg_last_error": ctypes.c_char_p, "pdg_mesh_graph_scratch_bytes": ctypes.c_long}
 
 LN_STAT_BYTES = 40   # sizeof(pdg_ln_stat)
-LN_BWD_BYTES = 32    # sizeof(pdg_ln_bwd)
+LN_BWD_BYTES = 24    # sizeof(pdg_ln_bwd)
 
 
 class PdgError(RuntimeError):

@@ -63,8 +63,7 @@ def test_struct_sizes_match_header():
                     ("count", ctypes.c_double)]
 
     class Bwd(ctypes.Structure):
-        _fields_ = [("c1", ctypes.c_float), ("c2", ctypes.c_float), ("S1", ctypes.c_double), ("S2", ctypes.c_double),
-                    ("ticket", ctypes.c_uint), ("pad_", ctypes.c_uint)]
+        _fields_ = [("c1", ctypes.c_float), ("c2", ctypes.c_float), ("S1", ctypes.c_double), ("S2", ctypes.c_double)]
 
     assert ctypes.sizeof(Stat) == LN_STAT_BYTES and ctypes.sizeof(Bwd) == LN_BWD_BYTES
 

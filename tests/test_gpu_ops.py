@@ -228,7 +228,7 @@ def test_ln_colsum_and_mlp2_bwd_vs_autograd(env):
     gy = rnd(M, L)
     lib.pdg_ln_colsum(M, gy.data_ptr(), None, a2.data_ptr(), st.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
     gg, gb = torch.zeros(L, device="cuda"), torch.zeros(L, device="cuda")
-    lb = torch.zeros(32, dtype=torch.uint8, device="cuda")   # sizeof(pdg_ln_bwd), ticket zero
+    lb = torch.zeros(24, dtype=torch.uint8, device="cuda")
     lib.pdg_ln_colsum_finalize(part.data_ptr(), n.value, g.data_ptr(), st.data_ptr(), gg.data_ptr(), gb.data_ptr(),
                                lb.data_ptr(), s)
     WT = W.T.contiguous()
@@ -353,7 +353,7 @@ def test_node_bwd_matches_separate_kernels(env, N):
     den = float(torch.tensor(sd, dtype=torch.float32) + 1e-5)
     st = torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, N * L)),
                           dtype=torch.uint8).cuda()
-    lb = torch.frombuffer(bytearray(struct.pack("ffddII", 0.013, -0.021, 1.0, 2.0, 0, 0)), dtype=torch.uint8).cuda()
+    lb = torch.frombuffer(bytearray(struct.pack("ffdd", 0.013, -0.021, 1.0, 2.0)), dtype=torch.uint8).cuda()
     outs0 = [torch.empty(N, L, device="cuda") for _ in range(4)]
     lib.pdg_mlp2_bwd(N, gy.data_ptr(), None, a2.data_ptr(), a1.data_ptr(), st.data_ptr(), lb.data_ptr(),
                      g.data_ptr(), W2T.data_ptr(), outs0[0].data_ptr(), outs0[1].data_ptr(), s)
