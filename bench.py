@@ -262,7 +262,7 @@ def main():
                                    if k in pmc else None),
                 "flops_per_launch": flops,
                 "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4), "frac_hbm": round(f_hbm, 4),
-                "avg_launch_ms": round(t * 1e3, 4), "share_of_step": round(ktot[k] / el, 4)}
+                "avg_launch_ms": round(t * 1e3, 4), "share_of_step": round(ktot[k] / (el * ev_steps / args.steps), 4)}
 
     dominant = max([k for k in ("edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])
     if rank == 0:
