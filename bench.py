@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--dp-mode", default="replica", choices=["replica", "sync"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay forward+backward from a HIP graph captured in warmup (measured no faster: DESIGN §6)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     args = ap.parse_args()
 
@@ -158,7 +160,7 @@ def main():
     model = EncodeProcessDecode(input_edges_features_size=1, message_passing_steps=cfg["steps"], latent_size=L,
                                 input_nodes_features_size=6, output_nodes_features_size=3, **stats).to(device)
     trainer = Trainer(model, lr=1e-3, divergence=cfg["divergence"], divergence_penalty=10.0, process_group=pg,
-                      dp_mode=args.dp_mode)
+                      dp_mode=args.dp_mode, capture=args.graph)
     plan = plan_for(batch)
     N, E = plan.n_nodes, plan.n_edges
 
@@ -180,12 +182,16 @@ def main():
                      "node_pq", "gemm_sum2", "pq_scatter_bwd"]
     fused = eng.fused_edge_wgrad
     ev_steps = min(args.steps, 3)
+    graph_steps = 0 if (infer or not trainer.capture) else args.steps - ev_steps
     if pg is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         if i == args.steps - ev_steps:
+            # the event-timed steps launch eagerly (events cannot bracket launches inside a graph
+            # replay); the other timed steps replay the graph captured during warmup
+            trainer.capture = False
             eng.timed = {k: [] for k in timed_kernels}
         out = run_step()
     torch.cuda.synchronize()
@@ -283,7 +289,8 @@ def main():
             "config": {"workload": cfg["workload"], "graphs_per_gpu": cfg["graphs"], "nodes_per_gpu": N,
                        "edges_per_gpu": E, "global_batch": cfg["graphs"] * world,
                        "message_passing_steps": cfg["steps"], "latent": L, "divergence": cfg["divergence"],
-                       "parallelism": f"graph-DP x{world}" + ("" if args.dp_mode == "replica" else " (sync-LN)"), "final_loss": round(loss, 6)},
+                       "parallelism": f"graph-DP x{world}" + ("" if args.dp_mode == "replica" else " (sync-LN)"), "final_loss": round(loss, 6),
+                       "hip_graph_steps": graph_steps},
             "roofline": roof(dominant),
             "roofline_gather_scatter": [roof(k) for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
             "roofline_node_net": roof("node_net") if "node_net" in kt else None,

@@ -18,6 +18,13 @@ are views into it), so the all-reduce is a single 669 KB collective and Adam a
 single kernel.  GradScaler (gnn_train.py:111) is an fp32 power-of-two rescale,
 numerically the identity except that it skips the update when a gradient is
 non-finite; the same skip is applied here.
+
+capture=True records forward, loss and backward of a batch once in a HIP graph
+(torch.cuda.CUDAGraph = hipGraph on ROCm) and replays it on later steps with the
+same batch object: ~250 kernel launches per step become one graph launch.  The
+all-reduce, the non-finite check and Adam (whose bias correction depends on the
+host step count) stay eager.  Replays run the same kernels on the same buffers,
+so the results are bit-identical to eager steps (tests/test_gpu_trainer_graph.py).
 """
 from __future__ import annotations
 
@@ -31,7 +38,7 @@ from .plan import plan_for
 class Trainer:
     def __init__(self, model, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  divergence: bool = False, divergence_penalty: float = 1.0, process_group=None,
-                 dp_mode: str = "replica") -> None:
+                 dp_mode: str = "replica", capture: bool = False) -> None:
         if dp_mode not in ("replica", "sync"):
             raise ValueError("dp_mode must be 'replica' or 'sync'")
         dev = next(model.parameters()).device
@@ -65,6 +72,9 @@ class Trainer:
         self.step_count = 0
         self._gt_cache: dict = {}
         self._skip = torch.zeros(1, dtype=torch.int32, device=dev)
+        # captured forward+backward per batch object (dp_mode="sync" reads counts on the host: eager)
+        self.capture = capture and not self.sync
+        self._graph = None            # (id(batch), torch.cuda.CUDAGraph, static outputs)
 
     def _gt(self, batch) -> torch.Tensor:
         key = id(batch)
@@ -89,11 +99,38 @@ class Trainer:
             n_g, e_g, Bn = (int(v) for v in cnt.tolist())
             self.engine.set_sync(self.pg, n_g, e_g)
         try:
-            return self._step(batch, plan, stats8, B, N, Bn, f32, s)
+            if self.capture:
+                out = self._replay(batch, plan, stats8, B, N, Bn, f32)
+            else:
+                out = self._fwd_bwd(batch, plan, stats8, B, N, Bn, f32, s)
+            return self._update(out, f32, s)
         finally:
             self.engine.set_sync(None)
 
-    def _step(self, batch, plan, stats8, B, N, Bn, f32, s) -> dict:
+    def _replay(self, batch, plan, stats8, B, N, Bn, f32) -> dict:
+        """Forward + loss + backward through a HIP graph captured for this batch object.
+
+        Every device buffer the graph reads must outlive it at a fixed address: the batch and
+        its plan are held by the record, the target by the record's copy of the _gt cache entry,
+        and the 8 dataset statistics (a fresh tensor per step) are copied into the captured one."""
+        if self._graph is None or self._graph[0] is not batch:
+            self._graph = None
+            stats_c = stats8.clone()
+            side = torch.cuda.Stream(self.device)
+            side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(side):      # warm the allocator on the capture stream's pool
+                self._fwd_bwd(batch, plan, stats_c, B, N, Bn, f32, stream_handle(self.device))
+            torch.cuda.current_stream(self.device).wait_stream(side)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                static = self._fwd_bwd(batch, plan, stats_c, B, N, Bn, f32, stream_handle(self.device))
+            self._graph = (batch, g, static, stats_c, plan, self._gt(batch))
+        _, g, static, stats_c, _, _ = self._graph
+        stats_c.copy_(stats8)
+        g.replay()
+        return dict(static)
+
+    def _fwd_bwd(self, batch, plan, stats8, B, N, Bn, f32, s) -> dict:
         m = self.model
         y, ctx = self.engine.forward(self.P, stats8, plan, batch.pos, batch.mean_stress,
                                      batch.nodes_types.reshape(-1).contiguous(), batch.edge_attr.reshape(-1),
@@ -122,6 +159,9 @@ class Trainer:
         self.flat_g.zero_()
         self.engine.backward(self.P, ctx, gy, self.G)
         del ctx
+        return out
+
+    def _update(self, out, f32, s) -> dict:
         if self.pg is not None:
             torch.distributed.all_reduce(self.flat_g, group=self.pg)
             if self.sync:                           # per-rank shares of the global-batch loss: sum
