@@ -566,6 +566,8 @@ extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat
 // Half-wave (32 lanes x 16 B) per destination node; rows of a segment are
 // contiguous in the dst-sorted edge order, summed sequentially from zero in
 // segment order (= PyG scatter_add_ order for a coalesced edge_index).
+constexpr int SEG_U = 8;
+
 __global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __restrict__ rowptr,
                                                           const float* __restrict__ rows,
                                                           const pdg_ln_stat* __restrict__ stp,
@@ -587,34 +589,29 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __re
   for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
     const int k0 = rowptr[v], k1 = rowptr[v + 1];
     f32x4 acc = {0.f, 0.f, 0.f, 0.f}, xs = {0.f, 0.f, 0.f, 0.f};
-    int k = k0;
-    for (; k + 1 < k1; k += 2) {
-      f32x4 x0 = reinterpret_cast<const f32x4*>(rows + (size_t)k * L)[j];
-      f32x4 x1 = reinterpret_cast<const f32x4*>(rows + (size_t)(k + 1) * L)[j];
-      if (ln) {
+    // SEG_U rows in flight per round trip (the in-degree of a triangulated mesh is ~6): loads past
+    // the segment end re-read its last row (an L1/L2 hit) and are not accumulated, so the sums
+    // are formed row by row in CSR order exactly as a one-row-at-a-time loop would
+    for (int k = k0; k < k1; k += SEG_U) {
+      f32x4 x[SEG_U];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float h0 = div_den(x0[c] - mean, den, rstd), h1 = div_den(x1[c] - mean, den, rstd);
-          xs[c] += h0;
-          xs[c] += h1;
-          x0[c] = h0 * g[c] + b[c];
-          x1[c] = h1 * g[c] + b[c];
-        }
+      for (int u = 0; u < SEG_U; ++u) {
+        const int kk = k + u < k1 ? k + u : k1 - 1;
+        x[u] = reinterpret_cast<const f32x4*>(rows + (size_t)kk * L)[j];
       }
-      acc += x0;
-      acc += x1;
-    }
-    if (k < k1) {
-      f32x4 x0 = reinterpret_cast<const f32x4*>(rows + (size_t)k * L)[j];
-      if (ln) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float h0 = div_den(x0[c] - mean, den, rstd);
-          xs[c] += h0;
-          x0[c] = h0 * g[c] + b[c];
+      for (int u = 0; u < SEG_U; ++u) {
+        if (k + u >= k1) break;
+        if (ln) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float h = div_den(x[u][c] - mean, den, rstd);
+            xs[c] += h;
+            x[u][c] = h * g[c] + b[c];
+          }
         }
+        acc += x[u];
       }
-      acc += x0;
     }
     reinterpret_cast<f32x4*>(out + (size_t)v * L)[j] = acc;
     if (xsum) reinterpret_cast<f32x4*>(xsum + (size_t)v * L)[j] = xs;
