@@ -574,6 +574,8 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
 }
 
 // ============================================================================ P/Q gather backward
+constexpr int PQ_U = 8;
+
 __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* __restrict__ rpd,
                                                              const int* __restrict__ rps,
                                                              const int* __restrict__ perm_s,
@@ -584,16 +586,41 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* _
   const int nhw = blockDim.x >> 5;
   for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
     f32x4 p = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
+    // PQ_U rows in flight per round trip (loads past a segment's end re-read its last row and are
+    // not accumulated): the sums are formed row by row in segment order as a serial loop would
     const int d0 = rpd[v], d1 = rpd[v + 1];
-    for (int k = d0; k < d1; ++k) {   // edges whose target is v: message x_i, edge-update x[col]
-      p += reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
-      if (gz1e) q += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+    for (int k = d0; k < d1; k += PQ_U) {   // edges whose target is v: message x_i, edge-update x[col]
+      f32x4 xm[PQ_U], xe[PQ_U];
+#pragma unroll
+      for (int u = 0; u < PQ_U; ++u) {
+        const size_t kk = (size_t)(k + u < d1 ? k + u : d1 - 1) * L;
+        xm[u] = reinterpret_cast<const f32x4*>(gz1m + kk)[j];
+        if (gz1e) xe[u] = reinterpret_cast<const f32x4*>(gz1e + kk)[j];
+      }
+#pragma unroll
+      for (int u = 0; u < PQ_U; ++u) {
+        if (k + u >= d1) break;
+        p += xm[u];
+        if (gz1e) q += xe[u];
+      }
     }
     const int s0 = rps[v], s1 = rps[v + 1];
-    for (int i = s0; i < s1; ++i) {   // edges whose source is v: message x_j, edge-update x[row]
-      const int k = perm_s[i];
-      q += reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
-      if (gz1e) p += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+    for (int i = s0; i < s1; i += PQ_U) {   // edges whose source is v: message x_j, edge-update x[row]
+      int ks[PQ_U];
+#pragma unroll
+      for (int u = 0; u < PQ_U; ++u) ks[u] = perm_s[i + u < s1 ? i + u : s1 - 1];
+      f32x4 xm[PQ_U], xe[PQ_U];
+#pragma unroll
+      for (int u = 0; u < PQ_U; ++u) {
+        xm[u] = reinterpret_cast<const f32x4*>(gz1m + (size_t)ks[u] * L)[j];
+        if (gz1e) xe[u] = reinterpret_cast<const f32x4*>(gz1e + (size_t)ks[u] * L)[j];
+      }
+#pragma unroll
+      for (int u = 0; u < PQ_U; ++u) {
+        if (i + u >= s1) break;
+        q += xm[u];
+        if (gz1e) p += xe[u];
+      }
     }
     reinterpret_cast<f32x4*>(gP + (size_t)v * L)[j] = p;
     reinterpret_cast<f32x4*>(gQ + (size_t)v * L)[j] = q;
