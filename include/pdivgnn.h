@@ -74,6 +74,11 @@ int pdg_encoder_fwd(int rows, int in_features, const float* x_in, const float* W
 
 /* Reduce LayerNorm partials -> statistics (mean, std_pop + eps). */
 int pdg_ln_finalize(const double* partials, int nparts, double count, pdg_ln_stat* out, void* stream);
+/* Two pdg_ln_finalize calls with the same nparts and count in one launch (the message and
+ * edge-update LayerNorms after pdg_edge_fwd); bit-identical to the two calls.  New in this
+ * build: the reference has no separate statistics step (models.py:42-55 computes them inline). */
+int pdg_ln_finalize2(const double* part_a, const double* part_b, int nparts, double count,
+                     pdg_ln_stat* out_a, pdg_ln_stat* out_b, void* stream);
 /* Exact data-parallel LayerNorm (optional "sync" DP mode): reduce the
  * per-block partials to out2 = {sum, sumsq} (device, 2 doubles) for an all-reduce over
  * ranks, then pdg_ln_finalize(out2, 1, global_count, ...).  New in this build: the

@@ -215,8 +215,8 @@ extern "C" int pdg_encoder_fwd(int rows, int in_features, const float* x_in, con
 }
 
 // ============================================================================ LN finalize
-__global__ void ln_finalize_kernel(const double* __restrict__ part, int n, double count,
-                                   pdg_ln_stat* __restrict__ out) {
+__device__ __forceinline__ void ln_finalize_block(const double* __restrict__ part, int n, double count,
+                                                  pdg_ln_stat* __restrict__ out) {
   __shared__ double red[2 * 16];
   double a = 0, b = 0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) { a += part[2 * i]; b += part[2 * i + 1]; }
@@ -236,6 +236,31 @@ __global__ void ln_finalize_kernel(const double* __restrict__ part, int n, doubl
     s.count = count;
     *out = s;
   }
+}
+
+__global__ void ln_finalize_kernel(const double* __restrict__ part, int n, double count,
+                                   pdg_ln_stat* __restrict__ out) {
+  ln_finalize_block(part, n, count, out);
+}
+
+// two independent statistics in one launch (one block each, the same per-block arithmetic as
+// ln_finalize_kernel, so the results are bit-identical to two separate launches)
+__global__ void ln_finalize2_kernel(const double* __restrict__ part_a, const double* __restrict__ part_b, int n,
+                                    double count, pdg_ln_stat* __restrict__ out_a, pdg_ln_stat* __restrict__ out_b) {
+  if (blockIdx.x == 0)
+    ln_finalize_block(part_a, n, count, out_a);
+  else
+    ln_finalize_block(part_b, n, count, out_b);
+}
+
+extern "C" int pdg_ln_finalize2(const double* part_a, const double* part_b, int nparts, double count,
+                                pdg_ln_stat* out_a, pdg_ln_stat* out_b, void* stream) {
+  PDG_CHECK_ARG(nparts > 0 && count > 0, "pdg_ln_finalize2: empty");
+  PDG_CHECK_ARG(part_a && part_b && out_a && out_b && out_a != out_b, "pdg_ln_finalize2: bad pointers");
+  hipLaunchKernelGGL(ln_finalize2_kernel, dim3(2), dim3(256), 0, (hipStream_t)stream, part_a, part_b, nparts, count,
+                     out_a, out_b);
+  PDG_CHECK_LAUNCH("pdg_ln_finalize2");
+  return PDG_OK;
 }
 
 extern "C" int pdg_ln_finalize(const double* partials, int nparts, double count, pdg_ln_stat* out,

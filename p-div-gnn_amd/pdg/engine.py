@@ -206,9 +206,13 @@ class EPDEngine:
             self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
                     _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
                     _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
-            self._finalize(self._part_a, E * L, st[i_m], s, True)
-            if eu:
-                self._finalize(self._part_b, E * L, st[i_e], s, True)
+            if eu and self.sync is None:    # both edge LayerNorms in one launch
+                lib.pdg_ln_finalize2(self._part_a.data_ptr(), self._part_b.data_ptr(), self._nparts.value,
+                                     float(E * L), st[i_m], st[i_e], s)
+            else:
+                self._finalize(self._part_a, E * L, st[i_m], s, True)
+                if eu:
+                    self._finalize(self._part_b, E * L, st[i_e], s, True)
             # aggregation (models.py:215-217) and node_net (:240-243)
             aggr = self._empty(N, L)
             xs = self._empty(N, L) if need_grad else None
