@@ -95,6 +95,13 @@ int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const 
 int pdg_node_pq_rw(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                    const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
                    float* Q, void* stream);
+/* pdg_node_pq_rw with the node LayerNorm statistics of a2_prev folded in: every block reduces the
+ * (sum, sumsq) partials of pdg_node_net itself in the pdg_ln_finalize order (bit-identical) and
+ * block 0 stores them to st_out for the backward, replacing a separate pdg_ln_finalize launch.
+ * New in this build (the reference computes the statistics inline, models.py:42-55). */
+int pdg_node_pq_rw_fin(int n_nodes, const float* a2_prev, const double* partials, int nparts, double count,
+                       pdg_ln_stat* st_out, const float* ln_g, const float* ln_b, const float* x_res,
+                       float* x_out, const float* W1, float* P, float* Q, void* stream);
 
 /* Fused edge pass of one message-passing step (models.py:215-222, :233-238).
  * with_edge_update == 0 skips the edge-update branch (the last step's e_S is never consumed,

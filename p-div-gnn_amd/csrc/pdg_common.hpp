@@ -404,4 +404,30 @@ __device__ __forceinline__ void block_sum2(double& a, double& b, double* red) {
   }
 }
 
+// Graph-LayerNorm statistics from per-block (sum, sumsq) partials in the fixed pdg_ln_finalize
+// order: threads 0..255 accumulate strided by 256, waves beyond the fourth add +0, so any block of
+// >= 256 threads gives bit-identical statistics.  Thread 0 writes *out (global or LDS).
+__device__ __forceinline__ void ln_stat_from_partials(const double* __restrict__ part, int n, double count,
+                                                      pdg_ln_stat* out, double* red) {
+  double a = 0, b = 0;
+  if (threadIdx.x < 256)
+    for (int i = threadIdx.x; i < n; i += 256) { a += part[2 * i]; b += part[2 * i + 1]; }
+  block_sum2(a, b, red);
+  if (threadIdx.x == 0) {
+    const double mean = a / count;
+    double var = b / count - mean * mean;
+    if (var < 0) var = 0;
+    const double sd = sqrt(var);
+    pdg_ln_stat s;
+    s.mean = (float)mean;
+    s.std_ = (float)sd;
+    s.den = s.std_ + LN_EPS;
+    s.rstd = 1.0f / s.den;
+    s.mean_d = mean;
+    s.std_d = sd;
+    s.count = count;
+    *out = s;
+  }
+}
+
 }  // namespace pdg

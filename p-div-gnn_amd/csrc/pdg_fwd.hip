@@ -218,24 +218,7 @@ extern "C" int pdg_encoder_fwd(int rows, int in_features, const float* x_in, con
 __device__ __forceinline__ void ln_finalize_block(const double* __restrict__ part, int n, double count,
                                                   pdg_ln_stat* __restrict__ out) {
   __shared__ double red[2 * 16];
-  double a = 0, b = 0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) { a += part[2 * i]; b += part[2 * i + 1]; }
-  block_sum2(a, b, red);
-  if (threadIdx.x == 0) {
-    const double mean = a / count;
-    double var = b / count - mean * mean;
-    if (var < 0) var = 0;
-    const double sd = sqrt(var);
-    pdg_ln_stat s;
-    s.mean = (float)mean;
-    s.std_ = (float)sd;
-    s.den = s.std_ + LN_EPS;
-    s.rstd = 1.0f / s.den;
-    s.mean_d = mean;
-    s.std_d = sd;
-    s.count = count;
-    *out = s;
-  }
+  ln_stat_from_partials(part, n, count, out, red);
 }
 
 __global__ void ln_finalize_kernel(const double* __restrict__ part, int n, double count,

@@ -381,13 +381,21 @@ template <bool RES>
 __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
     int N, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ xres, float* __restrict__ xout,
-    const float* __restrict__ W1, float* __restrict__ P, float* __restrict__ Q) {
+    const float* __restrict__ W1, float* __restrict__ P, float* __restrict__ Q, const double* __restrict__ part,
+    int nparts, double count, pdg_ln_stat* __restrict__ st_out) {
   __shared__ __attribute__((aligned(16))) float xt[3 * TILE * GS];
+  __shared__ LNStat st_sh;
+  __shared__ double red_fin[2 * NU_THREADS / 64];
   const int w = wave_id(), l = lane_id();
   const bool loader = w >= NU_COMPUTE;
   const int ntiles = tiles_of(N);
   const int lt = threadIdx.x - 64 * NU_COMPUTE;
-  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  if (part) {   // the node LayerNorm statistics of the previous step, folded in (pdg_node_pq_rw_fin)
+    ln_stat_from_partials(part, nparts, count, &st_sh, red_fin);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_sh;
+  }
+  const LNStat st = part ? st_sh : *reinterpret_cast<const LNStat*>(stp);
   const int r = l & 15, q = l >> 4;
   const int oc = 16 * w + 4 * q;
   f32x4 waf[8], wbf[8];
@@ -439,9 +447,10 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
   }
 }
 
-extern "C" int pdg_node_pq_rw(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                              const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
-                              float* Q, void* stream) {
+static int node_pq_rw_launch(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                             const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
+                             float* Q, const double* part, int nparts, double count, pdg_ln_stat* st_out,
+                             void* stream) {
   PDG_CHECK_ARG(n_nodes > 0, "pdg_node_pq_rw: n_nodes must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(x_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) && PDG_ALIGNED(W1) &&
                     PDG_ALIGNED(ln_g) && PDG_ALIGNED(ln_b) && PDG_ALIGNED(x_res),
@@ -451,12 +460,30 @@ extern "C" int pdg_node_pq_rw(int n_nodes, const float* a2_prev, const pdg_ln_st
   const int grid = tiles < cap ? tiles : cap;
   if (x_res)
     hipLaunchKernelGGL(node_pq_rw_kernel<true>, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes,
-                       a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q);
+                       a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, part, nparts, count, st_out);
   else
     hipLaunchKernelGGL(node_pq_rw_kernel<false>, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes,
-                       a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q);
+                       a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, part, nparts, count, st_out);
   PDG_CHECK_LAUNCH("pdg_node_pq_rw");
   return PDG_OK;
+}
+
+extern "C" int pdg_node_pq_rw(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                              const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
+                              float* Q, void* stream) {
+  PDG_CHECK_ARG(st != nullptr, "pdg_node_pq_rw: st is null");
+  return node_pq_rw_launch(n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, nullptr, 0, 0.0, nullptr,
+                           stream);
+}
+
+extern "C" int pdg_node_pq_rw_fin(int n_nodes, const float* a2_prev, const double* partials, int nparts,
+                                  double count, pdg_ln_stat* st_out, const float* ln_g, const float* ln_b,
+                                  const float* x_res, float* x_out, const float* W1, float* P, float* Q,
+                                  void* stream) {
+  PDG_CHECK_ARG(partials && st_out && nparts > 0 && nparts < MAX_BLOCKS && count > 0,
+                "pdg_node_pq_rw_fin: bad statistics arguments");
+  return node_pq_rw_launch(n_nodes, a2_prev, nullptr, ln_g, ln_b, x_res, x_out, W1, P, Q, partials, nparts, count,
+                           st_out, stream);
 }
 
 // ============================================================================ summed transposed GEMMs

@@ -191,11 +191,18 @@ class EPDEngine:
         a2e_prev, ste_prev, ge_prev, be_prev = a2_ee, st[1], P["edge_encoder.4.weight"], P["edge_encoder.4.bias"]
         x_prev = e_prev = None
         Pm, Qm = self._empty(N, L), self._empty(N, L)
+        pend_n = None                        # deferred node LayerNorm statistics (nparts)
         for t in range(steps):
             i_m, i_e, i_n = 2 + 3 * t, 3 + 3 * t, 4 + 3 * t
             x_t = self._empty(N, L)
-            self._t("node_pq", lib.pdg_node_pq_rw, N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev),
-                    _p(x_prev), _p(x_t), _p(W1), _p(Pm), _p(Qm), s)
+            if pend_n is not None:    # the previous step's node statistics, reduced inside node_pq
+                self._t("node_pq", lib.pdg_node_pq_rw_fin, N, _p(a2n_prev), self._part_a.data_ptr(), pend_n,
+                        float(N * L), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_t), _p(W1), _p(Pm),
+                        _p(Qm), s)
+                pend_n = None
+            else:
+                self._t("node_pq", lib.pdg_node_pq_rw, N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev),
+                        _p(x_prev), _p(x_t), _p(W1), _p(Pm), _p(Qm), s)
             # the last step's edge update has no consumer (models.py:316 decodes nodes only)
             eu = t < steps - 1
             e_t = self._empty(E, L)
@@ -222,7 +229,10 @@ class EPDEngine:
             a2n = self._empty(N, L)
             self._t("node_net", lib.pdg_node_net, N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(Wn2), _p(bn2), _p(a1n),
                     _p(a2n), _p(self._part_a), np_, s)
-            self._finalize(self._part_a, N * L, st[i_n], s)
+            if t < steps - 1 and self.sync is None:
+                pend_n = self._nparts.value          # finalised by the next step's node_pq
+            else:
+                self._finalize(self._part_a, N * L, st[i_n], s)
             if need_grad:
                 ctx.per_step.append(dict(x=x_t, e=e_t, a1m=a1m, a2m=a2m, a1e=a1e, a2e=a2e, aggr=aggr, xs=xs,
                                          a1n=a1n, a2n=a2n, i_m=i_m, i_e=i_e, i_n=i_n, eu=eu))

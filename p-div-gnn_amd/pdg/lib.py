@@ -28,6 +28,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_encoder_fwd": [I, I, P, P, P, P, P, P, P, P, P, P],
     "pdg_ln_finalize": [P, I, c_double, P, P],
     "pdg_ln_finalize2": [P, P, I, c_double, P, P, P],
+    "pdg_node_pq_rw_fin": [I, P, P, I, c_double, P, P, P, P, P, P, P, P, P],
     "pdg_ln_partials_sum": [P, I, P, P],
     "pdg_ln_bwd_rescale": [P, P, P],
     "pdg_node_pq": [I, P, P, P, P, P, P, P, P, P, P],
