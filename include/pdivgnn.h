@@ -311,10 +311,17 @@ int pdg_div_bwd(int n_graphs, const int* ptr, int n_nodes, const int* at_rowptr,
 int pdg_transpose(int rows, int cols, int ld, const float* in, float* out, void* stream);
 /* *flag = 1 if any grad element is inf/NaN (GradScaler's skip test, gnn_train.py:205-207). */
 int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream);
-/* Adam (torch.optim.Adam, amsgrad=False, weight_decay=0) on a flat parameter buffer; a no-op
- * when skip_flag (nullable, device) is set. */
+/* Adam as torch.optim.Adam (amsgrad=False, weight_decay=0) stepped by GradScaler.step
+ * (gnn_train.py:111,118,204-207) on a flat parameter buffer.  Adam's step count lives on the
+ * device: step_count[parity] = optimizer steps taken so far (c); the update uses
+ * table[2c] = (float) lr / (1 - beta1^(c+1)) and table[2c+1] = (float) sqrt(1 - beta2^(c+1)), both
+ * computed in double on the host as torch does, and writes step_count[parity ^ 1] = c + !skip.
+ * When *skip_flag (nullable, device) is set nothing else changes: parameters, moments and the
+ * step count stay as they were (GradScaler skips optimizer.step()).  w1 = (float)(1 - beta1),
+ * w2 = (float)(1 - beta2) rounded from double.  Requires table_len > c. */
 int pdg_adam(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
-             float lr, float beta1, float beta2, float eps, int step, const int* skip_flag, void* stream);
+             const float* table, int table_len, float w1, float beta2, float w2, float eps,
+             const int* skip_flag, int* step_count, int parity, void* stream);
 
 /* ---------------------------------------------------------------- device-side collate (§8f row 1) */
 /* One copy job: dst[i] = src[i] (+ add for the integer kinds), i < count.  `src`/`dst` are

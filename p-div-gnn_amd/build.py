@@ -17,12 +17,14 @@ from pathlib import Path
 HERE = Path(__file__).resolve().parent
 CSRC = Path(os.environ.get("PDG_CSRC", HERE / "csrc"))
 # PDG_OUT / PDG_BUILD_DIR / PDG_EXTRA_FLAGS build side-by-side variants for A/B timing
-# (loaded with PDG_LIB=...); the default build is the shipped library.
-OUT = Path(os.environ.get("PDG_OUT", HERE / "pdg" / "libpdivgnn_hip.so"))
+# (loaded with PDG_LIB=...); the default build is the shipped library, and it is always built
+# from csrc/ with the default flags (extra flags are refused for it).
+SHIPPED = HERE / "pdg" / "libpdivgnn_hip.so"
+OUT = Path(os.environ.get("PDG_OUT", SHIPPED))
 BUILD = Path(os.environ.get("PDG_BUILD_DIR", HERE / "build"))
 ARCH = os.environ.get("PDG_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         *os.environ.get("PDG_EXTRA_FLAGS", "").split()]
+EXTRA = os.environ.get("PDG_EXTRA_FLAGS", "").split()
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", *EXTRA]
 
 
 def hipcc() -> str:
@@ -49,6 +51,10 @@ def _compile(src: Path, report: bool) -> Path:
 
 
 def build(force: bool = False, report: bool = False) -> Path:
+    if OUT.resolve() == SHIPPED.resolve() and (EXTRA or CSRC.resolve() != (HERE / "csrc").resolve()
+                                               or ARCH != "gfx950"):
+        raise RuntimeError("the shipped library is built from csrc/ for gfx950 with the default flags only; "
+                           "set PDG_OUT (and PDG_BUILD_DIR) to build an A/B variant")
     BUILD.mkdir(parents=True, exist_ok=True)
     OUT.parent.mkdir(parents=True, exist_ok=True)
     srcs = sorted(CSRC.glob("*.hip"))

@@ -159,10 +159,6 @@ __device__ __forceinline__ void bias_acc(Acc& acc, const FeatVec& b) {
 // each dependent chain has a 64-cycle spacing (> the 40-cycle MFMA latency).
 // Scheduling barriers keep the compiler from hoisting all 64 LDS reads.
 __device__ __forceinline__ void gemm128(Acc& acc, const float* __restrict__ wl, const float (&v)[FRAG]) {
-#ifdef PDG_DIAG_NOGEMM   // timing experiment only: results are wrong
-  acc.b[0][0] += v[0];
-  return;
-#endif
   const int l = lane_id();
   const float* base = wl + opaque((l & 15) * WPAD + 4 * (l >> 4));
   f32x4 a0[2], a1[2];
@@ -201,12 +197,7 @@ __device__ __forceinline__ void gemm128(Acc& acc, const float* __restrict__ wl, 
   }
 }
 
-// Timing experiments only (results are wrong): drop the W2 GEMMs of the edge kernels.
-#ifdef PDG_DIAG_NOW2
-#define PDG_GEMM_W2(acc, w, v) ((acc).b[0][0] += (v)[0])
-#else
 #define PDG_GEMM_W2(acc, w, v) gemm128(acc, w, v)
-#endif
 
 // ----------------------------------------------------------------------------- edge-kernel weights
 // The fused edge kernels hold two weights in LDS: Wc (or Wc^T) in fp32 and W2 (or W2^T) as
@@ -227,10 +218,6 @@ __device__ __forceinline__ void load_wblock_swz(float* __restrict__ lds, const f
 
 // gemm128 on the swizzled fp32 image (same MFMA order and pipelining, so the same results).
 __device__ __forceinline__ void gemm128_swz(Acc& acc, const float* __restrict__ wl, const float (&v)[FRAG]) {
-#ifdef PDG_DIAG_NOMFMA   // timing experiment only: results are wrong
-  acc.b[0][0] += v[0];
-  return;
-#endif
   const int l = lane_id(), i = l & 15, q = l >> 4;
   // chunk (4t + q) ^ i = 4 (t ^ (i >> 2)) + (q ^ (i & 3))
   const float* base = wl + opaque(i * 128 + 4 * (q ^ (i & 3)));
@@ -314,10 +301,6 @@ __device__ __forceinline__ void load_wplanes(unsigned char* __restrict__ planes,
 
 __device__ __forceinline__ void gemm128_x6(Acc& acc, const unsigned char* __restrict__ planes,
                                            const float (&v)[FRAG]) {
-#ifdef PDG_DIAG_NOMFMA
-  acc.b[0][0] += v[0];
-  return;
-#endif
   const int l = lane_id(), i = l & 15, q = l >> 4;
   // chunk (4m + q) ^ i = 4 (m ^ (i >> 2)) + (q ^ (i & 3))
   const unsigned char* base = planes + opaque(i * 256 + 16 * (q ^ (i & 3)));

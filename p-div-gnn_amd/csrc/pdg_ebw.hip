@@ -102,10 +102,6 @@ __device__ __forceinline__ f32x4 ln_relu_bwd4(const f32x4& gy, const f32x4& a2, 
 // slab += G^T X over the 32 staged rows (K = rows): wave w owns o in 32 (w & 3) + [0, 32),
 // i in 64 (w >> 2) + [0, 64) as two 32x32 accumulators (wgrad_x6_kernel's operand reads).
 __device__ __forceinline__ void wgrad_round(f32x16 (&acc)[2], const unsigned char* gimg, const unsigned char* ximg) {
-#ifdef PDG_DIAG_NOMFMA   // timing experiment only: results are wrong
-  acc[0][0] += (float)gimg[lane_id()] + (float)ximg[lane_id()];
-  return;
-#endif
   const int l = lane_id(), w = wave_id(), h = l >> 5;
   const int ob = 32 * (w & 3), ib = 64 * (w >> 2);
   const int lrow = 8 * h + ((l & 15) >> 2);
@@ -145,10 +141,6 @@ __device__ __forceinline__ void gemm_round(f32x4 (&d)[NI][2], const WSlice& ws, 
   for (int u = 0; u < NI; ++u)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) d[u][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#ifdef PDG_DIAG_NOMFMA
-  for (int u = 0; u < NI; ++u) d[u][0][0] = (float)img[u][lane_id()] + ws.a[0][0][0];
-  return;
-#endif
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll

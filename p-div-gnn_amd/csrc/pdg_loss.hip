@@ -210,7 +210,7 @@ extern "C" int pdg_transpose(int rows, int cols, int ld, const float* in, float*
   return PDG_OK;
 }
 
-// torch.optim.Adam single-tensor step (amsgrad=False, weight_decay=0, maximize=False).
+// GradScaler's skip test (gnn_train.py:205-207).
 __global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* __restrict__ flag) {
   int bad = 0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -232,31 +232,49 @@ extern "C" int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream)
   return PDG_OK;
 }
 
+// torch.optim.Adam._single_tensor_adam (amsgrad=False, weight_decay=0, maximize=False) driven by
+// GradScaler.step (gnn_train.py:111,118,204-207): a skipped step (non-finite gradient) leaves the
+// parameters, both moments AND Adam's step count untouched.  The step count therefore lives on the
+// device, double-buffered by call parity: the kernel reads count[parity] (optimizer steps taken so
+// far), uses table entry count[parity] (the host-computed float32 images of torch's double-precision
+// step_size = lr / (1 - beta1^t) and sqrt(1 - beta2^t) for t = count + 1) and block 0 writes
+// count[parity ^ 1] = count + (skipped ? 0 : 1).  No host sync, no extra launch.
 __global__ void adam_kernel(long n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, float lr, float b1, float b2, float eps, float bc1,
-                            float bc2_sqrt, const int* __restrict__ skip) {
-  if (skip && *skip) return;
+                            float* __restrict__ v, const float2* __restrict__ tab, float w1, float b2, float w2,
+                            float eps, const int* __restrict__ skip, int* __restrict__ count, int parity, int tab_len) {
+  const int c = count[parity];
+  const int sk = skip ? *skip : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) count[parity ^ 1] = c + (sk ? 0 : 1);
+  if (sk) return;
+  // {step_size, bias_correction2_sqrt} of step c + 1; the host keeps tab_len > its call count >= c
+  const float2 t = tab[c < tab_len ? c : tab_len - 1];
+  // Explicitly rounded operations in torch's CPU kernel order (no contraction beyond what it does):
+  //   lerp_vec:  fmadd(w1, g - m, m)                 (weight < 0.5)
+  //   mul_ then addcmul_: (v * b2) + ((w2 * g) * g)
+  //   denom:     sqrt(v) / bc2_sqrt + eps
+  //   addcdiv_:  p + ((-step_size) * m) / denom
+  const float nstep = -t.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float gi = g[i];
-    const float mi = m[i] + (1.0f - b1) * (gi - m[i]);        // exp_avg.lerp_(grad, 1 - beta1)
-    const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;        // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+    const float mi = __fmaf_rn(w1, __fsub_rn(gi, m[i]), m[i]);
+    const float vi = __fadd_rn(__fmul_rn(v[i], b2), __fmul_rn(__fmul_rn(w2, gi), gi));
     m[i] = mi;
     v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    p[i] = p[i] - (lr / bc1) * (mi / denom);
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), t.y), eps);
+    p[i] = __fadd_rn(p[i], __fdiv_rn(__fmul_rn(nstep, mi), denom));
   }
 }
 
-extern "C" int pdg_adam(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq, float lr,
-                        float beta1, float beta2, float eps, int step, const int* skip_flag, void* stream) {
-  PDG_CHECK_ARG(n >= 0 && step >= 1, "pdg_adam: bad args");
-  if (n == 0) return PDG_OK;
-  const double bc1 = 1.0 - pow((double)beta1, step);
-  const double bc2 = 1.0 - pow((double)beta2, step);
+extern "C" int pdg_adam(int64_t n, float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        const float* table, int table_len, float w1, float beta2, float w2, float eps,
+                        const int* skip_flag, int* step_count, int parity, void* stream) {
+  PDG_CHECK_ARG(n >= 0 && table != nullptr && table_len >= 1 && step_count != nullptr && (parity == 0 || parity == 1),
+                "pdg_adam: bad args");
   long blocks = (n + 255) / 256;
   if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;             // block 0 always advances the step count
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (long)n, param, grad,
-                     exp_avg, exp_avg_sq, lr, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2), skip_flag);
+                     exp_avg, exp_avg_sq, (const float2*)table, w1, beta2, w2, eps, skip_flag, step_count, parity, table_len);
   PDG_CHECK_LAUNCH("pdg_adam");
   return PDG_OK;
 }

@@ -204,8 +204,13 @@ class EncodeProcessDecode(StressFieldBaseModel):
     def stats_tensor(self, device) -> torch.Tensor:
         vals = []
         for k in _STAT_ORDER:
-            v = getattr(self, k)
-            vals.append(torch.as_tensor(v, dtype=torch.float32).reshape(-1)[:1].to(device))
+            v = torch.as_tensor(getattr(self, k), dtype=torch.float32)
+            if v.numel() != 1:
+                # the reference's datasets compute scalar statistics (datasets.py:283-291); the HIP
+                # input formatting takes one scalar per statistic, never a silently truncated vector
+                raise ValueError(f"{k} must be a scalar (got {tuple(v.shape)}); per-axis statistics are "
+                                 "not supported by the HIP path")
+            vals.append(v.reshape(1).to(device))
         return torch.cat(vals).contiguous()
 
     def forward(self, mesh_graph, scale_output: bool = True, scale_input: bool = True):
@@ -235,6 +240,12 @@ class EncodeProcessDecode(StressFieldBaseModel):
                                                  self.message_passing_steps, bool(scale_input),
                                                  bool(scale_output), False)
             return Data(local_stress=y, edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)
+        if torch.is_grad_enabled() and any(t.requires_grad for t in (mesh_graph.pos, mesh_graph.mean_stress,
+                                                                      mesh_graph.edge_attr)):
+            # the reference never differentiates w.r.t. the mesh inputs (gnn_train.py:159-205); the
+            # HIP backward produces parameter gradients only, so refuse rather than return None
+            raise NotImplementedError("EncodeProcessDecode (HIP path): gradients w.r.t. pos / mean_stress / "
+                                      "edge_attr are not supported; detach the inputs")
         y = _EPDFunction.apply(self, plan, self.stats_tensor(dev), bool(scale_output), bool(scale_input), pos, ms,
                                types, ea, *params)
         return Data(local_stress=y, edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)

@@ -66,7 +66,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_transpose": [I, I, I, P, P, P],
     "pdg_nonfinite": [P, c_int64, P, P],
     "pdg_collate": [P, I, ctypes.c_long, P],
-    "pdg_adam": [c_int64, P, P, P, P, c_float, c_float, c_float, c_float, I, P, P],
+    "pdg_adam": [c_int64, P, P, P, P, P, I, c_float, c_float, c_float, c_float, P, P, I, P],
 }
 _RESTYPES = {"pdg_last_error": ctypes.c_char_p, "pdg_mesh_graph_scratch_bytes": ctypes.c_long}
 

@@ -18,7 +18,11 @@ with the same *input format* the hot path consumes:
   are d/dx, next N are d/dy), the role of ``op_div_matrix``
   (``datasets.py:191-213``);  A is an *input* of the loss, so its exact FEM
   weights do not matter for parity;
-* a smooth synthetic target ``local_stress`` around a random mean stress.
+* a smooth synthetic target ``local_stress`` around a random mean stress;  with
+  ``strain_range`` (BASELINE config 4, the hyperelastic dataset: imposed mean strains in
+  ±0.15, ``scripts/generate_dataset_hyperelast.py:631``) the mean stress comes from a
+  stiffening (non-linear) response to a random mean strain and the concentration field
+  grows with the strain.  Targets only enter the loss, never the cost of a step.
 """
 from __future__ import annotations
 
@@ -160,7 +164,7 @@ def p1_divergence_operator(pos: np.ndarray, faces: np.ndarray):
 
 def hole_plate(n: int = 71, hole_radius: float = 0.0, length: float = 100.0,
                jitter: float = 0.15, periodic: bool = True, seed: int = 69,
-               stress_scale: float = 100.0) -> MeshSample:
+               stress_scale: float = 100.0, strain_range: tuple[float, float] | None = None) -> MeshSample:
     """One synthetic sample.  ``hole_radius`` is a fraction of ``length``."""
     rng = np.random.default_rng(seed)
     h = length / (n - 1)
@@ -205,6 +209,12 @@ def hole_plate(n: int = 71, hole_radius: float = 0.0, length: float = 100.0,
     rows, cols, vals = p1_divergence_operator(pos, faces)
 
     mean = (rng.uniform(-1.0, 1.0, size=3) * stress_scale).astype(np.float32)
+    stiffen = 0.0
+    if strain_range is not None:
+        # hyperelastic-like targets: stiffening response sigma = k eps (1 + 4 |eps|) to a mean strain
+        eps = rng.uniform(strain_range[0], strain_range[1], size=3)
+        mean = (10.0 * stress_scale * eps * (1.0 + 4.0 * np.abs(eps))).astype(np.float32)
+        stiffen = 4.0 * float(np.abs(eps).max())
     center = np.array([length / 2, length / 2])
     rel = pos.astype(np.float64) - center
     rr = np.maximum(np.linalg.norm(rel, axis=1), 1e-6)
@@ -216,19 +226,44 @@ def hole_plate(n: int = 71, hole_radius: float = 0.0, length: float = 100.0,
     sxx = mean[0] * (1 + f * np.cos(2 * th)) + 0.5 * mean[2] * f * np.sin(2 * th) + amp * wave
     syy = mean[1] * (1 - f * np.cos(2 * th)) - 0.5 * mean[2] * f * np.sin(2 * th) - amp * wave
     sxy = mean[2] * (1 + f) + 0.25 * (mean[0] - mean[1]) * f * np.sin(2 * th) + 0.5 * amp * wave
-    local = np.stack([sxx, syy, sxy], 1).astype(np.float32)
+    local = np.stack([sxx, syy, sxy], 1)
+    if stiffen:
+        local = local * (1.0 + stiffen * f)[:, None]
+    local = local.astype(np.float32)
     return MeshSample(pos=pos, faces=faces, node_types=node_types, edge_index=edge_index,
                       edge_attr=edge_attr, op_div_rows=rows, op_div_cols=cols,
                       op_div_vals=vals, mean_stress=mean, local_stress=local)
 
 
-def make_dataset(num_graphs: int, n: int = 71, hole_radius: tuple[float, float] = (0.0, 0.0),
-                 periodic: bool = True, seed: int = 69, jitter: float = 0.15) -> list[MeshSample]:
-    """``num_graphs`` samples; hole radius drawn uniformly from ``hole_radius``."""
+def dataset_specs(num_graphs: int, hole_radius: tuple[float, float] = (0.0, 0.0),
+                  seed: int = 69) -> list[tuple[float, int]]:
+    """(hole radius, sample seed) of each graph ``make_dataset`` builds, without building it."""
     rng = np.random.default_rng(seed)
     out = []
-    for g in range(num_graphs):
+    for _ in range(num_graphs):
         r = float(rng.uniform(*hole_radius)) if hole_radius[1] > 0 else 0.0
-        out.append(hole_plate(n=n, hole_radius=r, periodic=periodic,
-                              seed=int(rng.integers(0, 2**31 - 1)), jitter=jitter))
+        out.append((r, int(rng.integers(0, 2**31 - 1))))
     return out
+
+
+def hole_plate_node_count(n: int, hole_radius: float, length: float = 100.0) -> int:
+    """Node count of ``hole_plate(n, hole_radius)`` (geometry only: cheap, for sharding)."""
+    h = length / (n - 1)
+    gi, gj = np.meshgrid(np.arange(n), np.arange(n), indexing="xy")
+    pos = np.stack([gi.ravel() * h, gj.ravel() * h], 1)
+    faces = _grid_triangles(n)
+    if hole_radius > 0:
+        r = np.linalg.norm(pos - np.array([length / 2, length / 2]), axis=1)
+        faces = faces[~(r < hole_radius * length)[faces].any(1)]
+    return int(np.unique(faces.ravel()).size)
+
+
+def make_dataset(num_graphs: int, n: int = 71, hole_radius: tuple[float, float] = (0.0, 0.0),
+                 periodic: bool = True, seed: int = 69, jitter: float = 0.15,
+                 strain_range: tuple[float, float] | None = None, indices=None) -> list[MeshSample]:
+    """``num_graphs`` samples; hole radius drawn uniformly from ``hole_radius``.  ``indices``
+    builds only those graphs of the dataset (a data-parallel shard), identical to the full build's."""
+    specs = dataset_specs(num_graphs, hole_radius, seed)
+    idx = range(num_graphs) if indices is None else indices
+    return [hole_plate(n=n, hole_radius=specs[i][0], periodic=periodic, seed=specs[i][1], jitter=jitter,
+                       strain_range=strain_range) for i in idx]

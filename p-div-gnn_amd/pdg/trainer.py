@@ -11,7 +11,12 @@ Per step (one minibatch already resident in HBM):
            all-reduces its (sum, sumsq) pair in the forward and its (S1, S2) pair in the
            backward, the loss is divided by the GLOBAL number of graphs and the gradient
            bucket is summed, not averaged (2 x 47 sixteen-byte collectives more per step).
-  update   Adam(lr, betas=(0.9, 0.999), eps=1e-8) on the flat parameter buffer (:118, :206)
+  update   Adam(lr, betas=(0.9, 0.999), eps=1e-8) on the flat parameter buffer (:118, :206),
+           stepped as GradScaler.step does it (:204-207): a step whose gradient holds an inf/NaN
+           leaves parameters, moments and Adam's step count unchanged.  The step count lives
+           on the device (no per-step host sync); state_dict()/load_state_dict() speak
+           torch.optim.Adam's format so checkpoints round-trip with the reference's
+           save_model_checkpoint / load_optimizer_checkpoint (models.py:44-95).
 
 Parameters and gradients live in one flat buffer each (the model's Parameters
 are views into it), so the all-reduce is a single 669 KB collective and Adam a
@@ -22,8 +27,7 @@ non-finite; the same skip is applied here.
 capture=True records forward, loss and backward of a batch once in a HIP graph
 (torch.cuda.CUDAGraph = hipGraph on ROCm) and replays it on later steps with the
 same batch object: ~250 kernel launches per step become one graph launch.  The
-all-reduce, the non-finite check and Adam (whose bias correction depends on the
-host step count) stay eager.  Replays run the same kernels on the same buffers,
+all-reduce, the non-finite check and Adam stay eager.  Replays run the same kernels on the same buffers,
 so the results are bit-identical to eager steps (tests/test_gpu_trainer_graph.py).
 """
 from __future__ import annotations
@@ -69,9 +73,14 @@ class Trainer:
                 self.P[name] = view
                 self.G[name] = self.flat_g[off:off + n].view(shape)
                 off += n
-        self.step_count = 0
         self._gt_cache: dict = {}
         self._skip = torch.zeros(1, dtype=torch.int32, device=dev)
+        # Adam's step count on the device, double-buffered by call parity (pdg_adam), and the
+        # host's bound on it (optimizer calls since the count was last set)
+        self._count = torch.zeros(2, dtype=torch.int32, device=dev)
+        self._calls = 0
+        self._count_bound = 0
+        self._table = None
         # captured forward+backward per batch object (dp_mode="sync" reads counts on the host: eager)
         self.capture = capture and not self.sync
         self._graph = None            # (id(batch), torch.cuda.CUDAGraph, static outputs)
@@ -172,14 +181,91 @@ class Trainer:
                     out["div"] = parts[1]
             else:
                 self.flat_g.mul_(1.0 / torch.distributed.get_world_size(self.pg))
-        self.step_count += 1
+        self._ensure_table(self._count_bound + 1)
         lib.pdg_nonfinite(self.flat_g.data_ptr(), self.flat_g.numel(), self._skip.data_ptr(), s)
         lib.pdg_adam(self.flat_p.numel(), self.flat_p.data_ptr(), self.flat_g.data_ptr(), self.exp_avg.data_ptr(),
-                     self.exp_avg_sq.data_ptr(), self.lr, self.betas[0], self.betas[1], self.eps, self.step_count,
-                     self._skip.data_ptr(), s)
+                     self.exp_avg_sq.data_ptr(), self._table.data_ptr(), self._table.shape[0],
+                     float(1.0 - self.betas[0]), self.betas[1], float(1.0 - self.betas[1]), self.eps,
+                     self._skip.data_ptr(), self._count.data_ptr(), self._calls & 1, s)
+        self._calls += 1
+        self._count_bound += 1
         out["skipped"] = self._skip
         out["total"] = out["nmse"] + out.get("div", 0.0)
         return out
+
+
+    # ------------------------------------------------------------------ optimizer state
+    def _ensure_table(self, need: int) -> None:
+        """Bias-correction table of torch.optim.Adam (_single_tensor_adam, capturable=False): entry
+        t-1 = (lr / (1 - beta1**t), (1 - beta2**t) ** 0.5) in Python double, stored as float32 (the
+        precision the elementwise ops apply them in).  Grown by doubling, never per step."""
+        if self._table is not None and self._table.shape[0] >= need:
+            return
+        n = max(64, 2 * need)
+        b1, b2 = self.betas
+        rows = []
+        for t in range(1, n + 1):
+            step = float(t)
+            rows.append((self.lr / (1 - b1 ** step), (1 - b2 ** step) ** 0.5))
+        self._table = torch.tensor(rows, dtype=torch.float32).to(self.device)
+
+    @property
+    def step_count(self) -> int:
+        """Adam steps taken (skipped steps excluded); reads the device counter (one sync)."""
+        return int(self._count[self._calls & 1])
+
+    def _param_views(self) -> list:
+        """(name, offset, numel, shape) of every parameter in model.parameters() order (the index
+        order of torch.optim.Adam's state_dict)."""
+        offs, off = {}, 0
+        for name, shape in PARAM_SHAPES:
+            n = int(torch.Size(shape).numel())
+            offs[name] = (off, n, shape)
+            off += n
+        return [(name, *offs[name]) for name, _ in self.model.named_parameters()]
+
+    def state_dict(self) -> dict:
+        """torch.optim.Adam(model.parameters()).state_dict() equivalent (what the reference saves
+        as optimizer_state_dict, models.py:50-62)."""
+        sd = torch.optim.Adam(self.model.parameters(), lr=self.lr, betas=self.betas, eps=self.eps).state_dict()
+        steps = self.step_count
+        if steps > 0:
+            for i, (_, o, n, shape) in enumerate(self._param_views()):
+                sd["state"][i] = {"step": torch.tensor(float(steps)),
+                                  "exp_avg": self.exp_avg[o:o + n].view(shape).clone(),
+                                  "exp_avg_sq": self.exp_avg_sq[o:o + n].view(shape).clone()}
+        return sd
+
+    def load_state_dict(self, sd: dict) -> None:
+        """Resume from a torch.optim.Adam state_dict (load_optimizer_checkpoint, models.py:89-95)."""
+        groups = sd["param_groups"]
+        if len(groups) != 1:
+            raise ValueError("expected one Adam param group")
+        g = groups[0]
+        if g.get("amsgrad") or g.get("weight_decay", 0) or g.get("maximize"):
+            raise ValueError("only plain Adam (amsgrad=False, weight_decay=0, maximize=False) is supported")
+        self.lr, self.betas, self.eps = float(g["lr"]), tuple(float(b) for b in g["betas"]), float(g["eps"])
+        self._table = None
+        views = self._param_views()
+        if len(g["params"]) != len(views):
+            raise ValueError("parameter count mismatch")
+        steps = set()
+        with torch.no_grad():
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            for pid, (_, o, n, _) in zip(g["params"], views):
+                st = sd["state"].get(pid)
+                if not st:
+                    steps.add(0)
+                    continue
+                self.exp_avg[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(st["step"])))
+        if len(steps) != 1:
+            raise ValueError(f"parameters at different Adam steps: {sorted(steps)}")
+        c = steps.pop()
+        self._count.fill_(c)
+        self._count_bound = c
 
 
 def param_names() -> list:

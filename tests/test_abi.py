@@ -78,3 +78,16 @@ def test_model_refuses_cpu_tensors():
         m(b)
     with pytest.raises(ValueError):
         EncodeProcessDecode(1, 2, latent_size=64, input_nodes_features_size=6, output_nodes_features_size=3)
+
+
+def test_vector_statistics_are_refused():
+    """Per-axis statistics would be truncated to their first element by the scalar input
+    formatting; the model refuses them (advisor round 1)."""
+    import torch
+    from gnn_local_stress.models import EncodeProcessDecode
+    m = EncodeProcessDecode(1, 2, latent_size=128, input_nodes_features_size=6, output_nodes_features_size=3,
+                            mean_pos=torch.tensor([1.0, 2.0]), std_pos=torch.tensor(3.0))
+    with pytest.raises(ValueError, match="mean_pos"):
+        m.stats_tensor("cpu")
+    m.mean_pos = torch.tensor(1.5)
+    assert m.stats_tensor("cpu")[0] == 1.5

@@ -96,23 +96,28 @@ def test_per_graph_losses_match_oracle():
         losses.compute_divergence(pred[:5], g["op_divs"][0].cuda(), batch.nodes_types[:5], reduce_strategy="cube")
 
 
-def _oracle_grads(model_params, stats, batch, steps, dtype, divergence, penalty):
+def _oracle_grads(model_params, stats, batch, steps, dtype, divergence, penalty, scale_output=False):
     from oracle import epd_oracle as O
     P = {k: v.detach().cpu().to(dtype).clone().requires_grad_(True) for k, v in model_params.items()}
     st = {k: torch.as_tensor(v).cpu().to(dtype) for k, v in stats.items()}
     b = batch
     args = (b.pos.cpu().to(dtype), b.mean_stress.cpu().to(dtype), b.nodes_types.cpu(), b.edge_index.cpu(),
             b.edge_attr.cpu().to(dtype))
-    pred = O.epd_forward(P, st, *args, steps, scale_output=False)
+    pred = O.epd_forward(P, st, *args, steps, scale_output=scale_output)
     gt = (b.local_stress.cpu().to(dtype) - st["mean_local_stress"]) / st["std_local_stress"]
+    if scale_output:    # loss on the unscaled field: exercises the d(unscale)/dy = std factor
+        gt = b.local_stress.cpu().to(dtype)
     ops = [d.op_div_matrix.to(dtype) for d in b._data_list]
     total, nmse, div = O.batch_loss(pred, gt, b.ptr, ops, b.nodes_types.cpu(), divergence, penalty)
     total.backward()
     return pred.detach(), float(total), {k: v.grad for k, v in P.items()}
 
 
-@pytest.mark.parametrize("nmesh,ngraph,steps,divergence", [(21, 2, 10, True), (31, 1, 4, False)])
-def test_training_step_matches_oracle_fp32_and_fp64(nmesh, ngraph, steps, divergence):
+@pytest.mark.parametrize("nmesh,ngraph,steps,divergence,scale_output",
+                         [(21, 2, 10, True, False), (31, 1, 4, False, False), (17, 3, 3, True, True)])
+def test_training_step_matches_oracle_fp32_and_fp64(nmesh, ngraph, steps, divergence, scale_output):
+    """(17, 3, 3, True, True): backward through the output unscaling (models.py:318-321,
+    y * std_local_stress + mean_local_stress) with the loss on the physical field."""
     from gnn_local_stress import losses
     from pdg import meshgen
     samples = meshgen.make_dataset(ngraph, n=nmesh, hole_radius=(0.15, 0.3), seed=5)
@@ -120,13 +125,15 @@ def test_training_step_matches_oracle_fp32_and_fp64(nmesh, ngraph, steps, diverg
     stats = {k: float(v) for k, v in dataset_stats(batch).items()}
     model = _model(steps, stats)
     params = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    pred = model(batch, scale_output=False).local_stress
+    pred = model(batch, scale_output=scale_output).local_stress
     gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
+    if scale_output:
+        gt = batch.local_stress
     total, _, _ = losses.batch_loss(pred, batch, gt, divergence=divergence, divergence_penalty=10.0)
     model.zero_grad()
     total.backward()
-    p32, t32, g32 = _oracle_grads(params, stats, batch, steps, torch.float32, divergence, 10.0)
-    p64, t64, g64 = _oracle_grads(params, stats, batch, steps, torch.float64, divergence, 10.0)
+    p32, t32, g32 = _oracle_grads(params, stats, batch, steps, torch.float32, divergence, 10.0, scale_output)
+    p64, t64, g64 = _oracle_grads(params, stats, batch, steps, torch.float64, divergence, 10.0, scale_output)
     floor = rel(p32, p64)
     assert rel(pred.detach(), p32) < OUT_TOL, (rel(pred.detach(), p32), floor)
     assert rel(pred.detach(), p64) < OUT_TOL
@@ -134,6 +141,19 @@ def test_training_step_matches_oracle_fp32_and_fp64(nmesh, ngraph, steps, diverg
     for name, p in model.named_parameters():
         ref32 = rel(g32[name], g64[name])
         assert rel(p.grad, g64[name]) <= max(GRAD_TOL, 2 * ref32), (name, rel(p.grad, g64[name]), ref32)
+
+
+def test_input_gradients_are_refused():
+    """Gradients w.r.t. the mesh inputs are not produced by the HIP backward: asking for them
+    raises instead of silently returning None."""
+    from pdg import meshgen
+    batch = make_batch([meshgen.hole_plate(9, seed=2)])
+    model = _model(2, {k: float(v) for k, v in dataset_stats(batch).items()})
+    batch.pos = batch.pos.clone().requires_grad_(True)
+    with pytest.raises(NotImplementedError, match="pos"):
+        model(batch)
+    with torch.no_grad():                 # inference never needs them
+        assert model(batch).local_stress.shape == (batch.num_nodes, 3)
 
 
 def test_zero_mean_stress_guard_returns_zeros():

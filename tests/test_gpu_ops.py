@@ -402,3 +402,38 @@ def test_register_weight_kernels_match_lds_kernels(env, N, res):
                   out.data_ptr(), s) == 0
         o.append(out)
     assert torch.equal(o[0], o[1])
+
+
+@pytest.mark.parametrize("N,nparts,res", [(7, 1, True), (1031, 37, False), (40328, 256, True), (5000, 700, False)])
+def test_node_pq_rw_fin_equals_finalize_then_pq_rw(env, N, nparts, res):
+    """pdg_node_pq_rw_fin (node LayerNorm statistics reduced inside the consumer) is bitwise
+    pdg_ln_finalize + pdg_node_pq_rw: x_out, P, Q and the 40-byte pdg_ln_stat it stores, for
+    nparts below, at and above one 256-thread reduction round (advisor round 1)."""
+    lib, sh, _ = env
+    s = sh()
+    a2 = torch.relu(rnd(N, L))
+    xr = rnd(N, L) if res else None
+    g, b = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
+    W1, _ = lin(L, 3 * L)
+    # partials as pdg_node_net writes them: (sum, sumsq) per block, here of row slices of a2
+    edges = torch.linspace(0, N, nparts + 1).round().long().tolist()
+    a64 = a2.double()
+    part = torch.stack([torch.stack([a64[i:j].sum(), a64[i:j].square().sum()])
+                        for i, j in zip(edges[:-1], edges[1:])]).reshape(-1).cuda()
+    st_ref = finalize(lib, s, part, nparts, N * L)
+    outs = []
+    x, P, Q = (torch.empty(N, L, device="cuda") for _ in range(3))
+    assert lib.pdg_node_pq_rw(N, a2.data_ptr(), st_ref.data_ptr(), g.data_ptr(), b.data_ptr(),
+                              xr.data_ptr() if res else None, x.data_ptr(), W1.data_ptr(), P.data_ptr(),
+                              Q.data_ptr(), s) == 0
+    outs.append((x, P, Q))
+    st_fin = torch.full((40,), 0xAB, dtype=torch.uint8, device="cuda")
+    x, P, Q = (torch.empty(N, L, device="cuda") for _ in range(3))
+    assert lib.pdg_node_pq_rw_fin(N, a2.data_ptr(), part.data_ptr(), nparts, float(N * L), st_fin.data_ptr(),
+                                  g.data_ptr(), b.data_ptr(), xr.data_ptr() if res else None, x.data_ptr(),
+                                  W1.data_ptr(), P.data_ptr(), Q.data_ptr(), s) == 0
+    outs.append((x, P, Q))
+    torch.cuda.synchronize()
+    assert torch.equal(st_ref, st_fin)
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
