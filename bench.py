@@ -4,27 +4,41 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-A step is one full training step of the reference's hot loop
-(scripts/gnn_train.py:154-207) on one minibatch resident in HBM: forward of
-EncodeProcessDecode (10 message-passing steps, latent 128), per-graph NMSE
-(+ lambda * divergence for config 3), backward, RCCL all-reduce of the flat
-gradient bucket (N > 1) and the Adam update — all on the HIP kernels of
-libpdivgnn_hip.so.  Workload per GPU (weak scaling, graph-level data
-parallelism): BASELINE.json configs[1] = 8 synthetic periodic triangulated
-71x71 meshes (5,041 nodes, 29,968 edges each).  value = nodes processed by all
-ranks / max-over-ranks wall time.  --config 5 times inference instead (one
-forward of a 100k-node mesh, 15 layers, model.forward under no_grad as
-gnn_inference.py calls it; metric mesh-nodes/sec (inference)).
+One process per GPU.  Launched without a torch.distributed launcher (no WORLD_SIZE in the
+environment), ``--gpus N`` > 1 spawns the N ranks itself (torch.multiprocessing "spawn",
+before anything touches the GPU); under torchrun the launcher's ranks are used and must
+number ``--gpus``.  Ranks talk over RCCL (torch.distributed backend "nccl").
 
-Also reported: the roofline of the dominant kernel (HIP events around its
-launches inside the timed region) and the reference algorithm's CPU path (the
-op-for-op oracle restatement) timed on this host's cores.
+A step is one full training step of the reference's hot loop (scripts/gnn_train.py:154-207)
+on one minibatch resident in HBM: forward of EncodeProcessDecode (10 message-passing steps,
+latent 128), per-graph NMSE (+ lambda * divergence), backward, RCCL all-reduce of the flat
+gradient bucket (N > 1), the non-finite check and the Adam update — all on the HIP kernels of
+libpdivgnn_hip.so.
+
+Main line (the driver's metric): BASELINE.json configs[1] = 8 synthetic periodic triangulated
+71x71 meshes (5,041 nodes, 29,968 edges each) PER GPU (weak scaling, graph-level DP).
+value = nodes processed by all ranks / max-over-ranks wall time of the K timed steps.
+
+Sub-results in the same JSON line ("sub_results"; skipped with --no-extras), each timed the
+same way (barrier + synchronize on both sides, max over ranks):
+  config3  P-DivGNN with the divergence loss, 32 x 5,041-node meshes per GPU (weak)
+  config4  hyperelastic-style hole plates, FIXED global batch of 64 graphs sharded over the
+           ranks by pdg.dist.shard_graphs (64/32/16/8 per GPU at N = 1/2/4/8: strong scaling)
+  config5  inference, one 100,489-node mesh per GPU, 15 MP layers (N independent replicas)
+
+Also reported: the roofline of the dominant kernel (HIP events around its launches inside the
+timed region) and the reference algorithm's CPU path (the op-for-op oracle restatement) timed
+on this host's cores (rank 0, N = 1 only).  --plumbing runs the launch / rendezvous / timing /
+reporting flow with a gradient-bucket all-reduce as the only work (CPU tests with gloo); its
+line says so and carries no throughput claim.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import statistics
 import sys
 import time
 from pathlib import Path
@@ -45,22 +59,39 @@ PEAK_BF16_MFMA = 16 * PEAK_FP32_MFMA   # dense bf16 MFMA (2.5 PF; the fp32 rate 
 X6 = 6                      # bf16x6: six bf16 products per fp32-accurate product
 PEAK_HBM = 8.0e12           # MI355X HBM3E spec bandwidth (same guide; 6.3 TB/s measured copy)
 L = 128
+N_PARAMS = 167_299
 
 CONFIGS = {
     2: dict(workload="P-GNN linear-elastic, 8 x 5,041-node periodic meshes per GPU, fwd+bwd (BASELINE configs[1])",
             graphs=8, n=71, hole=(0.0, 0.0), divergence=False, steps=10),
-    3: dict(workload="P-DivGNN with divergence loss (lambda=10), 32 x 5,041-node periodic meshes per GPU",
+    3: dict(workload="P-DivGNN with divergence loss (lambda=10), 32 x 5,041-node periodic meshes per GPU "
+                     "(BASELINE configs[2])",
             graphs=32, n=71, hole=(0.0, 0.0), divergence=True, steps=10),
-    4: dict(workload="P-DivGNN hole plates, 8 x ~4.8k-node meshes per GPU (global batch 8*N)",
-            graphs=8, n=71, hole=(0.08, 0.12), divergence=True, steps=10),
+    4: dict(workload="P-DivGNN hyperelastic-style hole plates (strain range +-0.15), fixed global batch of 64 "
+                     "~4.8k-node periodic meshes sharded over the ranks (BASELINE configs[3])",
+            graphs=64, n=71, hole=(0.08, 0.12), divergence=True, steps=10, strain=(-0.15, 0.15), global_batch=True),
     5: dict(workload="inference, one synthetic 100,489-node periodic mesh per GPU, 15 MP layers (BASELINE configs[4])",
             graphs=1, n=317, hole=(0.0, 0.0), divergence=False, steps=15, inference=True),
 }
 
 
-def build_batch(cfg, seed, device):
+# ---------------------------------------------------------------------------------- workload
+def shard_indices(cfg, rank: int, world: int) -> list[int]:
+    """Graph indices this rank builds: the whole per-GPU batch (weak scaling), or its share of
+    the fixed global batch (strong scaling), balanced by node count (pdg.dist.shard_graphs)."""
+    from pdg import meshgen
+    from pdg.dist import shard_graphs
+    if not cfg.get("global_batch"):
+        return list(range(cfg["graphs"]))
+    specs = meshgen.dataset_specs(cfg["graphs"], cfg["hole"], seed=69)
+    counts = [meshgen.hole_plate_node_count(cfg["n"], r) for r, _ in specs]
+    return shard_graphs(counts, world)[rank]
+
+
+def build_batch(cfg, seed, device, indices=None):
     from pdg import graph, meshgen
-    samples = meshgen.make_dataset(cfg["graphs"], n=cfg["n"], hole_radius=cfg["hole"], seed=seed)
+    samples = meshgen.make_dataset(cfg["graphs"], n=cfg["n"], hole_radius=cfg["hole"], seed=seed,
+                                   strain_range=cfg.get("strain"), indices=indices)
     datas = [graph.sample_to_data(s) for s in samples]
     return graph.Batch.from_data_list(datas).to(device), samples
 
@@ -72,151 +103,91 @@ def dataset_stats(b):
             "std_edge_weight": b.edge_attr.std()}
 
 
-def cpu_baseline(cfg, samples, seconds: float = 20.0):
-    """The reference algorithm on this host's CPU cores: oracle/epd_oracle.py (the op-for-op
-    restatement of models.py + gnn_train.py losses, validated against the reference's own
-    outputs in tests/golden), fp32, one graph of the workload per step."""
+# ---------------------------------------------------------------------------------- CPU baseline
+def _cpu_model_name() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _oracle_step_fn(cfg, samples):
+    """One step of the reference algorithm (oracle/epd_oracle.py, the op-for-op restatement of
+    models.py + gnn_train.py losses, validated against the reference's own outputs in
+    tests/golden) on a batch of `samples`, fp32, torch CPU."""
     from oracle import epd_oracle as O
     from pdg import graph
-    threads = max(1, min(16, os.cpu_count() or 1))
-    torch.set_num_threads(threads)
-    d = graph.sample_to_data(samples[0])
-    b = graph.Batch.from_data_list([d])
+    datas = [graph.sample_to_data(s) for s in samples]
+    b = graph.Batch.from_data_list(datas)
     st = {k: v.float() for k, v in dataset_stats(b).items()}
     P = {k: v.requires_grad_(True) for k, v in O.init_params().items()}
     args = (b.pos, b.mean_stress, b.nodes_types, b.edge_index, b.edge_attr)
     gt = (b.local_stress - st["mean_local_stress"]) / st["std_local_stress"]
-
-    infer = cfg.get("inference", False)
+    ops = [d.op_div_matrix for d in datas]
 
     def step():
-        if infer:
+        if cfg.get("inference"):
             with torch.no_grad():
                 O.epd_forward(P, st, *args, cfg["steps"], scale_output=True)
             return
         pred = O.epd_forward(P, st, *args, cfg["steps"], scale_output=False)
-        total, _, _ = O.batch_loss(pred, gt, b.ptr, [d.op_div_matrix], b.nodes_types, cfg["divergence"], 10.0)
+        total, _, _ = O.batch_loss(pred, gt, b.ptr, ops, b.nodes_types, cfg["divergence"], 10.0)
         for p in P.values():
             p.grad = None
         total.backward()
+    return step, b.num_nodes
 
-    step()  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
+
+def _median_rate(step, nodes, reps):
+    step()                                       # warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
         step()
-        n += 1
-        el = time.perf_counter() - t0
-        if el > seconds or n >= 50:
-            break
-    what = "inference forwards" if infer else f"training steps (fwd+NMSE{'+div' if cfg['divergence'] else ''}+bwd)"
-    return {"value": round(n * d.num_nodes / el, 1), "unit": "nodes/s", "cores": threads, "kind": "port",
-            "sample": f"{n} {what} of one {d.num_nodes}-node graph, {cfg['steps']} MP steps, fp32, torch CPU "
-                      f"({threads} threads), oracle/epd_oracle.py"}
+        ts.append(time.perf_counter() - t0)
+    return nodes / statistics.median(ts), ts
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
-    ap.add_argument("--dp-mode", default="replica", choices=["replica", "sync"])
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--graph", action="store_true",
-                    help="replay forward+backward from a HIP graph captured in warmup (measured no faster: DESIGN §6)")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
-    args = ap.parse_args()
+def cpu_baseline(cfg, samples, reps: int = 3, one_thread_graphs: int = 1, one_thread_reps: int = 3):
+    """The reference algorithm on this host's CPU cores: all the threads torch uses
+    here (OMP_NUM_THREADS / the CPU share of the box) on the config's own batch, median of `reps`
+    after one warm-up; plus one thread on `one_thread_graphs` graph(s) of it.  (The config-2 batch
+    takes ~16 s per step on 16 threads of the GPU box's EPYC, so the sample stays at 3 + 1 steps
+    to keep the default bench within a few minutes.)"""
+    threads = torch.get_num_threads()
+    what = "inference forwards" if cfg.get("inference") else \
+        f"training steps (fwd+NMSE{'+div' if cfg['divergence'] else ''}+bwd)"
+    step, nodes = _oracle_step_fn(cfg, samples)
+    rate, ts = _median_rate(step, nodes, reps)
+    torch.set_num_threads(1)
+    try:
+        step1, nodes1 = _oracle_step_fn(cfg, samples[:one_thread_graphs])
+        rate1, ts1 = _median_rate(step1, nodes1, one_thread_reps)
+    finally:
+        torch.set_num_threads(threads)
+    return {"value": round(rate, 1), "unit": "nodes/s", "cores": threads, "kind": "port",
+            "sample": f"median of {reps} {what} (after 1 warm-up) of the config's batch: {len(samples)} graph(s), "
+                      f"{nodes} nodes, {cfg['steps']} MP steps, fp32, torch CPU ({threads} threads), "
+                      f"oracle/epd_oracle.py",
+            "step_s": [round(t, 3) for t in ts],
+            "value_1thread": round(rate1, 1),
+            "sample_1thread": f"median of {one_thread_reps} (after 1 warm-up), {one_thread_graphs} graph(s), "
+                              f"{nodes1} nodes, 1 thread",
+            "host_cpu_count": os.cpu_count(), "host_affinity": len(os.sched_getaffinity(0)),
+            "cpu_model": _cpu_model_name()}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one process per GPU; PDG_DIST_BACKEND=gloo with more ranks than GPUs only rehearses the
-    # multi-rank flow (ranks share devices round-robin)
-    backend = os.environ.get("PDG_DIST_BACKEND", "nccl")
-    dev_index = local % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(dev_index)
-    device = torch.device("cuda", dev_index)
-    pg = None
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
-        pg = dist.group.WORLD
 
-    from gnn_local_stress.models import EncodeProcessDecode
-    from pdg.plan import plan_for
-    from pdg.trainer import Trainer
-
-    cfg = CONFIGS[args.config]
-    batch, samples = build_batch(cfg, seed=69 + rank, device=device)
-    stats = dataset_stats(batch)
-    if pg is not None:  # dataset statistics are global constants of the training set
-        v = torch.stack([stats[k].float() for k in stats])
-        dist.all_reduce(v)
-        stats = {k: v[i] / world for i, k in enumerate(stats)}
-    torch.manual_seed(69)
-    model = EncodeProcessDecode(input_edges_features_size=1, message_passing_steps=cfg["steps"], latent_size=L,
-                                input_nodes_features_size=6, output_nodes_features_size=3, **stats).to(device)
-    trainer = Trainer(model, lr=1e-3, divergence=cfg["divergence"], divergence_penalty=10.0, process_group=pg,
-                      dp_mode=args.dp_mode, capture=args.graph)
-    plan = plan_for(batch)
-    N, E = plan.n_nodes, plan.n_edges
-
-    infer = cfg.get("inference", False)
-    if infer:
-        def run_step():
-            with torch.no_grad():
-                return {"total": model(batch, scale_output=True).local_stress.abs().mean()}
-    else:
-        def run_step():
-            return trainer.step(batch)
-    for _ in range(args.warmup):
-        run_step()
-    torch.cuda.synchronize()
-    eng = trainer.engine
-    # HIP events bracket the timed kernels' launches in the last `ev_steps` steps of the timed
-    # region (each event pair costs a few us of queue time; sampling keeps the region clean)
-    timed_kernels = ["edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2", "segment_sum", "node_net", "node_bwd",
-                     "node_pq", "gemm_sum2", "pq_scatter_bwd"]
-    fused = eng.fused_edge_wgrad
-    ev_steps = min(args.steps, 3)
-    graph_steps = 0 if (infer or not trainer.capture) else args.steps - ev_steps
-    if pg is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        if i == args.steps - ev_steps:
-            # the event-timed steps launch eagerly (events cannot bracket launches inside a graph
-            # replay); the other timed steps replay the graph captured during warmup
-            trainer.capture = False
-            eng.timed = {k: [] for k in timed_kernels}
-        out = run_step()
-    torch.cuda.synchronize()
-    if pg is not None:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    ev = eng.timed
-    eng.timed = None
-    if pg is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t)
-    loss = float(out["total"])
-
-    ev = {k: v for k, v in ev.items() if v}
-    kt = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) * 1e-3 for k, v in ev.items()}
-    ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
-    S = cfg["steps"]
-    nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
-    # algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops and the bytes the
-    # kernel must read/write (inputs once, outputs once, int32 indices)
-    # per kernel: ([(executed MFMA flops, the peak of that instruction type)], bytes); an fp32-accurate
-    # 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA, or 6x that in bf16 (bf16x6)
+# ---------------------------------------------------------------------------------- roofline
+def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool) -> dict:
+    """Algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops with the peak of their
+    instruction type, and the bytes the kernel must read/write (inputs once, outputs once, int32
+    indices).  An fp32-accurate 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA,
+    or 6x that in bf16 (bf16x6)."""
     g = 2 * L * L
-    work = {
+    return {
         # W_c product (fp32 MFMA) + 2 W2 products (bf16x6) per edge; reads a2e_prev, e_prev, 4 gathered
         # P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e
         "edge_fwd": ([(E * g, PEAK_FP32_MFMA), (E * 2 * g * X6, PEAK_BF16_MFMA)],
@@ -239,8 +210,10 @@ def main():
         "pq_scatter_bwd": ([], 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
     }
 
+
+def load_pmc(fused: bool) -> dict:
     pmc = {}
-    if PMC_FILE.exists() and args.config == 2:
+    if PMC_FILE.exists():
         data = json.loads(PMC_FILE.read_text())
         for k, prefix in PMC_NAMES.items():
             if fused and k == "edge_bwd":
@@ -248,59 +221,267 @@ def main():
             hit = [v for name, v in data.items() if name.startswith(prefix)]
             if hit:
                 pmc[k] = round(hit[0]["total"])
+    return pmc
 
-    def roof(k):
-        terms, nbytes = work[k]
-        t = kt[k]
-        flops = sum(f for f, _ in terms)
-        t_peak = sum(f / pk for f, pk in terms)     # matrix-core time at peak rate
-        f_mfma = t_peak / t
-        f_hbm = nbytes / t / PEAK_HBM
-        bound = "mfma" if f_mfma >= f_hbm else "hbm"
-        if bound == "mfma":   # executed flops / time against the flop-weighted peak of the mix
-            ach, peak, unit = flops / t / 1e12, flops / t_peak / 1e12, "TFLOP/s"
-        else:
-            ach, peak, unit = nbytes / t / 1e9, PEAK_HBM / 1e9, "GB/s"
-        return {"kernel": k, "bound": bound, "achieved": round(ach, 2), "peak": round(peak, 1), "unit": unit,
-                "frac": round(ach / peak, 4), "traffic": pmc.get(k),
-                "traffic_source": (f"profiles/{PMC_FILE.name}: 2*FETCH_SIZE+WRITE_SIZE per dispatch"
-                                   + (" (mean over all weights' wgrad dispatches)" if k == "wgrad_W2" else "")
-                                   if k in pmc else None),
-                "flops_per_launch": flops,
-                "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4), "frac_hbm": round(f_hbm, 4),
-                "avg_launch_ms": round(t * 1e3, 4), "share_of_step": round(ktot[k] / (el * ev_steps / args.steps), 4)}
 
+def roofline(k, work, kt, ktot, step_s, pmc):
+    terms, nbytes = work[k]
+    t = kt[k]
+    flops = sum(f for f, _ in terms)
+    t_peak = sum(f / pk for f, pk in terms)     # matrix-core time at peak rate
+    f_mfma = t_peak / t
+    f_hbm = nbytes / t / PEAK_HBM
+    bound = "mfma" if f_mfma >= f_hbm else "hbm"
+    if bound == "mfma":   # executed flops / time against the flop-weighted peak of the mix
+        ach, peak, unit = flops / t / 1e12, flops / t_peak / 1e12, "TFLOP/s"
+    else:
+        ach, peak, unit = nbytes / t / 1e9, PEAK_HBM / 1e9, "GB/s"
+    return {"kernel": k, "bound": bound, "achieved": round(ach, 2), "peak": round(peak, 1), "unit": unit,
+            "frac": round(ach / peak, 4), "traffic": pmc.get(k),
+            "traffic_source": (f"profiles/{PMC_FILE.name}: 2*FETCH_SIZE+WRITE_SIZE per dispatch" if k in pmc else None),
+            "flops_per_launch": flops, "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4),
+            "frac_hbm": round(f_hbm, 4), "avg_launch_ms": round(t * 1e3, 4),
+            "share_of_step": round(ktot[k] / step_s, 4)}
+
+
+# ---------------------------------------------------------------------------------- timing
+TIMED_KERNELS = ["edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2", "segment_sum", "node_net", "node_bwd",
+                 "node_pq", "gemm_sum2", "pq_scatter_bwd"]
+
+
+def _allgather_ints(vals, world, device):
+    t = torch.tensor(vals, dtype=torch.int64, device=device)
+    if world == 1:
+        return [vals]
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def _max_over_ranks(x: float, world: int, device) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t)
+
+
+def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: bool = False) -> tuple[dict, list]:
+    """Build this rank's batch of config `cid`, run W warm-up and K timed steps, return the
+    record (value over all ranks, ms/step, rooflines) and this rank's samples."""
+    from gnn_local_stress.models import EncodeProcessDecode
+    from pdg.plan import plan_for
+    from pdg.trainer import Trainer
+
+    cfg = CONFIGS[cid]
+    idx = shard_indices(cfg, rank, world)
+    seed = 69 if cfg.get("global_batch") else 69 + rank
+    batch, samples = build_batch(cfg, seed=seed, device=device, indices=idx)
+    stats = dataset_stats(batch)
+    if pg is not None:  # dataset statistics are global constants of the training set
+        v = torch.stack([stats[k].float() for k in stats])
+        dist.all_reduce(v)
+        stats = {k: v[i] / world for i, k in enumerate(stats)}
+    torch.manual_seed(69)
+    model = EncodeProcessDecode(input_edges_features_size=1, message_passing_steps=cfg["steps"], latent_size=L,
+                                input_nodes_features_size=6, output_nodes_features_size=3, **stats).to(device)
+    trainer = Trainer(model, lr=1e-3, divergence=cfg["divergence"], divergence_penalty=10.0, process_group=pg,
+                      dp_mode=args.dp_mode, capture=args.graph)
+    plan = plan_for(batch)
+    N, E = plan.n_nodes, plan.n_edges
+    infer = cfg.get("inference", False)
+    if infer:
+        def run_step():
+            with torch.no_grad():
+                return {"total": model(batch, scale_output=True).local_stress.abs().mean()}
+    else:
+        def run_step():
+            return trainer.step(batch)
+    for _ in range(args.warmup):
+        run_step()
+    torch.cuda.synchronize()
+    eng = trainer.engine
+    # HIP events bracket the timed kernels' launches in the last `ev_steps` steps of the timed
+    # region (each event pair costs a few us of queue time; sampling keeps the region clean)
+    ev_steps = min(args.steps, 3)
+    graph_steps = 0 if (infer or not trainer.capture) else args.steps - ev_steps
+    if pg is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        if i == args.steps - ev_steps:
+            # the event-timed steps launch eagerly (events cannot bracket launches inside a graph
+            # replay); the other timed steps replay the graph captured during warmup
+            trainer.capture = False
+            eng.timed = {k: [] for k in TIMED_KERNELS}
+        out = run_step()
+    torch.cuda.synchronize()
+    if pg is not None:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, world, device)
+    ev = {k: v for k, v in eng.timed.items() if v}
+    eng.timed = None
+    loss = float(out["total"])
+    per_rank = _allgather_ints([N, E, len(idx)], world, device)
+    total_nodes = sum(r[0] for r in per_rank)
+
+    kt = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) * 1e-3 for k, v in ev.items()}
+    ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
+    fused = eng.fused_edge_wgrad
+    nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
+    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused)
+    pmc = load_pmc(fused) if with_pmc else {}
+    step_s = el * ev_steps / args.steps
     dominant = max([k for k in ("edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])
-    if rank == 0:
-        res = {
-            "metric": ("mesh-nodes/sec (inference) on periodic FEM graphs" if infer
-                       else "mesh-nodes/sec (fwd+bwd) on periodic FEM graphs"),
-            "value": round(world * N * args.steps / el, 1),
-            "unit": "nodes/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(el / args.steps * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic periodic triangulated meshes (pdg.meshgen, seed 69+rank), random-init weights (seed 69)",
-            "config": {"workload": cfg["workload"], "graphs_per_gpu": cfg["graphs"], "nodes_per_gpu": N,
-                       "edges_per_gpu": E, "global_batch": cfg["graphs"] * world,
-                       "message_passing_steps": cfg["steps"], "latent": L, "divergence": cfg["divergence"],
-                       "parallelism": f"graph-DP x{world}" + ("" if args.dp_mode == "replica" else " (sync-LN)"), "final_loss": round(loss, 6),
-                       "hip_graph_steps": graph_steps},
-            "roofline": roof(dominant),
-            "roofline_gather_scatter": [roof(k) for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
-            "roofline_node_net": roof("node_net") if "node_net" in kt else None,
-            "kernel_ms": {k: round(v * 1e3, 4) for k, v in kt.items()},
-        }
-        if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(cfg, samples, args.cpu_seconds)
+    strong = bool(cfg.get("global_batch"))
+    rec = {
+        "metric": ("mesh-nodes/sec (inference) on periodic FEM graphs" if infer
+                   else "mesh-nodes/sec (fwd+bwd) on periodic FEM graphs"),
+        "value": round(total_nodes * args.steps / el, 1),
+        "unit": "nodes/s",
+        "n_gpus": world,
+        "ms_per_step": round(el / args.steps * 1e3, 3),
+        "scaling": "strong" if strong else "weak",
+        "config": {"workload": cfg["workload"], "graphs_per_gpu": None if strong else cfg["graphs"],
+                   "nodes_per_gpu": N, "edges_per_gpu": E,
+                   "global_batch": cfg["graphs"] if strong else cfg["graphs"] * world,
+                   "message_passing_steps": cfg["steps"], "latent": L, "divergence": cfg["divergence"],
+                   "parallelism": f"graph-DP x{world}" + ("" if args.dp_mode == "replica" else " (sync-LN)"),
+                   "final_loss": round(loss, 6), "hip_graph_steps": graph_steps,
+                   "per_rank": {"nodes": [r[0] for r in per_rank], "edges": [r[1] for r in per_rank],
+                                "graphs": [r[2] for r in per_rank]}},
+        "roofline": roofline(dominant, work, kt, ktot, step_s, pmc),
+        "roofline_gather_scatter": [roofline(k, work, kt, ktot, step_s, pmc)
+                                    for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
+        "roofline_node_net": roofline("node_net", work, kt, ktot, step_s, pmc) if "node_net" in kt else None,
+        "kernel_ms": {k: round(v * 1e3, 4) for k, v in kt.items()},
+    }
+    del trainer, model, batch, plan
+    torch.cuda.empty_cache()
+    return rec, samples
+
+
+def time_plumbing(args, rank: int, world: int, pg, device) -> dict:
+    """--plumbing: the multi-rank flow of time_config with one all-reduce of a gradient-sized
+    bucket as the only work (no HIP kernels; CPU tests with gloo)."""
+    bucket = torch.zeros(N_PARAMS, dtype=torch.float32, device=device)
+    for _ in range(args.warmup):
+        dist.all_reduce(bucket) if pg is not None else None
+    if pg is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if pg is not None:
+            dist.all_reduce(bucket)
+    if pg is not None:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, world, device)
+    per_rank = _allgather_ints([rank, dist.get_world_size() if pg is not None else 1], world, device)
+    return {"metric": "plumbing only (no HIP kernels): launch, rendezvous, timing and reporting of bench.py",
+            "value": None, "unit": "nodes/s", "n_gpus": world, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "scaling": "weak", "plumbing": True,
+            "config": {"workload": "gradient-bucket all-reduce only", "parallelism": f"graph-DP x{world}",
+                       "per_rank": {"rank": [r[0] for r in per_rank], "world_seen": [r[1] for r in per_rank]}}}
+
+
+# ---------------------------------------------------------------------------------- launch
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawned_rank(i: int, n: int) -> None:
+    os.environ.update(RANK=str(i), LOCAL_RANK=str(i), WORLD_SIZE=str(n))
+    main()
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--dp-mode", default="replica", choices=["replica", "sync"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="main line only (no config 3/4/5 sub-results)")
+    ap.add_argument("--extra-steps", type=int, default=10, help="timed steps of each sub-result")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay forward+backward from a HIP graph captured in warmup (measured no faster: DESIGN §6)")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="launch/rendezvous/report flow only, no HIP kernels (CPU tests)")
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: spawn one rank per GPU before anything initialises the GPU here
+        import torch.multiprocessing as mp
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        mp.start_processes(_spawned_rank, args=(args.gpus,), nprocs=args.gpus, start_method="spawn", join=True)
+        return
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks")
+    # one process per GPU; PDG_DIST_BACKEND=gloo with more ranks than GPUs only rehearses the
+    # multi-rank flow (ranks share devices round-robin)
+    backend = os.environ.get("PDG_DIST_BACKEND", "gloo" if args.plumbing else "nccl")
+    if args.plumbing:
+        device = torch.device("cpu")
+    else:
+        dev_index = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
+    pg = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
         else:
-            res["cpu_baseline"] = None
-        print(json.dumps(res), flush=True)
+            dist.init_process_group(backend)
+        pg = dist.group.WORLD
+        assert dist.get_world_size() == world
+
+    if args.plumbing:
+        res = time_plumbing(args, rank, world, pg, device)
+        subs = {}
+    else:
+        res, samples = time_config(args.config, args, rank, world, pg, device, with_pmc=args.config == 2)
+        subs = {}
+        if args.config == 2 and not args.no_extras:
+            sub_args = argparse.Namespace(**{**vars(args), "steps": args.extra_steps})
+            for cid in (3, 4, 5):
+                r, s = time_config(cid, sub_args, rank, world, pg, device)
+                subs[f"config{cid}"] = (r, s)
+    if rank == 0:
+        line = {"metric": res["metric"], "value": res["value"], "unit": res["unit"], "n_gpus": res["n_gpus"],
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+                "higher_is_better": True, "scaling": res["scaling"], "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic periodic triangulated meshes (pdg.meshgen, seed 69+rank), random-init weights (seed 69)",
+                "world_size_rccl": dist.get_world_size() if pg is not None else 1,
+                "backend": backend if pg is not None else None}
+        line.update({k: v for k, v in res.items() if k not in line})
+        cpu_ok = world == 1 and not args.no_cpu_baseline and not args.plumbing
+        line["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], samples) if cpu_ok else None
+        if subs:
+            line["sub_results"] = {}
+            for name, (r, s) in subs.items():
+                cfg = CONFIGS[int(name[-1])]
+                if cpu_ok:   # bounded samples: 2 graphs (config 3/4) or one 5,041-node mesh (config 5)
+                    if cfg.get("inference"):
+                        from pdg import meshgen
+                        s = meshgen.make_dataset(1, n=71, seed=69)
+                    r["cpu_baseline"] = cpu_baseline(cfg, s[:2], reps=3, one_thread_reps=1)
+                r["steps"], r["warmup"] = args.extra_steps, args.warmup
+                line["sub_results"][name] = r
+        print(json.dumps(line), flush=True)
     if pg is not None:
         dist.barrier()
         dist.destroy_process_group()

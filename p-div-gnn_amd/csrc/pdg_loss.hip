@@ -250,14 +250,14 @@ __global__ void adam_kernel(long n, float* __restrict__ p, const float* __restri
   const float2 t = tab[c < tab_len ? c : tab_len - 1];
   // Explicitly rounded operations in torch's CPU kernel order (no contraction beyond what it does):
   //   lerp_vec:  fmadd(w1, g - m, m)                 (weight < 0.5)
-  //   mul_ then addcmul_: (v * b2) + ((w2 * g) * g)
+  //   mul_ then addcmul_: fmadd(w2 * g, g, v * b2)   (checked against torch's CPU kernels)
   //   denom:     sqrt(v) / bc2_sqrt + eps
   //   addcdiv_:  p + ((-step_size) * m) / denom
   const float nstep = -t.x;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const float gi = g[i];
     const float mi = __fmaf_rn(w1, __fsub_rn(gi, m[i]), m[i]);
-    const float vi = __fadd_rn(__fmul_rn(v[i], b2), __fmul_rn(__fmul_rn(w2, gi), gi));
+    const float vi = __fmaf_rn(__fmul_rn(w2, gi), gi, __fmul_rn(v[i], b2));
     m[i] = mi;
     v[i] = vi;
     const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(vi), t.y), eps);

@@ -3,8 +3,11 @@ against the reference's own update, torch.optim.Adam(lr=1e-3) stepped through
 GradScaler (scripts/gnn_train.py:111,118,204-207), applied on the CPU to the SAME gradients
 the HIP backward produced.
 
-* Five steps: parameters, exp_avg and exp_avg_sq agree to fp32 rounding (the elementwise
-  formulas are the same; only fma contraction / lerp evaluation order may differ by an ulp).
+* Five steps: exp_avg and exp_avg_sq are BIT-IDENTICAL (pdg_adam rounds every operation the
+  way torch's CPU kernels do: fma in lerp_ and addcmul_, (s*m)/d in addcdiv_); parameters agree
+  to a few ulps: torch's vectorised CPU sqrt (SLEEF, 0.5001 ulp) differs from the correctly
+  rounded sqrt of the GPU (and of CUDA, where the reference trains) in ~0.7 % of elements by
+  one ulp of the denominator.
 * An injected NaN gradient: GradScaler skips optimizer.step(), so parameters, moments and
   Adam's step count stay put and the next step's bias correction is that of the step after
   the last real one (the advisor's round-1 finding).
@@ -19,8 +22,7 @@ from pdg import graph, meshgen
 
 pytestmark = pytest.mark.gpu
 
-RTOL_P, ATOL_P = 2e-7, 1e-9       # a few fp32 ulps of the parameters
-RTOL_M, ATOL_M = 2e-6, 1e-20      # moments: ulp-level relative
+RTOL_P, ATOL_P = 5e-7, 1e-9       # a few fp32 ulps of the parameters (sqrt rounding, above)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -74,8 +76,8 @@ class _RefAdam:
             if not st:
                 assert not m.any() and not v.any()
                 continue
-            torch.testing.assert_close(m, st["exp_avg"], rtol=RTOL_M, atol=ATOL_M)
-            torch.testing.assert_close(v, st["exp_avg_sq"], rtol=RTOL_M, atol=ATOL_M)
+            assert torch.equal(m, st["exp_avg"]), n
+            assert torch.equal(v, st["exp_avg_sq"]), n
 
     def steps_taken(self):
         st = self.opt.state.get(self.params[0])

@@ -12,7 +12,7 @@ for v in "$@"; do
   if [ "$v" = default ]; then lib=$R/p-div-gnn_amd/pdg/libpdivgnn_hip.so
   elif [ -f "$R/variants/$v/bench.py" ]; then benchpy=$R/variants/$v/bench.py; lib=$R/variants/$v/p-div-gnn_amd/pdg/libpdivgnn_hip.so
   else lib=$R/variants/$v/libpdivgnn_hip.so; fi
-  PDG_LIB=$lib timeout -k 10 300 python "$benchpy" --config "$CFG" --no-cpu-baseline \
+  PDG_LIB=$lib timeout -k 10 300 python "$benchpy" --config "$CFG" --no-cpu-baseline --no-extras \
     > "$R/gpurun_out/$TAG/$v.c$CFG.log" 2>&1 || { echo "$v failed"; tail -5 "$R/gpurun_out/$TAG/$v.c$CFG.log"; exit 1; }
   python - "$R/gpurun_out/$TAG/$v.c$CFG.log" "$v" <<'PY'
 import json, sys

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Measurement pass on the GPU box (run through gpurun from the repo root):
-#   GPU parity tests, bench lines (configs 2, 3, 5), rocprofv3 kernel stats and
+#   GPU parity tests, the default bench line (config 2 + config 3/4/5 sub-results), rocprofv3 kernel stats and
 #   the two PMC passes (FETCH_SIZE, WRITE_SIZE) of the default bench command.
 # Every GPU step has its own time limit; the script stops at the first failure.
 #   usage: tools/gpu_measure.sh TAG [all|tests|bench|prof]
@@ -25,18 +25,16 @@ if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
   step pytest_gpu 900 python -m pytest tests -m gpu -x -q || exit 1
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
-  step bench2 400 python bench.py || exit 1
-  step bench3 400 python bench.py --config 3 --no-cpu-baseline || exit 1
-  step bench5 400 python bench.py --config 5 --steps 10 --no-cpu-baseline || exit 1
+  step bench2 600 python bench.py || exit 1
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
   step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o bench -- \
-    python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline || exit 1
+    python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-extras || exit 1
   step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o bench -- \
-    python "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline || exit 1
+    python "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-extras || exit 1
   step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o bench -- \
-    python "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline || exit 1
+    python "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-extras || exit 1
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
   cd "$R"
