@@ -1,0 +1,186 @@
+"""Training harness of the reference (``scripts/gnn_train.py``) on the HIP path.
+
+Mirrors ``run_experience`` (gnn_train.py:331-435), ``train`` (:95-305) and ``main``
+(:438-...): the same YAML keys (``configs_train/config_train_*.yml``), the same epoch loop
+with early stopping, the same train / test loss bookkeeping (per-batch losses summed on the
+device, divided by the number of batches once per epoch), the best-test-loss checkpoint
+``weights/model_weights.pth`` and the last-epoch checkpoint
+``weights/last_epoch_model_weights.pth`` in the reference's checkpoint format, and a copy of
+the config in the results folder.  What runs underneath is MI355X-native:
+
+* the datasets are uploaded once into HBM (``pdg.collate.DeviceGraphStore``) and every
+  minibatch is collated on the device in one launch;
+* each training step is ``pdg.trainer.Trainer.step`` (HIP forward, fused NMSE + divergence
+  loss, HIP backward, Adam stepped with GradScaler's skip semantics) with no host sync;
+* the test pass runs the HIP forward under ``no_grad`` and the fused batch loss.
+
+Shuffling uses ``torch.utils.data.RandomSampler`` over the graph indices, the sampler PyG's
+``DataLoader(shuffle=True)`` uses, so the minibatch order follows torch's global RNG as the
+reference's does.  TensorBoard logging, dataset histograms and the tqdm bars are out of scope
+(SURVEY §8); the losses they would log are printed and returned.
+
+    python -m gnn_local_stress.train configs_train/config_train_div.yml
+"""
+from __future__ import annotations
+
+import random
+import shutil
+import sys
+from pathlib import Path
+from typing import Any
+
+import numpy as np
+import torch
+
+from pdg.collate import DeviceGraphStore
+from pdg.trainer import Trainer
+
+from . import data_utils, datasets, losses, models
+
+SEED = 69   # gnn_train.py:38
+
+
+def _batches(store: DeviceGraphStore, batch_size: int, shuffle: bool):
+    """PyG DataLoader(batch_size, shuffle) order over a device-resident store."""
+    n = store.num_graphs
+    order = list(torch.utils.data.RandomSampler(range(n))) if shuffle else list(range(n))
+    for i in range(0, n, batch_size):
+        yield store.batch(order[i:i + batch_size])
+
+
+def evaluate(model, store: DeviceGraphStore, batch_size: int, monitor_divergence: bool):
+    """The test pass of gnn_train.py:208-252: sum over batches of (NMSE/B [+ div/B]) and of the
+    divergence term (unpenalised, as the reference monitors it), as device scalars."""
+    total = torch.zeros((), dtype=torch.float32, device=store.device)
+    div_sum = torch.zeros((), dtype=torch.float32, device=store.device)
+    nb = 0
+    with torch.no_grad():
+        for batch in _batches(store, batch_size, shuffle=False):
+            pred = model.forward(batch, scale_output=False, scale_input=True).local_stress
+            gt = data_utils.standardize(batch.local_stress, model.mean_local_stress, model.std_local_stress)
+            t, _, d = losses.batch_loss(pred, batch, gt.float().contiguous(), divergence=monitor_divergence,
+                                        divergence_penalty=1.0)
+            total = total + t
+            if monitor_divergence:
+                div_sum = div_sum + d
+            nb += 1
+    return total, div_sum, nb
+
+
+def train(model: models.EncodeProcessDecode, train_store: DeviceGraphStore, test_store: DeviceGraphStore,
+          epochs: int, batch_size: int, learning_rate: float = 0.001, weights_folder: str = "",
+          early_stopping_limit: int = 10, optimize_divergence: bool = True, divergence_penalty: float = 1.0,
+          train_all_epochs: bool = False, monitor_divergence_in_test: bool = False,
+          log=print) -> tuple[list[float], list[float]]:
+    """gnn_train.py:95-305 (without TensorBoard)."""
+    trainer = Trainer(model, lr=learning_rate, divergence=optimize_divergence,
+                      divergence_penalty=divergence_penalty)
+    folder = Path(weights_folder)
+    folder.mkdir(parents=True, exist_ok=False)
+    best_path = folder / "model_weights.pth"
+    last_path = folder / "last_epoch_model_weights.pth"
+    log(f"Device = {train_store.device};\nBatch size = {batch_size};\nLearning rate = {learning_rate};\n"
+        f"Epochs = {epochs};\nWeights path = {best_path.absolute()};\nOptimize divergence = {optimize_divergence};\n"
+        f"Divergence lamba = {divergence_penalty};\nEarly stopping limit = {early_stopping_limit};")
+    best_loss = sys.float_info.max
+    train_losses: list[float] = []
+    test_losses: list[float] = []
+    early_stopping_counter = 0
+    epoch = -1
+    dev = train_store.device
+    for epoch in range(epochs):
+        if not train_all_epochs and early_stopping_counter >= early_stopping_limit:
+            log("Training early stopped")
+            break
+        model.train()
+        nmse_sum = torch.zeros((), dtype=torch.float32, device=dev)
+        div_sum = torch.zeros((), dtype=torch.float32, device=dev)
+        total_sum = torch.zeros((), dtype=torch.float32, device=dev)
+        n_train = 0
+        for batch in _batches(train_store, batch_size, shuffle=True):
+            out = trainer.step(batch)
+            nmse_sum = nmse_sum + out["nmse"]
+            total_sum = total_sum + out["total"]
+            if optimize_divergence:
+                div_sum = div_sum + out["div"]
+            n_train += 1
+        model.eval()
+        test_total, test_div, n_test = evaluate(model, test_store, batch_size, monitor_divergence_in_test)
+        # one host sync per epoch (the reference's .item() calls, gnn_train.py:258-275)
+        vals = torch.stack([nmse_sum, total_sum, div_sum, test_total, test_div]).tolist()
+        train_mse_loss = vals[0] / n_train
+        total_loss = vals[1] / n_train
+        test_loss = vals[3] / n_test
+        if test_loss < best_loss:
+            models.save_model_checkpoint(model, trainer, epoch + 1, best_path.as_posix())
+            log(f"Checkpoint saved at {best_path}")
+            best_loss = test_loss
+            early_stopping_counter = 0
+        else:
+            early_stopping_counter += 1
+        msg = (f"Epoch: {epoch + 1} / {epochs}, \nTotal train Loss : {total_loss}\nMSE train Loss : "
+               f"{train_mse_loss} \nTest Loss : {test_loss}")
+        if optimize_divergence:
+            msg += f"\nDivergence term train {vals[2] / n_train}"
+        if monitor_divergence_in_test:
+            msg += f"\nDivergence test value {vals[4] / n_test}"
+        log(msg)
+        train_losses.append(total_loss)
+        test_losses.append(test_loss)
+    models.save_model_checkpoint(model, trainer, epoch + 1, last_path.as_posix())
+    log(f"Last checkpoint at epoch {epoch + 1} saved at {last_path}")
+    return train_losses, test_losses
+
+
+def run_experience(dataset_train_csv: str, dataset_test_csv: str, results_folder: str, epochs: int,
+                   batch_size: int, divergence: bool, latent_size: int, divergence_penalty: float,
+                   early_stopping_limit: int, learning_rate: float, message_passing_steps: int,
+                   train_all_epochs: bool = False, device: str = "cuda", periodic_graph: bool = True,
+                   monitor_divergence_in_test: bool = False, config_path: Path = Path(""), *args: Any,
+                   log=print, **kwargs: Any) -> tuple[list[float], list[float]]:
+    """gnn_train.py:331-435."""
+    import pandas as pd
+    log(f"DATASET TRAIN CSV {dataset_train_csv}\nDATASET TEST CSV {dataset_test_csv}\nEPOCHS {epochs}\n"
+        f"BATCH SIZE {batch_size}\nLEARNING RATE {learning_rate}\nPeriodic graph {periodic_graph}")
+    torch.manual_seed(SEED)
+    random.seed(SEED)
+    np.random.seed(SEED)
+    train_df = pd.read_csv(dataset_train_csv)
+    test_df = pd.read_csv(dataset_test_csv)
+    log(f"Size train dataset {len(train_df)}\nSize test dataset {len(test_df)}\nLoading datasets...")
+    train_dataset = datasets.MeshStressFieldDatasetInMemory(train_df, periodic_graph=periodic_graph)
+    # the reference builds the test set with the default periodic_graph=True (gnn_train.py:386;
+    # reproduced, not "fixed")
+    test_dataset = datasets.MeshStressFieldDatasetInMemory(test_df)
+    train_store = DeviceGraphStore(train_dataset.graphs, device)
+    test_store = DeviceGraphStore(test_dataset.graphs, device)
+    model = models.EncodeProcessDecode(
+        input_edges_features_size=1, input_nodes_features_size=6, message_passing_steps=message_passing_steps,
+        latent_size=latent_size, output_nodes_features_size=3,
+        **{k: v.to(device) for k, v in train_dataset.stats().items()})
+    log(models.print_model(model, None, device))
+    model.to(device)
+    results = Path(results_folder)
+    results.mkdir(parents=True, exist_ok=True)
+    if config_path and Path(config_path).is_file():
+        shutil.copyfile(config_path, results / Path(config_path).name)
+    return train(model=model, train_store=train_store, test_store=test_store, epochs=epochs,
+                 batch_size=batch_size, learning_rate=learning_rate,
+                 weights_folder=(results / "weights").as_posix(), early_stopping_limit=early_stopping_limit,
+                 optimize_divergence=divergence, divergence_penalty=divergence_penalty,
+                 train_all_epochs=train_all_epochs, monitor_divergence_in_test=monitor_divergence_in_test,
+                 log=log)
+
+
+def main(config_path: str, **overrides: Any):
+    """gnn_train.py:438-...: read the YAML config and run the experience."""
+    import yaml
+    with open(config_path) as f:
+        params = yaml.safe_load(f)
+    params.update(overrides)
+    params["config_path"] = Path(config_path)
+    return run_experience(**params)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])

@@ -264,6 +264,56 @@ def run_case(name: str, samples, periodic: bool, steps: int, divergence: bool, p
           f"loss={float(loss):.6f} nmse={float(nmse):.6f}")
 
 
+def run_checkpoint_case(models, datasets, data_utils, gnn_train):
+    """A checkpoint written by the reference's own save_model_checkpoint (models.py:44-63) after
+    one training step of gnn_train.py:154-207 (Adam lr=1e-3; GradScaler is inactive on the CPU),
+    plus what the reference computes from it: the forward after that step and the parameters
+    after a second step on the same batch (the resume path of load_model_checkpoint /
+    load_optimizer_checkpoint, models.py:66-95)."""
+    samples = meshgen.make_dataset(3, n=13, hole_radius=(0.15, 0.3), seed=7)
+    graphs = [reference_graph(s, True, datasets) for s in samples]
+    batch = StubBatch.from_list(graphs)
+    st = {
+        "mean_pos": batch.pos.mean(), "std_pos": batch.pos.std(),
+        "mean_mean_stress": batch.mean_stress.mean(), "std_mean_stress": batch.mean_stress.std(),
+        "mean_local_stress": batch.local_stress.mean(), "std_local_stress": batch.local_stress.std(),
+        "mean_edge_weight": batch.edge_attr.mean(), "std_edge_weight": batch.edge_attr.std(),
+    }
+    torch.manual_seed(gnn_train.SEED)
+    model = models.EncodeProcessDecode(input_edges_features_size=1, input_nodes_features_size=6,
+                                       message_passing_steps=3, latent_size=128,
+                                       output_nodes_features_size=3, **st)
+    optimizer = torch.optim.Adam(model.parameters(), lr=1e-3)
+    gt_raw = batch.local_stress.clone()
+
+    def train_step():
+        pred = model.forward(batch, scale_output=False, scale_input=True).local_stress
+        batch.local_stress = data_utils.standardize(gt_raw, model.mean_local_stress, model.std_local_stress)
+        loss = 0
+        div_loss = 0
+        for sample_i, pred_i in data_utils.slice_batch_gt_and_predictions(batch, pred):
+            loss = loss + gnn_train.normalized_mse_loss_single(
+                ground_truth_local_stress=sample_i.local_stress, predicted_local_stress=pred_i)
+            div_loss = div_loss + gnn_train.compute_divergence(
+                pred_i, sample_i.op_div_matrix, sample_i.surfaces_nodes_for_div, reduce_strategy="square") * 10.0
+        loss = loss / batch.batch_size + div_loss / batch.batch_size
+        optimizer.zero_grad()
+        loss.backward()
+        optimizer.step()
+        return float(loss)
+
+    loss1 = train_step()
+    models.save_model_checkpoint(model, optimizer, 1, str(HERE / "ref_checkpoint.pth"))
+    with torch.no_grad():
+        out1 = model.forward(batch, scale_output=True, scale_input=True).local_stress
+    loss2 = train_step()
+    rec = {"loss_step1": np.array(loss1), "loss_step2": np.array(loss2), "out_scaled_after_step1": out1.numpy()}
+    for k, v in model.state_dict().items():
+        rec[f"param_after_step2.{k}"] = v.numpy()
+    np.savez_compressed(HERE / "ref_checkpoint_case.npz", **rec)
+    print(f"ref_checkpoint: loss step1={loss1:.6f} step2={loss2:.6f}")
+
+
 def main():
     install_stubs()
     os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
@@ -282,6 +332,7 @@ def main():
              False, 10, False, 10.0, False, **mods)
     run_case("batch2_div_s10", meshgen.make_dataset(2, n=11, hole_radius=(0.2, 0.3), seed=11),
              True, 10, True, 10.0, False, **mods)
+    run_checkpoint_case(**mods)
 
 
 if __name__ == "__main__":
