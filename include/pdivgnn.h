@@ -156,23 +156,41 @@ int pdg_any_nonzero(const float* x, int64_t n, int* flag, void* stream);
 int pdg_decoder_bwd(int n_nodes, const float* gy, const float* a1d, const float* Wd2,
                     const float* Wd1T, float* gz1d, float* gx, void* stream);
 
+/* LayerNorm backward without finalize launches (every column-sum producer below): block b of a
+ * producer emits its row of per-channel partials, partials[b] = [sum gy (128) | sum gy*xhat (128)]
+ * (accumulate != 0: added to the row, so one buffer spans all message-passing steps and
+ * pdg_ln_param_grads turns it into the LayerNorm weight / bias gradients once), and, when
+ * pairs != NULL, pairs[2b..2b+1] = (sum_c g_c row_c, sum_c g_c row_{128+c}) with g = ln_g.  The
+ * consumer kernels (pdg_node_bwd, pdg_edge_bwd(_w2), pdg_mlp2_bwd) take these pairs in place of
+ * a finalized pdg_ln_bwd and reduce them themselves (S1, S2, c1 = S1/M, c2 = S2/(M std)).
+ * New in this build: the reference's autograd computes these sums inside the LayerNorm backward
+ * (models.py:199,207,265,273). */
 /* Per-channel LayerNorm backward sums over rows: sum gy, sum gy*xhat (xhat from a2 and st);
  * gy row k = gy_rows[gidx ? gidx[k] : k]. Writes per-block partials (2 x 128 doubles each). */
 int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, const float* a2,
-                  const pdg_ln_stat* st, double* partials, int* nparts, void* stream);
+                  const pdg_ln_stat* st, double* partials, int* nparts, const float* ln_g,
+                  double* pairs, int accumulate, void* stream);
 
 /* Node-level form of pdg_ln_colsum for the message LayerNorm, whose upstream gradient is the
  * gathered gaggr[dst]: sum_k gy = sum_v deg_v gaggr[v], sum_k gy*xhat = sum_v gaggr[v]*xhat_sum[v]
  * (deg from rowptr, xhat_sum from pdg_segment_sum).  Same partial layout as pdg_ln_colsum. */
 int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* rowptr, const float* xhat_sum,
-                        double* partials, int* nparts, void* stream);
+                        double* partials, int* nparts, const float* ln_g, double* pairs, int accumulate,
+                        void* stream);
 
 /* Reduce colsum partials: grad_b += sum gy, grad_g += sum gy*xhat, and the call's
- * backward scalars (S1 = sum g*gy, S2 = sum g*gy*xhat).  Row nparts of `partials`
- * (256 doubles after the last partial) is used as scratch. */
+ * backward scalars (S1 = sum g*gy, S2 = sum g*gy*xhat): the column sums of the LayerNorm
+ * backward (PyG LayerNorm graph mode, models.py:199,207,265,273; autograd of its weight/bias).
+ * One launch (a single 1024-thread block, fixed-order fp64 sums). */
 int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g,
                            const pdg_ln_stat* st, float* grad_g, float* grad_b, pdg_ln_bwd* out,
                            void* stream);
+/* LayerNorm weight / bias gradients from producer accumulators (accumulate mode above): for
+ * group i, grad_b[i][c] += sum over rows r < rows[i] of acc[i][r][c], grad_g[i][c] += ... [128 + c];
+ * fixed order; ngroups <= 4 (node_net, edge_net, node encoder, edge encoder LayerNorms).
+ * acc/rows/grad_g/grad_b are HOST arrays of device pointers. */
+int pdg_ln_param_grads(int ngroups, const double* const* acc, const int* rows, float* const* grad_g,
+                       float* const* grad_b, void* stream);
 /* Sync DP mode, backward: after lb->S1 and lb->S2 were all-reduced over ranks, recompute
  * lb->c1 = S1/M and lb->c2 = S2/(M std) with the global statistics in st. */
 int pdg_ln_bwd_rescale(const pdg_ln_stat* st, pdg_ln_bwd* lb, void* stream);
@@ -181,7 +199,7 @@ int pdg_ln_bwd_rescale(const pdg_ln_stat* st, pdg_ln_bwd* lb, void* stream);
  * gz1 = (W2^T gz2) * [a1 > 0].  gy row k = gy_rows[gidx ? gidx[k] : k]. */
 int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a2, const float* a1,
                  const pdg_ln_stat* st, const pdg_ln_bwd* lb, const float* ln_g, const float* W2T,
-                 float* gz2, float* gz1, void* stream);
+                 float* gz2, float* gz1, const double* lb_pairs, int lb_npairs, void* stream);
 
 /* Fused node_net backward of one step (the work of pdg_mlp2_bwd + pdg_gemm_dual with
  * res0 = NULL, res1 = gy): gz2 = LN_bwd(gy) * [a2n > 0]; gz1 = (Wn2^T gz2) * [a1n > 0];
@@ -189,7 +207,10 @@ int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a
  * results of the separate kernels. */
 int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, const float* a1n, const pdg_ln_stat* st,
                  const pdg_ln_bwd* lb, const float* ln_g, const float* Wn2T, const float* Wn1aT,
-                 const float* Wn1bT, float* gz2, float* gz1, float* gaggr, float* gx_part, void* stream);
+                 const float* Wn1bT, float* gz2, float* gz1, float* gaggr, float* gx_part,
+                 const double* lb_pairs, int lb_npairs, void* stream);
+/* lb_pairs != NULL: the LayerNorm backward scalars come from a producer's pairs (see
+ * pdg_ln_colsum) and lb is ignored. */
 
 /* out0 = W0T in [+ res0]; out1 = W1T in [+ res1]  (two 128x128 products of one input). */
 int pdg_gemm_dual(int rows, const float* in, const float* W0T, const float* W1T,
@@ -198,9 +219,14 @@ int pdg_gemm_dual(int rows, const float* in, const float* W0T, const float* W1T,
 /* out = res + W0T in0 + W1T in1. */
 int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
                   const float* res, float* out, void* stream);
-/* Same result as pdg_gemm_sum2 (bitwise), weights held in registers. */
+/* Same result as pdg_gemm_sum2 (bitwise), weights held in registers.  partials != NULL: also
+ * the pdg_ln_colsum partials of the LayerNorm backward with upstream gradient `out` and input
+ * ln_a2 / statistics ln_st (the node LayerNorm of the previous message-passing step, whose
+ * output x_t = LN(a2n) + x_{t-1} receives this gradient), *nparts rows of 256 doubles. */
 int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
-                     const float* res, float* out, void* stream);
+                     const float* res, float* out, const float* ln_a2, const pdg_ln_stat* ln_st,
+                     double* partials, int* nparts, const float* ln_g, double* pairs, int accumulate,
+                     void* stream);
 
 /* Fused edge backward of one step: both edge_net evaluations' LN/relu/Linear2 backward
  * (message: gy = gaggr[dst]; edge update: gy = ge_next), gC = gz1m + gz1e,
@@ -212,7 +238,7 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
                  const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
                  const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, const float* WcT,
                  float* gz2m, float* gz1m, float* gz2e, float* gz1e, float* gC, float* ge_out,
-                 void* stream);
+                 const double* pairs_m, int npairs_m, const double* pairs_e, int npairs_e, void* stream);
 
 /* Edge backward with the shared-weight gradients fused (pdg_ebw.hip), replacing
  * pdg_edge_bwd + the W2 / Wc passes of pdg_wgrad_segments (gnn_local_stress/models.py:194-208,
@@ -231,10 +257,12 @@ int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float
                     const float* a2m, const float* a1m, const float* a2e, const float* a1e,
                     const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
                     const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
-                    float* gz1e, float* gC, float* slabs, int nslabs, void* stream);
+                    float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
+                    const double* pairs_e, int npairs_e, void* stream);
 int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next,
                      const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
-                     const pdg_ln_stat* st_ln, double* ln_partials, void* stream);
+                     const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,
+                     int accumulate, void* stream);
 
 /* Mesh graph on the device (pdg_graph.hip): FaceToEdge of a triangle
  * mesh (convert_utils.py:47-60), edge lengths (datasets.py:182-188) and, when `periodic`,

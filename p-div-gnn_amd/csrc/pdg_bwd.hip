@@ -115,8 +115,10 @@ __global__ __launch_bounds__(256) void ln_colsum_kernel(int M, const float* __re
                                                         const int* __restrict__ gidx,
                                                         const float* __restrict__ a2,
                                                         const pdg_ln_stat* __restrict__ stp,
-                                                        double* __restrict__ part) {
+                                                        double* __restrict__ part, const float* __restrict__ lg,
+                                                        double* __restrict__ sp, int accumulate) {
   __shared__ double red[8][256];
+  __shared__ double row[256], tmp[256];
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const int nhw = blockDim.x >> 5;
   const float mean = stp->mean, den = stp->den, rstd = stp->rstd;
@@ -141,20 +143,24 @@ __global__ __launch_bounds__(256) void ln_colsum_kernel(int M, const float* __re
   for (int i = threadIdx.x; i < 256; i += blockDim.x) {
     double s = 0;
     for (int w = 0; w < nhw; ++w) s += red[w][i];
-    part[(size_t)blockIdx.x * 256 + i] = s;
+    row[i] = s;
   }
+  __syncthreads();
+  lnb_emit(row, lg, part, accumulate, sp, tmp);
 }
 
 extern "C" int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, const float* a2,
-                             const pdg_ln_stat* st, double* partials, int* nparts, void* stream) {
+                             const pdg_ln_stat* st, double* partials, int* nparts, const float* ln_g,
+                             double* pairs, int accumulate, void* stream) {
   PDG_CHECK_ARG(rows > 0, "pdg_ln_colsum: rows must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(gy_rows) && PDG_ALIGNED(a2), "pdg_ln_colsum: misaligned pointer");
   long want = (rows + 7) / 8;
   long cap = (long)device_cus() * 2;
   if (cap > MAX_BLOCKS) cap = MAX_BLOCKS;
   const int grid = (int)(want < cap ? want : cap);
+  PDG_CHECK_ARG(!pairs || ln_g, "pdg_ln_colsum: pairs need ln_g");
   hipLaunchKernelGGL(ln_colsum_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, rows, gy_rows, gidx, a2, st,
-                     partials);
+                     partials, ln_g, pairs, accumulate);
   PDG_CHECK_LAUNCH("pdg_ln_colsum");
   if (nparts) *nparts = grid;
   return PDG_OK;
@@ -163,8 +169,10 @@ extern "C" int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, co
 __global__ __launch_bounds__(256) void ln_colsum_nodes_kernel(int N, const float* __restrict__ gaggr,
                                                               const int* __restrict__ rowptr,
                                                               const float* __restrict__ xs,
-                                                              double* __restrict__ part) {
+                                                              double* __restrict__ part, const float* __restrict__ lg,
+                                                              double* __restrict__ sp, int accumulate) {
   __shared__ double red[8][256];
+  __shared__ double row[256], tmp[256];
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const int nhw = blockDim.x >> 5;
   double sg[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
@@ -187,19 +195,23 @@ __global__ __launch_bounds__(256) void ln_colsum_nodes_kernel(int N, const float
   for (int i = threadIdx.x; i < 256; i += blockDim.x) {
     double s = 0;
     for (int w = 0; w < nhw; ++w) s += red[w][i];
-    part[(size_t)blockIdx.x * 256 + i] = s;
+    row[i] = s;
   }
+  __syncthreads();
+  lnb_emit(row, lg, part, accumulate, sp, tmp);
 }
 
 extern "C" int pdg_ln_colsum_nodes(int n_nodes, const float* gaggr, const int* rowptr, const float* xhat_sum,
-                                   double* partials, int* nparts, void* stream) {
+                                   double* partials, int* nparts, const float* ln_g, double* pairs, int accumulate,
+                                   void* stream) {
   PDG_CHECK_ARG(n_nodes > 0, "pdg_ln_colsum_nodes: n_nodes must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(xhat_sum), "pdg_ln_colsum_nodes: misaligned pointer");
   long want = (n_nodes + 7) / 8;
   long cap = (long)device_cus();
   const int grid = (int)(want < cap ? want : cap);
+  PDG_CHECK_ARG(!pairs || ln_g, "pdg_ln_colsum_nodes: pairs need ln_g");
   hipLaunchKernelGGL(ln_colsum_nodes_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, gaggr, rowptr,
-                     xhat_sum, partials);
+                     xhat_sum, partials, ln_g, pairs, accumulate);
   PDG_CHECK_LAUNCH("pdg_ln_colsum_nodes");
   if (nparts) *nparts = grid;
   return PDG_OK;
@@ -267,6 +279,45 @@ extern "C" int pdg_ln_colsum_finalize(const double* partials, int nparts, const 
   return PDG_OK;
 }
 
+// End of the backward: the LayerNorm parameter gradients from the per-block column accumulators
+// (lnb_emit), one block per (group, column): grad_b[c] += sum of column c, grad_g[c] += column
+// 128 + c, summed over the group's rows in a fixed order.
+constexpr int LNP_MAX = 4;
+struct LnParamJobs {
+  const double* acc[LNP_MAX];
+  int rows[LNP_MAX];
+  float* grad_g[LNP_MAX];
+  float* grad_b[LNP_MAX];
+};
+
+__global__ __launch_bounds__(256) void ln_param_grads_kernel(LnParamJobs jb) {
+  __shared__ double red[256];
+  const int grp = blockIdx.y, col = blockIdx.x;          // col < 256: 0..127 sum gy, 128..255 sum gy*xhat
+  double s = 0;
+  for (int b = threadIdx.x; b < jb.rows[grp]; b += blockDim.x) s += jb.acc[grp][(size_t)b * 256 + col];
+  const double t = block_tree_sum(s, red);
+  if (threadIdx.x == 0) {
+    float* g = col < 128 ? jb.grad_b[grp] : jb.grad_g[grp];
+    if (g) g[col & 127] += (float)t;
+  }
+}
+
+extern "C" int pdg_ln_param_grads(int ngroups, const double* const* acc, const int* rows, float* const* grad_g,
+                                  float* const* grad_b, void* stream) {
+  PDG_CHECK_ARG(ngroups > 0 && ngroups <= LNP_MAX, "pdg_ln_param_grads: 1..%d groups", LNP_MAX);
+  LnParamJobs jb{};
+  for (int i = 0; i < ngroups; ++i) {
+    PDG_CHECK_ARG(acc[i] && rows[i] > 0 && rows[i] <= MAX_BLOCKS, "pdg_ln_param_grads: bad group %d", i);
+    jb.acc[i] = acc[i];
+    jb.rows[i] = rows[i];
+    jb.grad_g[i] = grad_g[i];
+    jb.grad_b[i] = grad_b[i];
+  }
+  hipLaunchKernelGGL(ln_param_grads_kernel, dim3(256, ngroups), dim3(256), 0, (hipStream_t)stream, jb);
+  PDG_CHECK_LAUNCH("pdg_ln_param_grads");
+  return PDG_OK;
+}
+
 // Exact data-parallel LayerNorm backward: after S1/S2 of `lb` have been all-reduced
 // over the process group, recompute c1 = S1/M, c2 = S2/(M sd) with the global count
 // and std held in `st` (same formulas as ln_colsum_finalize_kernel).
@@ -294,12 +345,13 @@ __global__ __launch_bounds__(384, 3) void mlp2_bwd_kernel(int M, const float* __
                                                            const pdg_ln_bwd* __restrict__ lbp,
                                                            const float* __restrict__ lg,
                                                            const float* __restrict__ W2T,
-                                                           float* __restrict__ gz2, float* __restrict__ gz1) {
+                                                           float* __restrict__ gz2, float* __restrict__ gz1,
+                                                           const double* __restrict__ lb_pairs, int lb_npairs) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   load_wblock(lds, W2T, L, 0);
   __syncthreads();
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
-  const pdg_ln_bwd lb = *lbp;
+  const pdg_ln_bwd lb = lnb_resolve(lbp, lb_pairs, lb_npairs, stp);
   const int l = lane_id();
   PDG_TILE_LOOP(M) {
     const int row = tile * TILE + (l & 15);
@@ -322,14 +374,15 @@ __global__ __launch_bounds__(384, 3) void mlp2_bwd_kernel(int M, const float* __
 
 extern "C" int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a2, const float* a1,
                             const pdg_ln_stat* st, const pdg_ln_bwd* lb, const float* ln_g, const float* W2T,
-                            float* gz2, float* gz1, void* stream) {
+                            float* gz2, float* gz1, const double* lb_pairs, int lb_npairs, void* stream) {
   PDG_CHECK_ARG(rows > 0, "pdg_mlp2_bwd: rows must be > 0");
+  PDG_CHECK_ARG(lb || lb_pairs, "pdg_mlp2_bwd: need lb or lb_pairs");
   PDG_CHECK_ARG(PDG_ALIGNED(gy_rows) && PDG_ALIGNED(a2) && PDG_ALIGNED(a1) && PDG_ALIGNED(gz2) &&
                     PDG_ALIGNED(gz1) && PDG_ALIGNED(W2T),
                 "pdg_mlp2_bwd: misaligned pointer");
   const int grid = persistent_grid(rows, 6, 2);
   hipLaunchKernelGGL(mlp2_bwd_kernel, dim3(grid), dim3(384), WBLK * sizeof(float), (hipStream_t)stream, rows,
-                     gy_rows, gidx, a2, a1, st, lb, ln_g, W2T, gz2, gz1);
+                     gy_rows, gidx, a2, a1, st, lb, ln_g, W2T, gz2, gz1, lb_pairs, lb_npairs);
   PDG_CHECK_LAUNCH("pdg_mlp2_bwd");
   return PDG_OK;
 }
@@ -448,7 +501,7 @@ __global__ __launch_bounds__(64 * EB_WAVES, EB_WAVES / 4) void edge_bwd_kernel(
     const pdg_ln_bwd* __restrict__ lbm_p, const pdg_ln_bwd* __restrict__ lbe_p, const float* __restrict__ lg,
     const float* __restrict__ W2T, const float* __restrict__ WcT, float* __restrict__ gz2m,
     float* __restrict__ gz1m, float* __restrict__ gz2e, float* __restrict__ gz1e, float* __restrict__ gC,
-    float* __restrict__ ge_out) {
+    float* __restrict__ ge_out, const double* __restrict__ pm, int npm, const double* __restrict__ pe, int npe) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
 #if PDG_EDGE_X6
   load_wblock_swz(lds, WcT, L, 0);                                   // Wc^T (fp32)
@@ -466,7 +519,8 @@ __global__ __launch_bounds__(64 * EB_WAVES, EB_WAVES / 4) void edge_bwd_kernel(
   __syncthreads();
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
   const LNStat ste = *reinterpret_cast<const LNStat*>(EU ? ste_p : stm_p);
-  const pdg_ln_bwd lbm = *lbm_p, lbe = *(EU ? lbe_p : lbm_p);
+  const pdg_ln_bwd lbm = lnb_resolve(lbm_p, pm, npm, stm_p);
+  const pdg_ln_bwd lbe = EU ? lnb_resolve(lbe_p, pe, npe, ste_p) : lbm;
   const int l = lane_id();
   const int lc = lane_col();
   const int nw = blockDim.x >> 6, ntiles = tiles_of(E), stride = gridDim.x * nw;
@@ -550,13 +604,15 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
                             const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
                             const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, const float* WcT,
                             float* gz2m, float* gz1m, float* gz2e, float* gz1e, float* gC, float* ge_out,
+                            const double* pairs_m, int npairs_m, const double* pairs_e, int npairs_e,
                             void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd: n_edges must be > 0");
+  PDG_CHECK_ARG(lb_m || pairs_m, "pdg_edge_bwd: need lb_m or pairs_m");
   PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(gz2m) &&
                     PDG_ALIGNED(gz1m) && PDG_ALIGNED(gC) && PDG_ALIGNED(ge_out),
                 "pdg_edge_bwd: misaligned pointer");
   PDG_CHECK_ARG(!ge_next || (PDG_ALIGNED(ge_next) && PDG_ALIGNED(a2e) && PDG_ALIGNED(a1e) && PDG_ALIGNED(gz2e) &&
-                             PDG_ALIGNED(gz1e) && st_e && lb_e),
+                             PDG_ALIGNED(gz1e) && st_e && (lb_e || pairs_e)),
                 "pdg_edge_bwd: edge-update arguments missing or misaligned");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd: ge_out must not alias ge_next");
   const int grid = persistent_grid(n_edges, EB_WAVES, 1);
@@ -564,11 +620,11 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
   if (ge_next)
     hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(64 * EB_WAVES), shm, (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
-                       gz1m, gz2e, gz1e, gC, ge_out);
+                       gz1m, gz2e, gz1e, gC, ge_out, pairs_m, npairs_m, pairs_e, npairs_e);
   else
     hipLaunchKernelGGL(edge_bwd_kernel<false>, dim3(grid), dim3(64 * EB_WAVES), shm, (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, WcT, gz2m,
-                       gz1m, gz2e, gz1e, gC, ge_out);
+                       gz1m, gz2e, gz1e, gC, ge_out, pairs_m, npairs_m, pairs_m, npairs_m);
   PDG_CHECK_LAUNCH("pdg_edge_bwd");
   return PDG_OK;
 }

@@ -373,6 +373,69 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
+// ----------------------------------------------------------------------------- LayerNorm backward
+// scalars without finalize launches.  The backward of the graph LayerNorm y = xhat*g + b needs
+// per-channel sums over all rows of gy and gy*xhat (the g / b gradients) and two scalars
+// S1 = sum_c g_c sum gy_c, S2 = sum_c g_c sum (gy xhat)_c for the input gradient.  Each producer
+// block emits its column-partial row (256 doubles, added into a per-block accumulator that spans
+// all message-passing steps; pdg_ln_param_grads reduces it once) and its own pair
+// (sum_c g_c row_c, sum_c g_c row_128+c).  The consumer reduces the <= MAX_BLOCKS pairs itself
+// (lnb_resolve), so no launch sits between producer and consumer.
+
+// All threads of the block (>= 128) call this with the block's complete row in LDS; `tmp` is a
+// 256-double LDS scratch.  accumulate ? part[b] += row : part[b] = row; sp[b] = the pair.
+__device__ __forceinline__ void lnb_emit(const double* row, const float* __restrict__ g, double* __restrict__ part,
+                                         int accumulate, double* __restrict__ sp, double* tmp) {
+  const int t = threadIdx.x, b = blockIdx.x;
+  for (int i = t; i < 256; i += blockDim.x) {
+    double* dst = part + (size_t)b * 256 + i;
+    *dst = accumulate ? *dst + row[i] : row[i];
+  }
+  if (sp == nullptr) return;
+  if (t < 128) {
+    tmp[t] = (double)g[t] * row[t];
+    tmp[128 + t] = (double)g[t] * row[128 + t];
+  }
+  __syncthreads();
+  for (int o = 64; o > 0; o >>= 1) {
+    if (t < o) {
+      tmp[t] += tmp[t + o];
+      tmp[128 + t] += tmp[128 + t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    sp[2 * b] = tmp[0];
+    sp[2 * b + 1] = tmp[128];
+  }
+}
+
+// The backward scalars of one LayerNorm call: *lbp (precomputed), or, when sp != NULL, from the
+// producers' np pairs.  Every wave computes them with the same lane order and xor butterfly (float
+// addition commutes, so all lanes of all waves of all blocks get bit-identical values).
+__device__ __forceinline__ pdg_ln_bwd lnb_resolve(const pdg_ln_bwd* __restrict__ lbp, const double* __restrict__ sp,
+                                                  int np, const pdg_ln_stat* __restrict__ stp) {
+  if (sp == nullptr) return *lbp;
+  double s1 = 0, s2 = 0;
+  for (int b = lane_id(); b < np; b += 64) {
+    const double2 v = reinterpret_cast<const double2*>(sp)[b];
+    s1 += v.x;
+    s2 += v.y;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  const double M = stp->count, sd = stp->std_d;
+  pdg_ln_bwd r;
+  r.S1 = s1;
+  r.S2 = s2;
+  r.c1 = (float)(s1 / M);
+  r.c2 = sd > 0 ? (float)(s2 / (M * sd)) : 0.f;
+  return r;
+}
+
 // Block-wide sum of two doubles; result valid in thread 0.  `red` needs 2*nwaves doubles.
 __device__ __forceinline__ void block_sum2(double& a, double& b, double* red) {
   a = wave_sum(a);

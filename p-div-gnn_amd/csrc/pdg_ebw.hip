@@ -208,7 +208,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ stm_p, const pdg_ln_stat* __restrict__ ste_p,
     const pdg_ln_bwd* __restrict__ lbm_p, const pdg_ln_bwd* __restrict__ lbe_p, const float* __restrict__ lg,
     const float* __restrict__ W2T, float* __restrict__ gz1m, float* __restrict__ gz1e, float* __restrict__ gC,
-    float* __restrict__ slabs, int E) {
+    float* __restrict__ slabs, int E, const double* __restrict__ pm, int npm, const double* __restrict__ pe,
+    int npe) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img_gm = sm;                                  // gz2m
   unsigned char* img_am = sm + EBW_IMG;                        // a1m
@@ -225,7 +226,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
   const LNStat ste = *reinterpret_cast<const LNStat*>(EU ? ste_p : stm_p);
-  const pdg_ln_bwd lbm = *lbm_p, lbe = *(EU ? lbe_p : lbm_p);
+  const pdg_ln_bwd lbm = lnb_resolve(lbm_p, pm, npm, stm_p);
+  const pdg_ln_bwd lbe = EU ? lnb_resolve(lbe_p, pe, npe, ste_p) : lbm;
   f32x16 acc[2];
 #pragma unroll
   for (int b = 0; b < 2; ++b)
@@ -331,7 +333,8 @@ template <bool RES>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
     const float* __restrict__ gC, const float* __restrict__ e, const float* __restrict__ ge_next,
     const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs,
-    const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, double* __restrict__ part, int E) {
+    const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, double* __restrict__ part, int E,
+    const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img_c = sm;                                         // gC
   unsigned char* img_e = sm + EBW_IMG;                               // e
@@ -432,11 +435,14 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
       red[rg * 2 * L + L + 4 * cg + j] = cs_x[j];
     }
     __syncthreads();
+    double* row = red + EBW_THREADS / 32 * 2 * L;      // after the row groups' sums
     for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) {
       double v = 0;
       for (int g = 0; g < EBW_THREADS / 32; ++g) v += red[g * 2 * L + i];
-      part[(size_t)blockIdx.x * 2 * L + i] = v;
+      row[i] = v;
     }
+    __syncthreads();
+    lnb_emit(row, ln_g, part, accumulate, pairs, row + 2 * L);
   }
 }
 
@@ -445,34 +451,35 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
                                const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
                                const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
-                               float* gz1e, float* gC, float* slabs, int nslabs, void* stream) {
+                               float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
+                               const double* pairs_e, int npairs_e, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_w2: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_bwd_w2: bad slabs");
-  PDG_CHECK_ARG(dst && gaggr && a2m && a1m && st_m && lb_m && ln_g && W2T && gz1m && gC,
+  PDG_CHECK_ARG(dst && gaggr && a2m && a1m && st_m && (lb_m || pairs_m) && ln_g && W2T && gz1m && gC,
                 "pdg_edge_bwd_w2: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(ln_g) &&
                     PDG_ALIGNED(W2T) && PDG_ALIGNED(gz1m) && PDG_ALIGNED(gC) && PDG_ALIGNED(slabs),
                 "pdg_edge_bwd_w2: misaligned pointer");
   const bool eu = ge_next != nullptr;
-  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && gz1e && st_e && lb_e && PDG_ALIGNED(a2e) &&
+  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && gz1e && st_e && (lb_e || pairs_e) && PDG_ALIGNED(a2e) &&
                         PDG_ALIGNED(a1e) && PDG_ALIGNED(gz1e)),
                 "pdg_edge_bwd_w2: edge-update arguments missing or misaligned");
   const size_t shm = eu ? 4 * EBW_IMG + 2 * EBW_MASK : 2 * EBW_IMG + EBW_MASK;
   if (eu)
     hipLaunchKernelGGL(edge_bwd_w2_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, dst,
                        gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, gz1m, gz1e, gC, slabs,
-                       n_edges);
+                       n_edges, pairs_m, npairs_m, pairs_e, npairs_e);
   else
     hipLaunchKernelGGL(edge_bwd_w2_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, dst,
                        gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, gz1m, gz1e, gC, slabs,
-                       n_edges);
+                       n_edges, pairs_m, npairs_m, pairs_m, npairs_m);
   PDG_CHECK_LAUNCH("pdg_edge_bwd_w2");
   return PDG_OK;
 }
 
 extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
                                 float* ge_out, float* slabs, int nslabs, const float* a2ln, const pdg_ln_stat* st_ln,
-                                double* ln_partials, void* stream) {
+                                double* ln_partials, const float* ln_g, double* pairs, int accumulate, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_gout_wc: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_gout_wc: bad slabs");
   PDG_CHECK_ARG(gC && e && WcT && ge_out, "pdg_edge_gout_wc: null argument");
@@ -481,13 +488,15 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
                 "pdg_edge_gout_wc: misaligned pointer");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_gout_wc: ge_out must not alias ge_next");
   PDG_CHECK_ARG(!a2ln || (PDG_ALIGNED(a2ln) && st_ln && ln_partials), "pdg_edge_gout_wc: LayerNorm column-sum arguments");
-  const size_t shm = 2 * EBW_IMG + (size_t)EBW_THREADS / 32 * 2 * L * sizeof(double);   // >= the row tile
+  PDG_CHECK_ARG(!pairs || (a2ln && ln_g), "pdg_edge_gout_wc: pairs need a2ln and ln_g");
+  // LDS: the two images, then (LayerNorm column sums) the row groups' sums + one row + its scratch
+  const size_t shm = 2 * EBW_IMG + ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
   if (ge_next)
     hipLaunchKernelGGL(edge_gout_wc_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges);
+                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
   else
     hipLaunchKernelGGL(edge_gout_wc_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges);
+                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
   PDG_CHECK_LAUNCH("pdg_edge_gout_wc");
   return PDG_OK;
 }

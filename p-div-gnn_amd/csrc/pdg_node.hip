@@ -61,6 +61,30 @@ __device__ __forceinline__ void store_tile(float* __restrict__ xb, int lt, const
 
 __device__ __forceinline__ int nu_tile(int i) { return xcd_block() + i * (int)gridDim.x; }
 
+// LayerNorm-backward column partials accumulated by the compute waves (the pdg_ln_colsum layout:
+// [sum gy (128) | sum gy*xhat (128)] per block): lane (r, q) of wave w holds fp64 sums for
+// features 16w + 4q + c over the rows it produced.  The 16 lanes of each q are added with a
+// fixed xor butterfly and lane r = 0 writes the block's entries to `row` (LDS; every feature has
+// one owner).
+__device__ __forceinline__ void write_ln_partials(double (&sg)[4], double (&sx)[4], double* row) {
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      sg[c] += __shfl_xor(sg[c], off);
+      sx[c] += __shfl_xor(sx[c], off);
+    }
+  const int l = lane_id();
+  if ((l & 15) == 0) {
+    const int f = 16 * wave_id() + 4 * (l >> 4);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      row[f + c] = sg[c];
+      row[L + f + c] = sx[c];
+    }
+  }
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
@@ -230,7 +254,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
     const pdg_ln_stat* __restrict__ stp, const pdg_ln_bwd* __restrict__ lbp, const float* __restrict__ lg,
     const float* __restrict__ W2T, const float* __restrict__ W1aT, const float* __restrict__ W1bT,
     float* __restrict__ gz2_out, float* __restrict__ gz1_out, float* __restrict__ gaggr,
-    float* __restrict__ gx_part) {
+    float* __restrict__ gx_part, const double* __restrict__ lb_pairs, int lb_npairs) {
   __shared__ __attribute__((aligned(16))) float gz2t[3 * TILE * GS];
   __shared__ __attribute__((aligned(16))) float gz1t[2 * TILE * GS];
   const int w = wave_id(), l = lane_id();
@@ -238,7 +262,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
   const int ntiles = tiles_of(N);
   const int lt = threadIdx.x - 64 * NU_COMPUTE;
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
-  const pdg_ln_bwd lb = *lbp;
+  const pdg_ln_bwd lb = lnb_resolve(lbp, lb_pairs, lb_npairs, stp);
   const int r = l & 15, q = l >> 4;
   const int oc = 16 * w + 4 * q;   // this lane's 4 output features (D rows 4q .. 4q+3 of block w)
   f32x4 w2f[8], waf[8], wbf[8];
@@ -316,9 +340,10 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
 
 extern "C" int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, const float* a1n, const pdg_ln_stat* st,
                             const pdg_ln_bwd* lb, const float* ln_g, const float* Wn2T, const float* Wn1aT,
-                            const float* Wn1bT, float* gz2, float* gz1, float* gaggr, float* gx_part, void* stream) {
+                            const float* Wn1bT, float* gz2, float* gz1, float* gaggr, float* gx_part,
+                            const double* lb_pairs, int lb_npairs, void* stream) {
   PDG_CHECK_ARG(n_nodes > 0, "pdg_node_bwd: n_nodes must be > 0");
-  PDG_CHECK_ARG(gy && a2n && a1n && st && lb && ln_g && gz2 && gz1 && gaggr && gx_part,
+  PDG_CHECK_ARG(gy && a2n && a1n && st && (lb || lb_pairs) && ln_g && gz2 && gz1 && gaggr && gx_part,
                 "pdg_node_bwd: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2n) && PDG_ALIGNED(a1n) && PDG_ALIGNED(Wn2T) &&
                     PDG_ALIGNED(Wn1aT) && PDG_ALIGNED(Wn1bT) && PDG_ALIGNED(gz2) && PDG_ALIGNED(gz1) &&
@@ -328,7 +353,7 @@ extern "C" int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, cons
   const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
   const int grid = tiles < cap ? tiles : cap;
   hipLaunchKernelGGL(node_bwd_kernel, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes, gy, a2n, a1n,
-                     st, lb, ln_g, Wn2T, Wn1aT, Wn1bT, gz2, gz1, gaggr, gx_part);
+                     st, lb, ln_g, Wn2T, Wn1aT, Wn1bT, gz2, gz1, gaggr, gx_part, lb_pairs, lb_npairs);
   PDG_CHECK_LAUNCH("pdg_node_bwd");
   return PDG_OK;
 }
@@ -488,11 +513,17 @@ extern "C" int pdg_node_pq_rw_fin(int n_nodes, const float* a2_prev, const doubl
 
 // ============================================================================ summed transposed GEMMs
 // out = W0T in0 + W1T in1 [+ res] (the input gradient of x through P = Wa x, Q = Wb x plus the
-// node_net path), weights held in registers; bitwise pdg_gemm_sum2.
+// node_net path), weights held in registers; bitwise pdg_gemm_sum2.  COLS: also the column
+// partials (pdg_ln_colsum layout) of the backward of the LayerNorm LN(ln_a2) whose upstream
+// gradient is `out` (x_{t} = LN(a2n_{t-1}) + x_{t-1}: the node LayerNorm of the previous step).
+template <bool COLS>
 __global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
     int N, const float* __restrict__ in0, const float* __restrict__ in1, const float* __restrict__ W0T,
-    const float* __restrict__ W1T, const float* __restrict__ res, float* __restrict__ out) {
+    const float* __restrict__ W1T, const float* __restrict__ res, float* __restrict__ out,
+    const float* __restrict__ ln_a2, const pdg_ln_stat* __restrict__ ln_st, double* __restrict__ cpart,
+    const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate) {
   __shared__ __attribute__((aligned(16))) float xin[3 * XBUF];
+  __shared__ double crow[COLS ? 256 : 1], ctmp[COLS ? 256 : 1];
   const int w = wave_id(), l = lane_id();
   const bool loader = w >= NU_COMPUTE;
   const int ntiles = tiles_of(N);
@@ -500,6 +531,13 @@ __global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
   const int r = l & 15, q = l >> 4;
   const int oc = 16 * w + 4 * q;
   f32x4 wf[16];
+  double csg[4] = {0, 0, 0, 0}, csx[4] = {0, 0, 0, 0};
+  float mean = 0.f, den = 1.f, rstd = 1.f;
+  if (COLS) {
+    mean = ln_st->mean;
+    den = ln_st->den;
+    rstd = ln_st->rstd;
+  }
   if (!loader) {
     const float* p0 = W0T + (size_t)(16 * w + r) * L + 4 * q;
     const float* p1 = W1T + (size_t)(16 * w + r) * L + 4 * q;
@@ -530,6 +568,8 @@ __global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
       const int rc = row < N ? row : N - 1;
       f32x4 rv = {0.f, 0.f, 0.f, 0.f};
       if (res) rv = *reinterpret_cast<const f32x4*>(res + (size_t)rc * L + oc);
+      f32x4 av;
+      if (COLS) av = *reinterpret_cast<const f32x4*>(ln_a2 + (size_t)rc * L + oc);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       const float* xr = xin + (i % 3) * XBUF + r * XS + 4 * q;
 #pragma unroll
@@ -539,15 +579,32 @@ __global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
         for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[T][jj], bv[jj], acc, 0, 0, 0);
       }
       if (res) acc += rv;
-      if (row < N) *reinterpret_cast<f32x4*>(out + (size_t)row * L + oc) = acc;
+      if (row < N) {
+        *reinterpret_cast<f32x4*>(out + (size_t)row * L + oc) = acc;
+        if (COLS) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {   // the pdg_ln_colsum formulas
+            const float xhat = div_den(av[c] - mean, den, rstd);
+            csg[c] += (double)acc[c];
+            csx[c] += (double)(acc[c] * xhat);
+          }
+        }
+      }
     }
     __syncthreads();
     if (loader && ahead) store_tile(xin + ((i + 2) % 3) * XBUF, lt, tr);   // last read in iteration i - 1
   }
+  if (COLS) {
+    if (!loader) write_ln_partials(csg, csx, crow);
+    __syncthreads();
+    lnb_emit(crow, ln_g, cpart, accumulate, pairs, ctmp);
+  }
 }
 
 extern "C" int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
-                                const float* res, float* out, void* stream) {
+                                const float* res, float* out, const float* ln_a2, const pdg_ln_stat* ln_st,
+                                double* partials, int* nparts, const float* ln_g, double* pairs, int accumulate,
+                                void* stream) {
   PDG_CHECK_ARG(rows > 0, "pdg_gemm_sum2_rw: rows must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(in0) && PDG_ALIGNED(in1) && PDG_ALIGNED(out) && PDG_ALIGNED(W0T) && PDG_ALIGNED(W1T) &&
                     PDG_ALIGNED(res),
@@ -555,8 +612,16 @@ extern "C" int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, co
   const int tiles = tiles_of(rows);
   const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
   const int grid = tiles < cap ? tiles : cap;
-  hipLaunchKernelGGL(gemm_sum2_rw_kernel, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, rows, in0, in1, W0T,
-                     W1T, res, out);
+  if (partials) {
+    PDG_CHECK_ARG(ln_a2 && ln_st && PDG_ALIGNED(ln_a2) && PDG_ALIGNED(partials) && (!pairs || ln_g),
+                  "pdg_gemm_sum2_rw: column partials need an aligned ln_a2, ln_st (and ln_g for pairs)");
+    hipLaunchKernelGGL(gemm_sum2_rw_kernel<true>, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, rows, in0,
+                       in1, W0T, W1T, res, out, ln_a2, ln_st, partials, ln_g, pairs, accumulate);
+  } else {
+    hipLaunchKernelGGL(gemm_sum2_rw_kernel<false>, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, rows, in0,
+                       in1, W0T, W1T, res, out, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+  }
   PDG_CHECK_LAUNCH("pdg_gemm_sum2_rw");
+  if (nparts) *nparts = grid;
   return PDG_OK;
 }

@@ -94,6 +94,13 @@ class EPDEngine:
         self._part_a = torch.empty(self.max_blocks * 2, **f64)
         self._part_b = torch.empty(self.max_blocks * 2, **f64)
         self._part_col = torch.empty(self.max_blocks * 256, **f64)
+        # LayerNorm backward (no finalize launches, pdg_ln_colsum in include/pdivgnn.h): per-block
+        # column accumulators of the 4 LayerNorm parameter groups (node_net, edge_net, node and edge
+        # encoder), rows <= the largest producer grid (2 x CUs), zeroed once per backward
+        self._acc_rows = min(2 * torch.cuda.get_device_properties(self.device).multi_processor_count,
+                             self.max_blocks)
+        self._ln_acc = torch.zeros(4, self._acc_rows * 256, **f64)
+        self._sync_pairs = torch.zeros(8, 2, **f64)
         self._part_narrow = torch.empty(self.max_blocks * (L * 6 + L + 6), **f64)
         self._nparts = ctypes.c_int(0)
         # one weight-gradient slab per block of pdg_wgrad_segments: three blocks per CU
@@ -134,14 +141,6 @@ class EPDEngine:
         lib.pdg_ln_partials_sum(part.data_ptr(), self._nparts.value, self._pair.data_ptr(), s)
         torch.distributed.all_reduce(self._pair, group=group)
         lib.pdg_ln_finalize(self._pair.data_ptr(), 1, float((e_glob if edges else n_glob) * L), out_ptr, s)
-
-    def _sync_bwd(self, lb_buf: "_StatBuf", i: int, st_ptr: int, s) -> None:
-        """Sync mode: all-reduce S1/S2 of backward scalar set i, then recompute c1/c2."""
-        if self.sync is None:
-            return
-        o = i * lb_buf.nbytes + 8               # pdg_ln_bwd: {float c1, c2; double S1, S2}
-        torch.distributed.all_reduce(lb_buf.buf[o:o + 16].view(torch.float64), group=self.sync[0])
-        lib.pdg_ln_bwd_rescale(st_ptr, lb_buf[i], s)
 
     def set_sync(self, group, n_nodes_global: int = 0, n_edges_global: int = 0) -> None:
         """Enable (group given) or disable (None) the exact data-parallel LayerNorm: every
@@ -288,30 +287,43 @@ class EPDEngine:
         np_ = ctypes.byref(self._nparts)
         T = self.transposed(P)
         st = ctx.stats
-        lb = _StatBuf(4, LN_BWD_BYTES, self.device)
         segs: dict[str, list] = {k: [] for k in ("W2", "Wc", "Wa", "Wb", "Wn2", "Wn1a", "Wn1b", "d1", "ne2", "ee2")}
         fused = self.fused_edge_wgrad
         if fused:
             nse = self._nslabs_e
             slabs_w2 = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
             slabs_wc = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
-            part_e = torch.empty((nse + 1) * 2 * L, dtype=torch.float64, device=self.device)
+        # LayerNorm backward scalars without finalize launches: every column-sum producer adds its
+        # per-block rows into the group accumulator and writes per-block (S1, S2) pairs; the consumer
+        # kernel reduces the pairs (include/pdivgnn.h, pdg_ln_colsum)
+        acc = self._ln_acc
+        acc.zero_()
+        ACC_N, ACC_E, ACC_NE, ACC_EE = (acc[i] for i in range(4))
+        S = ctx.steps
+        pairs = torch.empty(3 * S + 2, self.max_blocks * 2, dtype=torch.float64, device=self.device)
+        PN, PM, PE = (lambda t: pairs[t]), (lambda t: pairs[S + t]), (lambda t: pairs[2 * S + t])
+        P_NENC, P_EENC = pairs[3 * S], pairs[3 * S + 1]
+        g_node, g_edge = P["processor.node_net.4.weight"], P["processor.edge_net.4.weight"]
+        sync_slot = [0]
 
-        def colsum(rows, gy_rows, gidx, a2, st_ptr, gname, bname, lb_i):
-            lib.pdg_ln_colsum(rows, _p(gy_rows), _p(gidx), _p(a2), st_ptr, _p(self._part_col), np_, s)
-            lib.pdg_ln_colsum_finalize(_p(self._part_col), self._nparts.value, _p(P[gname]), st_ptr,
-                                       _p(G[gname]), _p(G[bname]), lb[lb_i], s)
-            self._sync_bwd(lb, lb_i, st_ptr, s)
+        def src(pp, n):
+            """(pairs pointer, count) for a consumer; sync DP mode reduces them first and
+            all-reduces the (S1, S2) pair over the ranks (global-minibatch LayerNorm)."""
+            if self.sync is None:
+                return _p(pp), n
+            out = self._sync_pairs[sync_slot[0] % 8]
+            sync_slot[0] += 1
+            lib.pdg_ln_partials_sum(_p(pp), n, _p(out), s)
+            torch.distributed.all_reduce(out, group=self.sync[0])
+            return _p(out), 1
 
-        def colsum_e(rows, gy_rows, a2, st_ptr, gname, bname, lb_i):
-            """Column sums of the LayerNorm that produced an edge state e: fused mode takes the
-            partials pdg_edge_gout_wc wrote while producing gy_rows = d loss / d e."""
+        def edge_ln_pairs(pp, gy_rows, a2, st_ptr, accb, g):
+            """Pairs of the LayerNorm that produced an edge state e: fused mode has them from
+            pdg_edge_gout_wc (written while producing gy_rows = d loss / d e)."""
             if not fused:
-                colsum(rows, gy_rows, None, a2, st_ptr, gname, bname, lb_i)
-                return
-            lib.pdg_ln_colsum_finalize(_p(part_e), nse, _p(P[gname]), st_ptr, _p(G[gname]), _p(G[bname]),
-                                       lb[lb_i], s)
-            self._sync_bwd(lb, lb_i, st_ptr, s)
+                lib.pdg_ln_colsum(E, _p(gy_rows), None, _p(a2), st_ptr, _p(accb), np_, _p(g), _p(pp), 1, s)
+                return pp, self._nparts.value
+            return pp, nse
 
         gy = gy.contiguous()
         if ctx.scale_output:
@@ -330,7 +342,14 @@ class EPDEngine:
         ge_bufs = [self._empty(E, L), self._empty(E, L)]
         gC_fused = self._empty(E, L) if fused else None
         gx_next = gx
-        for t in reversed(range(ctx.steps)):
+        # node LayerNorm of the last step (upstream gradient: the decoder's); for the earlier steps
+        # the previous iteration's pdg_gemm_sum2_rw produces these partials
+        dl = ctx.per_step[S - 1]
+        lib.pdg_ln_colsum(N, _p(gx_next), None, _p(dl["a2n"]), st[dl["i_n"]], _p(ACC_N), np_, _p(g_node),
+                          _p(PN(S - 1)), 1, s)
+        n_node = self._nparts.value
+        n_edge = 0
+        for t in reversed(range(S)):
             d = ctx.per_step[t]
             eu = d["eu"]
             assert eu == (ge_next is not None)
@@ -339,43 +358,51 @@ class EPDEngine:
             gz2m = None if fused else self._empty(E, L)
             gz2e = self._empty(E, L) if (eu and not fused) else None
             ge_out = ge_bufs[t % 2]
-            # node_net tail: n_t = LN_n(a2n_t), gy = gx_next   (x_{t+1} = n_t + x_t)
-            colsum(N, gx_next, None, d["a2n"], st[d["i_n"]], "processor.node_net.4.weight",
-                   "processor.node_net.4.bias", 0)
-            self._t("node_bwd", lib.pdg_node_bwd, N, _p(gx_next), _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], lb[0],
-                    _p(P["processor.node_net.4.weight"]), _p(T["Wn2T"]), _p(T["Wn1aT"]), _p(T["Wn1bT"]),
-                    _p(gz2n), _p(gz1n), _p(gaggr), _p(gx_part), s)
-            # edge_net LayerNorm sums.  message: gy = gaggr[dst], reduced per node from the forward's
-            # sum of xhat over each destination segment; edge update: gy = ge_next (per edge)
-            lib.pdg_ln_colsum_nodes(N, _p(gaggr), _p(plan.rowptr_dst), _p(d["xs"]), _p(self._part_col), np_, s)
-            lib.pdg_ln_colsum_finalize(_p(self._part_col), self._nparts.value, _p(P["processor.edge_net.4.weight"]),
-                                       st[d["i_m"]], _p(G["processor.edge_net.4.weight"]),
-                                       _p(G["processor.edge_net.4.bias"]), lb[1], s)
-            self._sync_bwd(lb, 1, st[d["i_m"]], s)
-            if eu:
-                colsum_e(E, ge_next, d["a2e"], st[d["i_e"]], "processor.edge_net.4.weight",
-                         "processor.edge_net.4.bias", 2)
+            # node_net backward (n_t = LN_n(a2n_t), gy = gx_next; x_{t+1} = n_t + x_t)
+            pn, nn = src(PN(t), n_node)
+            self._t("node_bwd", lib.pdg_node_bwd, N, _p(gx_next), _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], None,
+                    _p(g_node), _p(T["Wn2T"]), _p(T["Wn1aT"]), _p(T["Wn1bT"]), _p(gz2n), _p(gz1n), _p(gaggr),
+                    _p(gx_part), pn, nn, s)
+            # message LayerNorm: gy = gaggr[dst], summed per node with the forward's sum of xhat
+            lib.pdg_ln_colsum_nodes(N, _p(gaggr), _p(plan.rowptr_dst), _p(d["xs"]), _p(ACC_E), np_, _p(g_edge),
+                                    _p(PM(t)), 1, s)
+            pm, nm = src(PM(t), self._nparts.value)
+            pe, ne = None, 0
+            if eu:   # edge-update LayerNorm: gy = ge_next (per edge)
+                pp, n_e = edge_ln_pairs(PE(t), ge_next, d["a2e"], st[d["i_e"]], ACC_E, g_edge)
+                pe, ne = src(pp, n_e if not fused else n_edge)
             if fused:
                 self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
                         _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
-                        st[d["i_e"]] if eu else None, lb[1], lb[2] if eu else None,
-                        _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(gz1m), _p(gz1e if eu else None),
-                        _p(gC), _p(slabs_w2), nse, s)
-                # + the column sums of the LayerNorm that produced e_t (LN_e of step t-1, or the encoder's)
-                a2ln, st_ln = ((ctx.per_step[t - 1]["a2e"], st[ctx.per_step[t - 1]["i_e"]]) if t > 0
-                               else (ctx.a2_ee, st[1]))
+                        st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
+                        _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, s)
+                # + the column sums / pairs of the LayerNorm that produced e_t (LN_e of step t-1, or the
+                # edge encoder's)
+                if t > 0:
+                    a2ln, st_ln, accb, gl, pp = (ctx.per_step[t - 1]["a2e"], st[ctx.per_step[t - 1]["i_e"]], ACC_E,
+                                                 g_edge, PE(t - 1))
+                else:
+                    a2ln, st_ln, accb, gl, pp = ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"], P_EENC
                 self._t("edge_gout", lib.pdg_edge_gout_wc, E, _p(gC), _p(d["e"]), _p(ge_next), _p(T["WcT"]),
-                        _p(ge_out), _p(slabs_wc), nse, _p(a2ln), st_ln, _p(part_e), s)
+                        _p(ge_out), _p(slabs_wc), nse, _p(a2ln), st_ln, _p(accb), _p(gl), _p(pp), 1, s)
+                n_edge = nse
             else:
                 self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr),
                         _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
-                        st[d["i_e"]] if eu else None, lb[1], lb[2] if eu else None,
-                        _p(P["processor.edge_net.4.weight"]), _p(T["W2T"]), _p(T["WcT"]), _p(gz2m), _p(gz1m),
-                        _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), s)
+                        st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(T["WcT"]),
+                        _p(gz2m), _p(gz1m), _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), pm, nm, pe, ne, s)
             self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
                     _p(plan.perm_src), _p(gz1m), _p(gz1e if eu else None), _p(gP), _p(gQ), s)
+            # gx_t, with the column sums / pairs of the LayerNorm whose output it is the gradient of:
+            # the node LayerNorm of step t-1, or the node encoder's
+            if t > 0:
+                a2n_prev, st_prev, accb, gl, pp = (ctx.per_step[t - 1]["a2n"], st[ctx.per_step[t - 1]["i_n"]], ACC_N,
+                                                   g_node, PN(t - 1))
+            else:
+                a2n_prev, st_prev, accb, gl, pp = ctx.a2_ne, st[0], ACC_NE, P["node_encoder.4.weight"], P_NENC
             self._t("gemm_sum2", lib.pdg_gemm_sum2_rw, N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part),
-                    _p(gx_t), s)
+                    _p(gx_t), _p(a2n_prev), st_prev, _p(accb), np_, _p(gl), _p(pp), 1, s)
+            n_node = self._nparts.value
             if not fused:
                 segs["W2"].append((gz2m, d["a1m"], E))
                 if eu:
@@ -390,19 +417,26 @@ class EPDEngine:
             ge_next = ge_out
         # encoders
         gz2, gz1 = self._empty(N, L), self._empty(N, L)
-        colsum(N, gx_next, None, ctx.a2_ne, st[0], "node_encoder.4.weight", "node_encoder.4.bias", 3)
-        lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], lb[3],
-                         _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), s)
+        pn, nn = src(P_NENC, n_node)
+        lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], None,
+                         _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), pn, nn, s)
         segs["ne2"].append((gz2, ctx.a1_ne, N))
         lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
                              _p(G["node_encoder.0.bias"]), None, s)
         gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
-        colsum_e(E, ge_next, ctx.a2_ee, st[1], "edge_encoder.4.weight", "edge_encoder.4.bias", 3)
-        lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], lb[3],
-                         _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), s)
+        pp, n_e = edge_ln_pairs(P_EENC, ge_next, ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"])
+        pe, ne = src(pp, n_e if not fused else n_edge)
+        lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], None,
+                         _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), pe, ne, s)
         segs["ee2"].append((gz2e_, ctx.a1_ee, E))
         lib.pdg_wgrad_narrow(E, _p(gz1e_), _p(ctx.e_in), 1, 0, _p(self._part_narrow), _p(G["edge_encoder.0.weight"]),
                              _p(G["edge_encoder.0.bias"]), None, s)
+        # LayerNorm weight / bias gradients: one launch over the four accumulators
+        names = ("processor.node_net.4", "processor.edge_net.4", "node_encoder.4", "edge_encoder.4")
+        lib.pdg_ln_param_grads(4, (ctypes.c_void_p * 4)(*[_p(acc[i]) for i in range(4)]),
+                               (ctypes.c_int * 4)(*([self._acc_rows] * 4)),
+                               (ctypes.c_void_p * 4)(*[_p(G[n + ".weight"]) for n in names]),
+                               (ctypes.c_void_p * 4)(*[_p(G[n + ".bias"]) for n in names]), s)
         # deferred weight gradients: one segmented pass + slab reduction per shared weight block
         red = [
             ("W2", "processor.edge_net.2.weight", L, 0, "processor.edge_net.2.bias"),

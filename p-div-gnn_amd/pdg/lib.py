@@ -41,20 +41,21 @@ SIGNATURES: dict[str, list] = {
     "pdg_decoder_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
     "pdg_any_nonzero": [P, c_int64, P, P],
     "pdg_decoder_bwd": [I, P, P, P, P, P, P, P],
-    "pdg_ln_colsum": [I, P, P, P, P, P, P, P],
-    "pdg_ln_colsum_nodes": [I, P, P, P, P, P, P],
+    "pdg_ln_colsum": [I, P, P, P, P, P, P, P, P, I, P],
+    "pdg_ln_colsum_nodes": [I, P, P, P, P, P, P, P, I, P],
     "pdg_ln_colsum_finalize": [P, I, P, P, P, P, P, P],
-    "pdg_mlp2_bwd": [I, P, P, P, P, P, P, P, P, P, P, P],
-    "pdg_node_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdg_ln_param_grads": [I, P, P, P, P, P],
+    "pdg_mlp2_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, I, P],
+    "pdg_node_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_dual": [I, P, P, P, P, P, P, P, P],
     "pdg_gemm_sum2": [I, P, P, P, P, P, P, P],
-    "pdg_gemm_sum2_rw": [I, P, P, P, P, P, P, P],
-    "pdg_edge_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "pdg_gemm_sum2_rw": [I, P, P, P, P, P, P, P, P, P, P, P, P, I, P],
+    "pdg_edge_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P],
     "pdg_pq_scatter_bwd": [I, P, P, P, P, P, P, P, P],
     "pdg_wgrad_accum": [I, P, P, P, P, P, I, P],
     "pdg_wgrad_reduce": [P, I, P, I, I, P, P],
-    "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P],
-    "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P],
+    "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P, I, P],
+    "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P, P, I, P],
     "pdg_mesh_graph": [I, P, I, I, P, I, P, P, P, ctypes.c_long, P, P, ctypes.c_long, P],
     "pdg_mesh_graph_scratch_bytes": [I, I],
     "pdg_wgrad_segments": [I, P, P, P, P, I, P],

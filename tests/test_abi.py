@@ -91,3 +91,28 @@ def test_vector_statistics_are_refused():
         m.stats_tensor("cpu")
     m.mean_pos = torch.tensor(1.5)
     assert m.stats_tensor("cpu")[0] == 1.5
+
+
+def test_call_sites_match_signatures():
+    """Every direct call of a C-ABI entry point in the host code and the tests passes as many
+    arguments as the header declares (calls through lib.pdg_x(...) and engine._t(name, lib.pdg_x, ...)
+    without star-arguments), so a signature change cannot leave a stale call behind."""
+    import ast
+    from pdg.lib import SIGNATURES
+    files = list((ROOT / "p-div-gnn_amd").rglob("*.py")) + list((ROOT / "tests").glob("*.py")) + [ROOT / "bench.py"]
+    bad = []
+    for f in files:
+        tree = ast.parse(f.read_text())
+        for node in ast.walk(tree):
+            if not isinstance(node, ast.Call):
+                continue
+            fn, args = node.func, node.args
+            if isinstance(fn, ast.Attribute) and fn.attr == "_t" and len(args) >= 2:
+                fn, args = args[1], args[2:]
+            if not (isinstance(fn, ast.Attribute) and fn.attr in SIGNATURES):
+                continue
+            if any(isinstance(a, ast.Starred) for a in args):
+                continue
+            if len(args) != len(SIGNATURES[fn.attr]):
+                bad.append(f"{f.name}:{node.lineno} {fn.attr} {len(args)} != {len(SIGNATURES[fn.attr])}")
+    assert not bad, bad

@@ -134,7 +134,8 @@ def test_segment_sum_with_layernorm(env, N, E):
     gaggr = rnd(N, L)
     part = torch.empty(4096 * 256, dtype=torch.float64, device="cuda")
     n = ctypes.c_int(0)
-    lib.pdg_ln_colsum_nodes(N, gaggr.data_ptr(), rp_d.data_ptr(), xs.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
+    lib.pdg_ln_colsum_nodes(N, gaggr.data_ptr(), rp_d.data_ptr(), xs.data_ptr(), part.data_ptr(), ctypes.byref(n),
+                            None, None, 0, s)
     tot = part[: n.value * 256].view(n.value, 256).sum(0).cpu()
     gy = gaggr.double().cpu()[dst]
     assert rel(tot[:L], gy.sum(0)) < 1e-6
@@ -226,7 +227,8 @@ def test_ln_colsum_and_mlp2_bwd_vs_autograd(env):
     lib.pdg_mlp2_fwd(M, a1.data_ptr(), W.data_ptr(), b.data_ptr(), a2.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
     st = finalize(lib, s, part, n.value, M * L)
     gy = rnd(M, L)
-    lib.pdg_ln_colsum(M, gy.data_ptr(), None, a2.data_ptr(), st.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
+    lib.pdg_ln_colsum(M, gy.data_ptr(), None, a2.data_ptr(), st.data_ptr(), part.data_ptr(), ctypes.byref(n), None,
+                      None, 0, s)
     gg, gb = torch.zeros(L, device="cuda"), torch.zeros(L, device="cuda")
     lb = torch.zeros(24, dtype=torch.uint8, device="cuda")
     lib.pdg_ln_colsum_finalize(part.data_ptr(), n.value, g.data_ptr(), st.data_ptr(), gg.data_ptr(), gb.data_ptr(),
@@ -234,7 +236,23 @@ def test_ln_colsum_and_mlp2_bwd_vs_autograd(env):
     WT = W.T.contiguous()
     gz2, gz1 = torch.empty(M, L, device="cuda"), torch.empty(M, L, device="cuda")
     lib.pdg_mlp2_bwd(M, gy.data_ptr(), None, a2.data_ptr(), a1.data_ptr(), st.data_ptr(), lb.data_ptr(),
-                     g.data_ptr(), WT.data_ptr(), gz2.data_ptr(), gz1.data_ptr(), s)
+                     g.data_ptr(), WT.data_ptr(), gz2.data_ptr(), gz1.data_ptr(), None, 0, s)
+    # the launch-free form: the producer accumulates column rows and writes (S1, S2) pairs, the
+    # consumer reduces the pairs, pdg_ln_param_grads turns the accumulator into g / b gradients
+    acc = torch.zeros(4096 * 256, dtype=torch.float64, device="cuda")
+    pairs = torch.zeros(4096 * 2, dtype=torch.float64, device="cuda")
+    for rep in range(2):      # accumulate twice: the accumulator holds 2x the sums
+        lib.pdg_ln_colsum(M, gy.data_ptr(), None, a2.data_ptr(), st.data_ptr(), acc.data_ptr(), ctypes.byref(n),
+                          g.data_ptr(), pairs.data_ptr(), 1, s)
+    gz2p, gz1p = torch.empty(M, L, device="cuda"), torch.empty(M, L, device="cuda")
+    lib.pdg_mlp2_bwd(M, gy.data_ptr(), None, a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None,
+                     g.data_ptr(), WT.data_ptr(), gz2p.data_ptr(), gz1p.data_ptr(), pairs.data_ptr(), n.value, s)
+    assert rel(gz2p, gz2) < 1e-6 and rel(gz1p, gz1) < 1e-6
+    gg2, gb2 = torch.zeros(L, device="cuda"), torch.zeros(L, device="cuda")
+    P = ctypes.c_void_p
+    lib.pdg_ln_param_grads(1, (P * 1)(acc.data_ptr()), (ctypes.c_int * 1)(n.value), (P * 1)(gg2.data_ptr()),
+                           (P * 1)(gb2.data_ptr()), s)
+    assert rel(gg2, 2 * gg.double().cpu()) < 1e-6 and rel(gb2, 2 * gb.double().cpu()) < 1e-6
     # reference
     a1d = a1.double().cpu().requires_grad_(True)
     Wd, bd = W.double().cpu(), b.double().cpu()
@@ -356,14 +374,29 @@ def test_node_bwd_matches_separate_kernels(env, N):
     lb = torch.frombuffer(bytearray(struct.pack("ffdd", 0.013, -0.021, 1.0, 2.0)), dtype=torch.uint8).cuda()
     outs0 = [torch.empty(N, L, device="cuda") for _ in range(4)]
     lib.pdg_mlp2_bwd(N, gy.data_ptr(), None, a2.data_ptr(), a1.data_ptr(), st.data_ptr(), lb.data_ptr(),
-                     g.data_ptr(), W2T.data_ptr(), outs0[0].data_ptr(), outs0[1].data_ptr(), s)
+                     g.data_ptr(), W2T.data_ptr(), outs0[0].data_ptr(), outs0[1].data_ptr(), None, 0, s)
     lib.pdg_gemm_dual(N, outs0[1].data_ptr(), WaT.data_ptr(), WbT.data_ptr(), None, gy.data_ptr(),
                       outs0[2].data_ptr(), outs0[3].data_ptr(), s)
     outs1 = [torch.empty(N, L, device="cuda") for _ in range(4)]
     assert lib.pdg_node_bwd(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), lb.data_ptr(),
                             g.data_ptr(), W2T.data_ptr(), WaT.data_ptr(), WbT.data_ptr(), *[o.data_ptr() for o in outs1],
-                            s) == 0
+                            None, 0, s) == 0
     for a, b in zip(outs0, outs1):
+        assert torch.equal(a, b)
+    # the backward scalars from producer pairs instead of a finalized pdg_ln_bwd: dyadic pieces of
+    # (S1, S2) sum exactly, so c1 / c2 and therefore every output are bitwise those of lb
+    S1, S2 = 37.25, -12.5
+    M, sdv = float(N * L), sd
+    lb2 = torch.frombuffer(bytearray(struct.pack("ffdd", S1 / M, S2 / (M * sdv), S1, S2)), dtype=torch.uint8).cuda()
+    pairs = torch.tensor([[S1 / 2, S2 / 4], [S1 / 4, S2 / 2], [S1 / 4, S2 / 4]], dtype=torch.float64).cuda()
+    outs2, outs3 = ([torch.empty(N, L, device="cuda") for _ in range(4)] for _ in range(2))
+    assert lib.pdg_node_bwd(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), lb2.data_ptr(),
+                            g.data_ptr(), W2T.data_ptr(), WaT.data_ptr(), WbT.data_ptr(), *[o.data_ptr() for o in outs2],
+                            None, 0, s) == 0
+    assert lib.pdg_node_bwd(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None,
+                            g.data_ptr(), W2T.data_ptr(), WaT.data_ptr(), WbT.data_ptr(), *[o.data_ptr() for o in outs3],
+                            pairs.data_ptr(), 3, s) == 0
+    for a, b in zip(outs2, outs3):
         assert torch.equal(a, b)
 
 
@@ -396,12 +429,31 @@ def test_register_weight_kernels_match_lds_kernels(env, N, res):
     W1T, _ = lin(L, L)
     rr = rnd(N, L) if res else None
     o = []
-    for fn in (lib.pdg_gemm_sum2, lib.pdg_gemm_sum2_rw):
+    out = torch.empty(N, L, device="cuda")
+    assert lib.pdg_gemm_sum2(N, i0.data_ptr(), i1.data_ptr(), W0T.data_ptr(), W1T.data_ptr(),
+                             rr.data_ptr() if res else None, out.data_ptr(), s) == 0
+    o.append(out)
+    part = torch.zeros(lib.pdg_max_blocks() * 256, dtype=torch.float64, device="cuda")
+    pairs = torch.zeros(lib.pdg_max_blocks() * 2, dtype=torch.float64, device="cuda")
+    npart = ctypes.c_int(0)
+    for cols in (False, True):
         out = torch.empty(N, L, device="cuda")
-        assert fn(N, i0.data_ptr(), i1.data_ptr(), W0T.data_ptr(), W1T.data_ptr(), rr.data_ptr() if res else None,
-                  out.data_ptr(), s) == 0
+        assert lib.pdg_gemm_sum2_rw(N, i0.data_ptr(), i1.data_ptr(), W0T.data_ptr(), W1T.data_ptr(),
+                                    rr.data_ptr() if res else None, out.data_ptr(), a2.data_ptr() if cols else None,
+                                    st.data_ptr() if cols else None, part.data_ptr() if cols else None,
+                                    ctypes.byref(npart), g.data_ptr() if cols else None,
+                                    pairs.data_ptr() if cols else None, 0, s) == 0
         o.append(out)
-    assert torch.equal(o[0], o[1])
+    assert torch.equal(o[0], o[1]) and torch.equal(o[0], o[2])
+    # the LayerNorm column partials folded into the _rw kernel (pdg_ln_colsum formulas)
+    got = part[:npart.value * 256].view(-1, 256).sum(0).cpu()
+    gyv = o[0].double().cpu()
+    xhat = ((a2.double() - mean) / den).cpu()
+    ref = torch.cat([gyv.sum(0), (gyv * xhat).sum(0)])
+    assert rel(got, ref) < 1e-6
+    sp = pairs[:2 * npart.value].view(-1, 2).sum(0).cpu()
+    gd = g.double().cpu()
+    assert rel(sp, torch.stack([(gd * got[:L]).sum(), (gd * got[L:]).sum()])) < 1e-9
 
 
 @pytest.mark.parametrize("N,nparts,res", [(7, 1, True), (1031, 37, False), (40328, 256, True), (5000, 700, False)])
