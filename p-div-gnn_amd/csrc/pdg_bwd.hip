@@ -631,6 +631,9 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
 
 // ============================================================================ P/Q gather backward
 constexpr int PQ_U = 8;
+#ifndef PQ_CHUNK
+#define PQ_CHUNK 512
+#endif
 
 __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* __restrict__ rpd,
                                                              const int* __restrict__ rps,
@@ -640,7 +643,14 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* _
                                                              float* __restrict__ gP, float* __restrict__ gQ) {
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const int nhw = blockDim.x >> 5;
-  for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
+  // node order: chunks of PQ_CHUNK consecutive nodes dealt round-robin over the 8 XCDs (block b
+  // runs on XCD b & 7), so the source-side rows of a node (in its mesh neighbours' destination
+  // segments) are mostly read by the same XCD at about the same time
+  // (the launcher makes the grid a multiple of 8; v grows with i, so the first v >= N ends the loop)
+  const int x = blockIdx.x & 7, m = blockIdx.x >> 3, gx = gridDim.x >> 3;
+  for (int i = m * nhw + hw;; i += gx * nhw) {
+    const int v = ((i / PQ_CHUNK) * 8 + x) * PQ_CHUNK + i % PQ_CHUNK;
+    if (v >= N) break;
     f32x4 p = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
     // PQ_U rows in flight per round trip (loads past a segment's end re-read its last row and are
     // not accumulated): the sums are formed row by row in segment order as a serial loop would
@@ -690,7 +700,7 @@ extern "C" int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int*
                 "pdg_pq_scatter_bwd: misaligned pointer");
   long want = (n_nodes + 7) / 8;
   long cap = (long)device_cus() * 8;
-  const int grid = (int)(want < cap ? want : cap);
+  const int grid = (int)(((want < cap ? want : cap) + 7) / 8 * 8);   // a multiple of 8 (node order)
   hipLaunchKernelGGL(pq_scatter_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, rowptr_dst,
                      rowptr_src, perm_src, gz1m, gz1e, gP, gQ);
   PDG_CHECK_LAUNCH("pdg_pq_scatter_bwd");
