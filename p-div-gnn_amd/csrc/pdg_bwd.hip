@@ -635,7 +635,7 @@ constexpr int PQ_U = 8;
 #define PQ_CHUNK 512
 #endif
 
-__global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* __restrict__ rpd,
+__global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, int chunk, const int* __restrict__ rpd,
                                                              const int* __restrict__ rps,
                                                              const int* __restrict__ perm_s,
                                                              const float* __restrict__ gz1m,
@@ -649,7 +649,7 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, const int* _
   // (the launcher makes the grid a multiple of 8; v grows with i, so the first v >= N ends the loop)
   const int x = blockIdx.x & 7, m = blockIdx.x >> 3, gx = gridDim.x >> 3;
   for (int i = m * nhw + hw;; i += gx * nhw) {
-    const int v = ((i / PQ_CHUNK) * 8 + x) * PQ_CHUNK + i % PQ_CHUNK;
+    const int v = ((i / chunk) * 8 + x) * chunk + i % chunk;
     if (v >= N) break;
     f32x4 p = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
     // PQ_U rows in flight per round trip (loads past a segment's end re-read its last row and are
@@ -701,7 +701,8 @@ extern "C" int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int*
   long want = (n_nodes + 7) / 8;
   long cap = (long)device_cus() * 8;
   const int grid = (int)(((want < cap ? want : cap) + 7) / 8 * 8);   // a multiple of 8 (node order)
-  hipLaunchKernelGGL(pq_scatter_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, rowptr_dst,
+  const int chunk = PQ_CHUNK > 0 ? PQ_CHUNK : (n_nodes + 7) / 8;   // 0: one contiguous range per XCD
+  hipLaunchKernelGGL(pq_scatter_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, chunk, rowptr_dst,
                      rowptr_src, perm_src, gz1m, gz1e, gP, gQ);
   PDG_CHECK_LAUNCH("pdg_pq_scatter_bwd");
   return PDG_OK;

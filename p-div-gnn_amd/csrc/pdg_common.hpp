@@ -89,7 +89,11 @@ __device__ __forceinline__ f32x4 ld4(const float* __restrict__ p, int T) {
   return *reinterpret_cast<const f32x4*>(p + 16 * T);
 }
 __device__ __forceinline__ void st4(float* __restrict__ p, int T, const f32x4& x) {
+#if PDG_NT_ST
+  __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p + 16 * T));
+#else
   *reinterpret_cast<f32x4*>(p + 16 * T) = x;
+#endif
 }
 // Feature index of fragment element s in lane quarter q.
 __device__ __forceinline__ int frag_feature(int s, int q) { return 16 * (s >> 2) + 4 * q + (s & 3); }
@@ -346,7 +350,11 @@ __device__ __forceinline__ void load_frag(float (&v)[FRAG], const float* __restr
   const float* p = row + lane_col();
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
+#if PDG_NT_LD
+    const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 16 * t));
+#else
     const f32x4 x = ld4(p, t);
+#endif
     v[4 * t + 0] = x[0]; v[4 * t + 1] = x[1]; v[4 * t + 2] = x[2]; v[4 * t + 3] = x[3];
   }
 }
