@@ -630,11 +630,18 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
 }
 
 // ============================================================================ P/Q gather backward
-constexpr int PQ_U = 8;
+constexpr int PQ_U = 8;   // rows of each half in flight per node (6: 3 % slower; 12: spills)
 #ifndef PQ_CHUNK
 #define PQ_CHUNK 512
 #endif
 
+// Half-wave (32 lanes x 16 B) per node.  Both halves' first PQ_U rows of a node are in flight
+// together (row pointers -> destination rows and source permutation -> source rows: 3 dependent
+// round trips per node instead of 5), which also brings a node's destination-side and source-side
+// rows into the XCD's L2 at the same time: 405 -> 324 MB per launch at config 2 (algorithmic
+// 288 MB), 67.7 -> 62.2 us.  Loads past a segment's end re-read row / entry 0 and are not
+// accumulated, so every sum is formed row by row in segment order (destination rows, then source
+// rows) as a serial loop would.
 __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, int chunk, const int* __restrict__ rpd,
                                                              const int* __restrict__ rps,
                                                              const int* __restrict__ perm_s,
@@ -643,53 +650,65 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, int chunk, c
                                                              float* __restrict__ gP, float* __restrict__ gQ) {
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const int nhw = blockDim.x >> 5;
-  // node order: chunks of PQ_CHUNK consecutive nodes dealt round-robin over the 8 XCDs (block b
+  // node order: chunks of `chunk` consecutive nodes dealt round-robin over the 8 XCDs (block b
   // runs on XCD b & 7), so the source-side rows of a node (in its mesh neighbours' destination
   // segments) are mostly read by the same XCD at about the same time
-  // (the launcher makes the grid a multiple of 8; v grows with i, so the first v >= N ends the loop)
-  const int x = blockIdx.x & 7, m = blockIdx.x >> 3, gx = gridDim.x >> 3;
-  for (int i = m * nhw + hw;; i += gx * nhw) {
-    const int v = ((i / chunk) * 8 + x) * chunk + i % chunk;
-    if (v >= N) break;
-    f32x4 p = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
-    // PQ_U rows in flight per round trip (loads past a segment's end re-read its last row and are
-    // not accumulated): the sums are formed row by row in segment order as a serial loop would
-    const int d0 = rpd[v], d1 = rpd[v + 1];
-    for (int k = d0; k < d1; k += PQ_U) {   // edges whose target is v: message x_i, edge-update x[col]
-      f32x4 xm[PQ_U], xe[PQ_U];
+  // (the launcher makes the grid a multiple of 8; node_of grows with i, so the first v >= N ends)
+  const int x = blockIdx.x & 7, m = blockIdx.x >> 3, step = (gridDim.x >> 3) * nhw;
+  auto node_of = [&](int i) { return ((i / chunk) * 8 + x) * chunk + i % chunk; };
+  int i = m * nhw + hw;
+  int v = node_of(i);
+  if (v >= N) return;
+  int d0 = rpd[v], d1 = rpd[v + 1], s0 = rps[v], s1 = rps[v + 1];
+  int ks[PQ_U];
 #pragma unroll
-      for (int u = 0; u < PQ_U; ++u) {
-        const size_t kk = (size_t)(k + u < d1 ? k + u : d1 - 1) * L;
-        xm[u] = reinterpret_cast<const f32x4*>(gz1m + kk)[j];
-        if (gz1e) xe[u] = reinterpret_cast<const f32x4*>(gz1e + kk)[j];
-      }
+  for (int u = 0; u < PQ_U; ++u) ks[u] = perm_s[s0 + u < s1 ? s0 + u : 0];
+  for (;;) {
+    const int vn = node_of(i + step);
+    const bool more = vn < N;
+    f32x4 xm[PQ_U], xe[PQ_U], ym[PQ_U], ye[PQ_U];
 #pragma unroll
-      for (int u = 0; u < PQ_U; ++u) {
-        if (k + u >= d1) break;
-        p += xm[u];
-        if (gz1e) q += xe[u];
-      }
+    for (int u = 0; u < PQ_U; ++u) {
+      const size_t kk = (size_t)(d0 + u < d1 ? d0 + u : 0) * L;
+      xm[u] = reinterpret_cast<const f32x4*>(gz1m + kk)[j];
+      if (gz1e) xe[u] = reinterpret_cast<const f32x4*>(gz1e + kk)[j];
     }
-    const int s0 = rps[v], s1 = rps[v + 1];
-    for (int i = s0; i < s1; i += PQ_U) {   // edges whose source is v: message x_j, edge-update x[row]
-      int ks[PQ_U];
 #pragma unroll
-      for (int u = 0; u < PQ_U; ++u) ks[u] = perm_s[i + u < s1 ? i + u : s1 - 1];
-      f32x4 xm[PQ_U], xe[PQ_U];
+    for (int u = 0; u < PQ_U; ++u) {
+      const size_t kk = (size_t)ks[u] * L;
+      ym[u] = reinterpret_cast<const f32x4*>(gz1m + kk)[j];
+      if (gz1e) ye[u] = reinterpret_cast<const f32x4*>(gz1e + kk)[j];
+    }
+    f32x4 p = {0.f, 0.f, 0.f, 0.f}, q = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < PQ_U; ++u) {
-        xm[u] = reinterpret_cast<const f32x4*>(gz1m + (size_t)ks[u] * L)[j];
-        if (gz1e) xe[u] = reinterpret_cast<const f32x4*>(gz1e + (size_t)ks[u] * L)[j];
-      }
+    for (int u = 0; u < PQ_U; ++u) {
+      if (d0 + u >= d1) break;
+      p += xm[u];
+      if (gz1e) q += xe[u];
+    }
+    for (int k = d0 + PQ_U; k < d1; ++k) {   // destination segments longer than PQ_U
+      p += reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
+      if (gz1e) q += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+    }
 #pragma unroll
-      for (int u = 0; u < PQ_U; ++u) {
-        if (i + u >= s1) break;
-        q += xm[u];
-        if (gz1e) p += xe[u];
-      }
+    for (int u = 0; u < PQ_U; ++u) {
+      if (s0 + u >= s1) break;
+      q += ym[u];
+      if (gz1e) p += ye[u];
+    }
+    for (int k = s0 + PQ_U; k < s1; ++k) {   // source segments longer than PQ_U
+      const size_t kk = (size_t)perm_s[k] * L;
+      q += reinterpret_cast<const f32x4*>(gz1m + kk)[j];
+      if (gz1e) p += reinterpret_cast<const f32x4*>(gz1e + kk)[j];
     }
     reinterpret_cast<f32x4*>(gP + (size_t)v * L)[j] = p;
     reinterpret_cast<f32x4*>(gQ + (size_t)v * L)[j] = q;
+    if (!more) break;
+    i += step;
+    v = vn;
+    d0 = rpd[v]; d1 = rpd[v + 1]; s0 = rps[v]; s1 = rps[v + 1];
+#pragma unroll
+    for (int u = 0; u < PQ_U; ++u) ks[u] = perm_s[s0 + u < s1 ? s0 + u : 0];
   }
 }
 
@@ -701,7 +720,8 @@ extern "C" int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int*
   long want = (n_nodes + 7) / 8;
   long cap = (long)device_cus() * 8;
   const int grid = (int)(((want < cap ? want : cap) + 7) / 8 * 8);   // a multiple of 8 (node order)
-  const int chunk = PQ_CHUNK > 0 ? PQ_CHUNK : (n_nodes + 7) / 8;   // 0: one contiguous range per XCD
+  // 512-node chunks: contiguous per-XCD ranges (0) and 128 / 2,048 measured slower
+  const int chunk = PQ_CHUNK > 0 ? PQ_CHUNK : (n_nodes + 7) / 8;
   hipLaunchKernelGGL(pq_scatter_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, chunk, rowptr_dst,
                      rowptr_src, perm_src, gz1m, gz1e, gP, gQ);
   PDG_CHECK_LAUNCH("pdg_pq_scatter_bwd");

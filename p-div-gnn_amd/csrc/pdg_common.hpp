@@ -88,6 +88,12 @@ __device__ __forceinline__ int lane_col() { return opaque(4 * (lane_id() >> 4));
 __device__ __forceinline__ f32x4 ld4(const float* __restrict__ p, int T) {
   return *reinterpret_cast<const f32x4*>(p + 16 * T);
 }
+// Row stores are nontemporal (streamed past the caches' normal allocation): measured -0.08 ms per
+// config-2 step, all from pdg_segment_sum re-reading the edge forward's a2m rows; nontemporal
+// LOADS of whole rows made pdg_edge_fwd 4 % slower and are off.
+#ifndef PDG_NT_ST
+#define PDG_NT_ST 1
+#endif
 __device__ __forceinline__ void st4(float* __restrict__ p, int T, const f32x4& x) {
 #if PDG_NT_ST
   __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p + 16 * T));

@@ -192,11 +192,14 @@ def test_transpose_strided(env):
     assert torch.equal(out.cpu(), W[:, 2 * L:].T.contiguous().cpu())
 
 
-def test_pq_scatter_bwd(env):
+@pytest.mark.parametrize("N,E,isolated", [(300, 2500, 0), (300, 2500, 7), (5000, 30000, 3)])
+def test_pq_scatter_bwd(env, N, E, isolated):
+    """Heavy node (in-degree N/7 > the 8 rows kept in flight), random degrees, and `isolated`
+    trailing nodes with no edge at all (their row pointers equal E: nothing may be read there)."""
     lib, sh, _ = env
     s = sh()
-    N, E = 300, 2500
-    src, dst, rp = _csr(N, E, seed=3)
+    src, dst, rp = _csr(N - isolated, E, seed=3)
+    rp = torch.cat([rp, rp[-1:].expand(isolated)])
     key2 = src * N + dst
     perm_src = torch.sort(key2, stable=True).indices
     rps = torch.zeros(N + 1, dtype=torch.int64)
