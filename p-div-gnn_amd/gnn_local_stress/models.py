@@ -14,9 +14,10 @@ Mirrors the reference module's public surface (gnn_local_stress/models.py):
 * checkpoint helpers (:44-95) with the same dict keys.
 
 ``forward`` on a HIP device runs the whole stack through libpdivgnn_hip.so
-(pdg.engine); autograd is wired with one ``torch.autograd.Function`` whose
-backward is the HIP backward.  There is no silent fallback: on a CPU tensor
-the call raises (the CPU path of this repo is the test oracle, not product).
+(pdg.engine) as the ``torch.ops.pdivgnn.epd_forward`` custom op (pdg.ops), whose
+registered autograd backward is the HIP backward.  There is no silent fallback:
+on a CPU tensor the call raises (the CPU path of this repo is the test oracle,
+not product).
 """
 from __future__ import annotations
 
@@ -26,6 +27,7 @@ from typing import Optional
 import torch
 from torch.nn import Linear, Sequential
 
+from pdg import ops
 from pdg.engine import PARAM_NAMES, EPDEngine
 from pdg.graph import Data
 from pdg.plan import plan_for
@@ -152,31 +154,6 @@ class Processor(torch.nn.Module):
                                    Linear(latent_size, latent_size), torch.nn.ReLU(), GraphLayerNorm(latent_size))
 
 
-class _EPDFunction(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, model, plan, stats8, scale_output, scale_input, pos, mean_stress, nodes_types, edge_attr,
-                *params):
-        P = dict(zip(PARAM_NAMES, params))
-        y, fctx = model._engine_for(pos.device).forward(
-            P, stats8, plan, pos, mean_stress, nodes_types, edge_attr, model.message_passing_steps,
-            scale_input, scale_output, True)
-        ctx.fctx = fctx
-        ctx.model = model
-        ctx.save_for_backward(*params)
-        return y
-
-    @staticmethod
-    def backward(ctx, gy):
-        params = ctx.saved_tensors
-        P = dict(zip(PARAM_NAMES, params))
-        if ctx.fctx.scale_output:
-            P["_std_local_stress"] = ctx.model.std_local_stress
-        G = {n: torch.zeros_like(p) for n, p in zip(PARAM_NAMES, params)}
-        ctx.model._engine_for(gy.device).backward(P, ctx.fctx, gy, G)
-        ctx.fctx = None
-        return (None,) * 9 + tuple(G[n] for n in PARAM_NAMES)
-
-
 class EncodeProcessDecode(StressFieldBaseModel):
     """models.py:246-326."""
 
@@ -196,10 +173,13 @@ class EncodeProcessDecode(StressFieldBaseModel):
         self._engines: dict = {}
 
     def _engine_for(self, device) -> EPDEngine:
+        """This model's executor on ``device`` (its own scratch and data-parallel settings; the custom
+        op finds it by the key ops.register_engine returns)."""
         key = str(device)
         if key not in self._engines:
-            self._engines[key] = EPDEngine(device)
-        return self._engines[key]
+            eng = EPDEngine(device)
+            self._engines[key] = (ops.register_engine(eng), eng)
+        return self._engines[key][1]
 
     def stats_tensor(self, device) -> torch.Tensor:
         vals = []
@@ -228,24 +208,20 @@ class EncodeProcessDecode(StressFieldBaseModel):
         if not bool(flag.item()):   # models.py:294-299 (same host sync as the reference's torch.any)
             return Data(local_stress=torch.zeros_like(ms), edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)
         plan = plan_for(mesh_graph)
+        ops.register_plan(mesh_graph.edge_index, plan)
         params = [self.get_parameter(n) for n in PARAM_NAMES]
-        pos = mesh_graph.pos.float().contiguous()
-        ms = ms.float().contiguous()
-        types = mesh_graph.nodes_types.reshape(-1).to(torch.int64).contiguous()
-        ea = mesh_graph.edge_attr.reshape(-1).float().contiguous()
-        if not (torch.is_grad_enabled() and any(p.requires_grad for p in params)):
-            # inference (gnn_inference.py runs under no_grad): nothing is kept for a backward
-            P = dict(zip(PARAM_NAMES, params))
-            y, _ = self._engine_for(dev).forward(P, self.stats_tensor(dev), plan, pos, ms, types, ea,
-                                                 self.message_passing_steps, bool(scale_input),
-                                                 bool(scale_output), False)
-            return Data(local_stress=y, edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)
+        need_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         if torch.is_grad_enabled() and any(t.requires_grad for t in (mesh_graph.pos, mesh_graph.mean_stress,
                                                                       mesh_graph.edge_attr)):
             # the reference never differentiates w.r.t. the mesh inputs (gnn_train.py:159-205); the
             # HIP backward produces parameter gradients only, so refuse rather than return None
             raise NotImplementedError("EncodeProcessDecode (HIP path): gradients w.r.t. pos / mean_stress / "
                                       "edge_attr are not supported; detach the inputs")
-        y = _EPDFunction.apply(self, plan, self.stats_tensor(dev), bool(scale_output), bool(scale_input), pos, ms,
-                               types, ea, *params)
+        # inference (gnn_inference.py runs under no_grad) keeps nothing for a backward
+        self._engine_for(dev)
+        y, _handle = torch.ops.pdivgnn.epd_forward(params, self.stats_tensor(dev), mesh_graph.pos, ms,
+                                                   mesh_graph.nodes_types, mesh_graph.edge_attr,
+                                                   mesh_graph.edge_index, plan.n_nodes, self.message_passing_steps,
+                                                   bool(scale_input), bool(scale_output), need_grad,
+                                                   self._engines[str(dev)][0])
         return Data(local_stress=y, edge_index=mesh_graph.edge_index, pos=mesh_graph.pos)

@@ -116,3 +116,21 @@ def test_call_sites_match_signatures():
             if len(args) != len(SIGNATURES[fn.attr]):
                 bad.append(f"{f.name}:{node.lineno} {fn.attr} {len(args)} != {len(SIGNATURES[fn.attr])}")
     assert not bad, bad
+
+
+def test_custom_ops_registered_and_refuse_cpu():
+    """torch.library boundary (pdg/ops.py): the four ops exist with their schemas, and a CPU
+    tensor is refused before any HIP call (no CPU fallback)."""
+    import torch
+    from pdg import ops  # noqa: F401
+    for name in ("epd_forward", "epd_backward", "batch_loss", "batch_loss_backward"):
+        assert hasattr(torch.ops.pdivgnn, name), name
+    sch = str(torch.ops.pdivgnn.epd_forward.default._schema)
+    assert "Tensor[] params" in sch and "bool need_grad" in sch
+    z = torch.zeros(4, 2)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        torch.ops.pdivgnn.epd_forward([z], torch.zeros(8), z, torch.zeros(4, 3), torch.zeros(4, 1, dtype=torch.long),
+                                      torch.zeros(2), torch.zeros(2, 2, dtype=torch.long), 4, 1, True, True, False, 0)
+    with pytest.raises(RuntimeError, match="HIP device"):
+        torch.ops.pdivgnn.batch_loss(torch.zeros(4, 3), torch.zeros(4, 3), torch.tensor([0, 4]), None, None, None,
+                                     None, None, None, None, None, True, False, 1.0, False)
