@@ -155,8 +155,11 @@ class EPDEngine:
         N, E = plan.n_nodes, plan.n_edges
         if N == 0:
             raise ValueError("empty graph")
-        if E == 0:
-            raise ValueError("graphs without edges are not supported by the fused edge kernels")
+        # E == 0 (an edgeless batch): as in the reference, every message aggregate is zero
+        # (scatter of no rows), the edge branch produces empty tensors and the edge parameters get
+        # zero gradients; the edge kernels are skipped
+        if E == 0 and self.sync is not None:
+            raise ValueError("exact (sync) data parallelism needs edges on every rank's shard")
         np_ = ctypes.byref(self._nparts)
         ctx = FwdCtx(plan=plan, steps=steps, scale_output=scale_output)
         ctx.stats = _StatBuf(2 + 3 * steps, LN_STAT_BYTES, self.device)
@@ -172,10 +175,11 @@ class EPDEngine:
                             _p(self._part_a), np_, s)
         self._finalize(self._part_a, N * L, st[0], s)
         a1_ee, a2_ee = self._empty(E, L), self._empty(E, L)
-        lib.pdg_encoder_fwd(E, 1, _p(e_in), _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]),
-                            _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]), _p(a1_ee), _p(a2_ee),
-                            _p(self._part_a), np_, s)
-        self._finalize(self._part_a, E * L, st[1], s, True)
+        if E:
+            lib.pdg_encoder_fwd(E, 1, _p(e_in), _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]),
+                                _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]), _p(a1_ee), _p(a2_ee),
+                                _p(self._part_a), np_, s)
+            self._finalize(self._part_a, E * L, st[1], s, True)
         if need_grad:
             ctx.x_in, ctx.e_in, ctx.a1_ne, ctx.a2_ne, ctx.a1_ee, ctx.a2_ee = x_in, e_in, a1_ne, a2_ne, a1_ee, a2_ee
 
@@ -209,21 +213,26 @@ class EPDEngine:
             a1m = self._empty(E, L) if need_grad else None          # layer-1 outputs: backward only
             a2e = self._empty(E, L) if eu else None
             a1e = self._empty(E, L) if (eu and need_grad) else None
-            self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
-                    _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
-                    _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
-            if eu and self.sync is None:    # both edge LayerNorms in one launch
-                lib.pdg_ln_finalize2(self._part_a.data_ptr(), self._part_b.data_ptr(), self._nparts.value,
-                                     float(E * L), st[i_m], st[i_e], s)
-            else:
-                self._finalize(self._part_a, E * L, st[i_m], s, True)
-                if eu:
-                    self._finalize(self._part_b, E * L, st[i_e], s, True)
+            if E:
+                self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
+                        _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
+                        _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
+                if eu and self.sync is None:    # both edge LayerNorms in one launch
+                    lib.pdg_ln_finalize2(self._part_a.data_ptr(), self._part_b.data_ptr(), self._nparts.value,
+                                         float(E * L), st[i_m], st[i_e], s)
+                else:
+                    self._finalize(self._part_a, E * L, st[i_m], s, True)
+                    if eu:
+                        self._finalize(self._part_b, E * L, st[i_e], s, True)
             # aggregation (models.py:215-217) and node_net (:240-243)
-            aggr = self._empty(N, L)
-            xs = self._empty(N, L) if need_grad else None
-            self._t("segment_sum", lib.pdg_segment_sum, N, _p(plan.rowptr_dst), _p(a2m), st[i_m], _p(ge), _p(be),
-                    _p(aggr), _p(xs), s)
+            if E:
+                aggr = self._empty(N, L)
+                xs = self._empty(N, L) if need_grad else None
+                self._t("segment_sum", lib.pdg_segment_sum, N, _p(plan.rowptr_dst), _p(a2m), st[i_m], _p(ge),
+                        _p(be), _p(aggr), _p(xs), s)
+            else:
+                aggr = torch.zeros(N, L, dtype=torch.float32, device=self.device)
+                xs = torch.zeros(N, L, dtype=torch.float32, device=self.device) if need_grad else None
             a1n = self._empty(N, L) if need_grad else None
             a2n = self._empty(N, L)
             self._t("node_net", lib.pdg_node_net, N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(Wn2), _p(bn2), _p(a1n),
@@ -352,7 +361,7 @@ class EPDEngine:
         for t in reversed(range(S)):
             d = ctx.per_step[t]
             eu = d["eu"]
-            assert eu == (ge_next is not None)
+            assert E == 0 or eu == (ge_next is not None)
             gz2n, gz1n, gP, gQ = (self._empty(N, L) for _ in range(4))
             gC = gC_fused if fused else self._empty(E, L)   # fused: consumed within the step
             gz2m = None if fused else self._empty(E, L)
@@ -363,36 +372,40 @@ class EPDEngine:
             self._t("node_bwd", lib.pdg_node_bwd, N, _p(gx_next), _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], None,
                     _p(g_node), _p(T["Wn2T"]), _p(T["Wn1aT"]), _p(T["Wn1bT"]), _p(gz2n), _p(gz1n), _p(gaggr),
                     _p(gx_part), pn, nn, s)
-            # message LayerNorm: gy = gaggr[dst], summed per node with the forward's sum of xhat
-            lib.pdg_ln_colsum_nodes(N, _p(gaggr), _p(plan.rowptr_dst), _p(d["xs"]), _p(ACC_E), np_, _p(g_edge),
-                                    _p(PM(t)), 1, s)
-            pm, nm = src(PM(t), self._nparts.value)
-            pe, ne = None, 0
-            if eu:   # edge-update LayerNorm: gy = ge_next (per edge)
-                pp, n_e = edge_ln_pairs(PE(t), ge_next, d["a2e"], st[d["i_e"]], ACC_E, g_edge)
-                pe, ne = src(pp, n_e if not fused else n_edge)
-            if fused:
-                self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
-                        _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
-                        st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
-                        _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, s)
-                # + the column sums / pairs of the LayerNorm that produced e_t (LN_e of step t-1, or the
-                # edge encoder's)
-                if t > 0:
-                    a2ln, st_ln, accb, gl, pp = (ctx.per_step[t - 1]["a2e"], st[ctx.per_step[t - 1]["i_e"]], ACC_E,
-                                                 g_edge, PE(t - 1))
-                else:
-                    a2ln, st_ln, accb, gl, pp = ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"], P_EENC
-                self._t("edge_gout", lib.pdg_edge_gout_wc, E, _p(gC), _p(d["e"]), _p(ge_next), _p(T["WcT"]),
-                        _p(ge_out), _p(slabs_wc), nse, _p(a2ln), st_ln, _p(accb), _p(gl), _p(pp), 1, s)
-                n_edge = nse
+            if E == 0:             # no edge: P and Q feed nothing (models.py:215-222 on empty tensors)
+                gP.zero_()
+                gQ.zero_()
             else:
-                self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr),
-                        _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
-                        st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(T["WcT"]),
-                        _p(gz2m), _p(gz1m), _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), pm, nm, pe, ne, s)
-            self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
-                    _p(plan.perm_src), _p(gz1m), _p(gz1e if eu else None), _p(gP), _p(gQ), s)
+                # message LayerNorm: gy = gaggr[dst], summed per node with the forward's sum of xhat
+                lib.pdg_ln_colsum_nodes(N, _p(gaggr), _p(plan.rowptr_dst), _p(d["xs"]), _p(ACC_E), np_, _p(g_edge),
+                                        _p(PM(t)), 1, s)
+                pm, nm = src(PM(t), self._nparts.value)
+                pe, ne = None, 0
+                if eu:   # edge-update LayerNorm: gy = ge_next (per edge)
+                    pp, n_e = edge_ln_pairs(PE(t), ge_next, d["a2e"], st[d["i_e"]], ACC_E, g_edge)
+                    pe, ne = src(pp, n_e if not fused else n_edge)
+                if fused:
+                    self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
+                            _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
+                            st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
+                            _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, s)
+                    # + the column sums / pairs of the LayerNorm that produced e_t (LN_e of step t-1, or the
+                    # edge encoder's)
+                    if t > 0:
+                        a2ln, st_ln, accb, gl, pp = (ctx.per_step[t - 1]["a2e"], st[ctx.per_step[t - 1]["i_e"]], ACC_E,
+                                                     g_edge, PE(t - 1))
+                    else:
+                        a2ln, st_ln, accb, gl, pp = ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"], P_EENC
+                    self._t("edge_gout", lib.pdg_edge_gout_wc, E, _p(gC), _p(d["e"]), _p(ge_next), _p(T["WcT"]),
+                            _p(ge_out), _p(slabs_wc), nse, _p(a2ln), st_ln, _p(accb), _p(gl), _p(pp), 1, s)
+                    n_edge = nse
+                else:
+                    self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr),
+                            _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
+                            st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(T["WcT"]),
+                            _p(gz2m), _p(gz1m), _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), pm, nm, pe, ne, s)
+                self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
+                        _p(plan.perm_src), _p(gz1m), _p(gz1e if eu else None), _p(gP), _p(gQ), s)
             # gx_t, with the column sums / pairs of the LayerNorm whose output it is the gradient of:
             # the node LayerNorm of step t-1, or the node encoder's
             if t > 0:
@@ -403,7 +416,7 @@ class EPDEngine:
             self._t("gemm_sum2", lib.pdg_gemm_sum2_rw, N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part),
                     _p(gx_t), _p(a2n_prev), st_prev, _p(accb), np_, _p(gl), _p(pp), 1, s)
             n_node = self._nparts.value
-            if not fused:
+            if not fused and E:
                 segs["W2"].append((gz2m, d["a1m"], E))
                 if eu:
                     segs["W2"].append((gz2e, d["a1e"], E))
@@ -423,14 +436,15 @@ class EPDEngine:
         segs["ne2"].append((gz2, ctx.a1_ne, N))
         lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
                              _p(G["node_encoder.0.bias"]), None, s)
-        gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
-        pp, n_e = edge_ln_pairs(P_EENC, ge_next, ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"])
-        pe, ne = src(pp, n_e if not fused else n_edge)
-        lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], None,
-                         _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), pe, ne, s)
-        segs["ee2"].append((gz2e_, ctx.a1_ee, E))
-        lib.pdg_wgrad_narrow(E, _p(gz1e_), _p(ctx.e_in), 1, 0, _p(self._part_narrow), _p(G["edge_encoder.0.weight"]),
-                             _p(G["edge_encoder.0.bias"]), None, s)
+        if E:
+            gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
+            pp, n_e = edge_ln_pairs(P_EENC, ge_next, ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"])
+            pe, ne = src(pp, n_e if not fused else n_edge)
+            lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], None,
+                             _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), pe, ne, s)
+            segs["ee2"].append((gz2e_, ctx.a1_ee, E))
+            lib.pdg_wgrad_narrow(E, _p(gz1e_), _p(ctx.e_in), 1, 0, _p(self._part_narrow),
+                                 _p(G["edge_encoder.0.weight"]), _p(G["edge_encoder.0.bias"]), None, s)
         # LayerNorm weight / bias gradients: one launch over the four accumulators
         names = ("processor.node_net.4", "processor.edge_net.4", "node_encoder.4", "edge_encoder.4")
         lib.pdg_ln_param_grads(4, (ctypes.c_void_p * 4)(*[_p(acc[i]) for i in range(4)]),

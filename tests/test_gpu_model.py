@@ -216,3 +216,40 @@ def test_fused_edge_weight_gradients_match_separate_passes(nmesh, ngraph, steps)
         grads[fused] = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
     for name, g in grads[True].items():
         assert rel(g, grads[False][name]) < 1e-5, (name, rel(g, grads[False][name]))
+
+
+def test_edgeless_batch_matches_oracle():
+    """A batch whose graphs have no edge at all (SURVEY §4 T1 'E=0 graphs'): as in the reference,
+    every message aggregate is zero and the edge parameters get zero gradients; output and every
+    parameter gradient match the fp64 oracle (the oracle runs the reference's ops on empty
+    tensors), with the divergence loss on."""
+    from gnn_local_stress import losses
+    from pdg import graph, meshgen
+    datas = []
+    for s in meshgen.make_dataset(2, n=9, hole_radius=(0.15, 0.25), seed=8):
+        d = graph.sample_to_data(s)
+        d.edge_index = d.edge_index[:, :0]
+        d.edge_attr = d.edge_attr[:0]
+        datas.append(d)
+    batch = graph.Batch.from_data_list(datas).to("cuda")
+    assert batch.num_edges == 0
+    stats = {k: float(v) for k, v in dataset_stats(batch).items() if k not in ("mean_edge_weight",
+                                                                                "std_edge_weight")}
+    stats.update(mean_edge_weight=0.0, std_edge_weight=1.0)
+    steps = 3
+    model = _model(steps, stats)
+    params = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    pred = model(batch, scale_output=False).local_stress
+    gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
+    total, _, _ = losses.batch_loss(pred, batch, gt, divergence=True, divergence_penalty=10.0)
+    model.zero_grad()
+    total.backward()
+    p64, t64, g64 = _oracle_grads(params, stats, batch, steps, torch.float64, True, 10.0, False)
+    assert rel(pred.detach(), p64) < OUT_TOL
+    assert abs(float(total) - t64) <= OUT_TOL * abs(t64)
+    for name, p in model.named_parameters():
+        ref = g64[name]
+        if float(ref.abs().max()) == 0.0:
+            assert float(p.grad.abs().max()) == 0.0, name        # the edge branch: exactly zero
+        else:
+            assert rel(p.grad, ref) <= GRAD_TOL, (name, rel(p.grad, ref))
