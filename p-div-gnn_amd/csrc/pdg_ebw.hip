@@ -35,7 +35,15 @@ namespace {
 constexpr int EBW_WAVES = 8;
 constexpr int EBW_THREADS = 64 * EBW_WAVES;
 constexpr int EBW_IMG = 3 * X6_TERM;        // one bf16x6 image of 32 rows (24 KB)
-constexpr int EBW_MASK = X6_ROWS * L;       // relu mask bytes of 32 rows
+// relu mask bytes of 32 rows, row stride MSK_STRIDE: the epilogue reads one 4-byte word per lane
+// from 16 rows at a time, which a 128-B stride put on 2 of the 32 banks of a ds_read_b32 lane
+// group (16-way conflicts); 136 B (34 words) spreads them over all 32.  The staging writes (32
+// consecutive words of a row per lane group) stay conflict free.
+#ifndef PDG_MSK_STRIDE
+#define PDG_MSK_STRIDE 136
+#endif
+constexpr int MSK_STRIDE = PDG_MSK_STRIDE;
+constexpr int EBW_MASK = X6_ROWS * MSK_STRIDE;
 constexpr int WSLAB = L * L + L;            // floats per slab (weight + bias sums)
 // fp32 row tile in LDS that turns the product's output layout (16 rows x 64 B per wave
 // instruction: 25 % below whole-row access in an isolated stream, tools/membench.hip) into
@@ -272,14 +280,14 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
       bsum += zm;
       img_store4(img_gm, r, cg, zm);
       img_store4(img_am, r, cg, am);
-      *reinterpret_cast<unsigned*>(msk_m + r * L + 4 * cg) = relu_mask4(am);
+      *reinterpret_cast<unsigned*>(msk_m + r * MSK_STRIDE + 4 * cg) = relu_mask4(am);
       if (EU) {
         const f32x4 ze = ok ? ln_relu_bwd4(pge[u], pa2e[u], ste, lbe, g4) : zero;
         const f32x4 ae = ok ? pa1e[u] : zero;
         bsum += ze;
         img_store4(img_ge, r, cg, ze);
         img_store4(img_ae, r, cg, ae);
-        *reinterpret_cast<unsigned*>(msk_e + r * L + 4 * cg) = relu_mask4(ae);
+        *reinterpret_cast<unsigned*>(msk_e + r * MSK_STRIDE + 4 * cg) = relu_mask4(ae);
       }
     }
     __syncthreads();
@@ -305,13 +313,13 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     for (int nb = 0; nb < 2; ++nb) {
       const int r = 16 * nb + (l & 15);
       const int row = base + r;
-      const unsigned mm = *reinterpret_cast<const unsigned*>(msk_m + r * L + oc);
+      const unsigned mm = *reinterpret_cast<const unsigned*>(msk_m + r * MSK_STRIDE + oc);
       f32x4 zm;
 #pragma unroll
       for (int j = 0; j < 4; ++j) zm[j] = (mm >> (8 * j)) & 1u ? d[0][nb][j] : 0.f;
       f32x4 c = zm;
       if (EU) {
-        const unsigned me = *reinterpret_cast<const unsigned*>(msk_e + r * L + oc);
+        const unsigned me = *reinterpret_cast<const unsigned*>(msk_e + r * MSK_STRIDE + oc);
         f32x4 ze;
 #pragma unroll
         for (int j = 0; j < 4; ++j) ze[j] = (me >> (8 * j)) & 1u ? d[NI - 1][nb][j] : 0.f;

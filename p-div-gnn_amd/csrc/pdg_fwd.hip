@@ -504,9 +504,6 @@ __global__ __launch_bounds__(64 * EF_WAVES, EF_WAVES / 4) void edge_fwd_kernel(
     zero_acc(Z);
     if (valid && a1m) store_frag(a1m + (size_t)row * L, v);   // a1m / a1e: kept for the backward only
     if (EU && valid && a1e) store_frag(a1e + (size_t)row * L, ve);
-#if PDG_EF_NEXT == 2
-    issue(tile + stride);   // the next tile's rows fly during both W2 products
-#endif
     PDG_GEMM_2(Z, v);
     bias_relu_fv(v, Z, fb2);
     accum_stats(v, valid, sm1, sm2);
@@ -518,10 +515,7 @@ __global__ __launch_bounds__(64 * EF_WAVES, EF_WAVES / 4) void edge_fwd_kernel(
       bias_relu_fv(v, Z, fb2);
       accum_stats(v, valid, se1, se2);
     }
-#if PDG_EF_NEXT == 2
-    PDG_FENCE();
-    if (valid) store_frag((EU ? a2e : a2m) + (size_t)row * L, v);
-#elif PDG_EF_NEXT
+#if PDG_EF_NEXT
     issue(tile + stride);   // before this tile's last store
     PDG_FENCE();
     if (valid) store_frag((EU ? a2e : a2m) + (size_t)row * L, v);
