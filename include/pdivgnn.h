@@ -71,6 +71,7 @@ int pdg_format_inputs(int n_nodes, int n_edges, const float* pos, const float* m
 int pdg_encoder_fwd(int rows, int in_features, const float* x_in, const float* W0, const float* b0,
                     const float* W2, const float* b2, float* a1, float* a2,
                     double* partials, int* nparts, void* stream);
+/* (a1 == NULL: the layer-1 output is not stored; pdg_edge_enc_bwd recomputes it.) */
 
 /* Reduce LayerNorm partials -> statistics (mean, std_pop + eps). */
 int pdg_ln_finalize(const double* partials, int nparts, double count, pdg_ln_stat* out, void* stream);
@@ -259,6 +260,17 @@ int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float
                     const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
                     float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
                     const double* pairs_e, int npairs_e, void* stream);
+/* Edge encoder backward (models.py:268-274), fused: gz2 = LN_bwd(gy) [a2 > 0], slabs (zeroed
+ * before, pdg_wgrad_reduce layout) += gz2^T a1 and the b2 sums, gz1 = (W2T gz2) [a1 > 0], and per
+ * block narrow_sums[b] = (sum gz1 e_in, sum gz1) as 2 x 128 doubles; a1 = relu(w0 e_in + b0) is
+ * recomputed (pdg_encoder_fwd may skip storing it).  Replaces pdg_mlp2_bwd + the edge encoder's
+ * pdg_wgrad_segments and pdg_wgrad_narrow passes.  lb / lb_pairs as pdg_mlp2_bwd. */
+int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, const float* e_in, const float* w0,
+                     const float* b0, const pdg_ln_stat* st, const pdg_ln_bwd* lb, const double* lb_pairs,
+                     int lb_npairs, const float* ln_g, const float* W2T, float* slabs, double* narrow_sums,
+                     int nslabs, void* stream);
+/* grad_w0 += sum_b narrow_sums[b][0:128], grad_b0 += sum_b narrow_sums[b][128:256] (block order). */
+int pdg_enc_narrow_reduce(const double* narrow_sums, int nslabs, float* grad_w0, float* grad_b0, void* stream);
 int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next,
                      const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
                      const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,

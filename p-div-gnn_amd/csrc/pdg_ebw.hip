@@ -454,6 +454,121 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
   }
 }
 
+// ============================================================================ edge encoder backward
+// Backward of edge_encoder = Lin(1 -> 128) ReLU Lin(128 -> 128) ReLU LN (models.py:268-274) over the
+// E scalar inputs e_in, upstream gradient gy = d loss / d e_0 (ge_out of the first step):
+//   gz2 = LN_bwd(gy) [a2 > 0];   dW2 += gz2^T a1,  db2 += sum gz2   (slab, as edge_bwd_w2)
+//   gz1 = (W2^T gz2) [a1 > 0];   dw0 += sum gz1 e, db0 += sum gz1   (fp64 per block)
+// a1 = relu(w0 e + b0) is recomputed from the scalar input exactly as encoder_kernel forms it (so
+// the forward keeps no a1), and neither gz2 nor gz1 is written: this reads two E-row arrays where
+// pdg_mlp2_bwd + the ee2 weight-gradient pass + pdg_wgrad_narrow moved eight.
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd_kernel(
+    const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ e_in,
+    const float* __restrict__ w0, const float* __restrict__ b0, const pdg_ln_stat* __restrict__ st_p,
+    const pdg_ln_bwd* __restrict__ lb_p, const double* __restrict__ pairs, int npairs,
+    const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ slabs,
+    double* __restrict__ nsums, int E) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img_g = sm;                                   // gz2
+  unsigned char* img_a = sm + EBW_IMG;                         // a1
+  unsigned char* msk = sm + 2 * EBW_IMG;                       // [a1 > 0]
+  float* ev = reinterpret_cast<float*>(msk + EBW_MASK);        // the round's 32 inputs
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(E, r0, r1);
+  WSlice ws;
+  load_wslice(ws, W2T, w);
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+  const f32x4 w04 = *reinterpret_cast<const f32x4*>(w0 + 4 * cg);
+  const f32x4 b04 = *reinterpret_cast<const f32x4*>(b0 + 4 * cg);
+  const LNStat st = *reinterpret_cast<const LNStat*>(st_p);
+  const pdg_ln_bwd lb = lnb_resolve(lb_p, pairs, npairs, st_p);
+  f32x16 acc[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
+  double sw[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};   // narrow sums of features oc .. oc+3
+  f32x4 pg[2], pa2[2];
+  float pe[2];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int rc = clamp_row(base + rg + 16 * u, r1);
+      pg[u] = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + 4 * cg);
+      pa2[u] = *reinterpret_cast<const f32x4*>(a2 + (size_t)rc * L + 4 * cg);
+      pe[u] = e_in[rc];
+    }
+  };
+  if (r0 < r1) issue(r0);
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const bool ok = base + r < r1;
+      const f32x4 zg = ok ? ln_relu_bwd4(pg[u], pa2[u], st, lb, g4) : zero;
+      bsum += zg;
+      img_store4(img_g, r, cg, zg);
+      f32x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = fmaxf(fmaf(w04[j], pe[u], 0.f) + b04[j], 0.f);   // encoder_kernel's a1
+      a = ok ? a : zero;
+      img_store4(img_a, r, cg, a);
+      *reinterpret_cast<unsigned*>(msk + r * MSK_STRIDE + 4 * cg) = relu_mask4(a);
+      if (cg == 0) ev[r] = ok ? pe[u] : 0.f;
+    }
+    __syncthreads();
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    wgrad_round(acc, img_g, img_a);                        // dW2 += gz2^T a1
+    f32x4 d[1][2];
+    const unsigned char* imgs[1] = {img_g};
+    gemm_round<1>(d, ws, imgs);                            // W2^T gz2, features oc .. oc+3
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = 16 * nb + (l & 15);
+      const unsigned mm = *reinterpret_cast<const unsigned*>(msk + r * MSK_STRIDE + oc);
+      const double e = (double)ev[r];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float z = (mm >> (8 * j)) & 1u ? d[0][nb][j] : 0.f;
+        sw[j] += (double)z * e;
+        sb[j] += (double)z;
+      }
+    }
+    __syncthreads();   // the images are rewritten by the next round
+  }
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+  // the 16 lanes holding the same features (different rows): fixed xor butterfly
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sw[j] += __shfl_xor(sw[j], off);
+      sb[j] += __shfl_xor(sb[j], off);
+    }
+  if ((l & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      nsums[(size_t)blockIdx.x * 2 * L + oc + j] = sw[j];
+      nsums[(size_t)blockIdx.x * 2 * L + L + oc + j] = sb[j];
+    }
+  }
+}
+
+// grad_w0 += sum over blocks of the dw0 sums, grad_b0 += the db0 sums (block order: deterministic).
+__global__ void enc_narrow_reduce_kernel(const double* __restrict__ nsums, int nb, float* __restrict__ gw0,
+                                         float* __restrict__ gb0) {
+  const int t = threadIdx.x;
+  double s = 0;
+  for (int b = 0; b < nb; ++b) s += nsums[(size_t)b * 2 * L + t];
+  if (t < L) gw0[t] += (float)s;
+  else gb0[t - L] += (float)s;
+}
+
 // ============================================================================ C ABI
 extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
@@ -506,5 +621,32 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
     hipLaunchKernelGGL(edge_gout_wc_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
                        ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
   PDG_CHECK_LAUNCH("pdg_edge_gout_wc");
+  return PDG_OK;
+}
+
+extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, const float* e_in, const float* w0,
+                                const float* b0, const pdg_ln_stat* st, const pdg_ln_bwd* lb, const double* lb_pairs,
+                                int lb_npairs, const float* ln_g, const float* W2T, float* slabs, double* narrow_sums,
+                                int nslabs, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_enc_bwd: n_edges must be > 0");
+  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs && narrow_sums, "pdg_edge_enc_bwd: bad slabs");
+  PDG_CHECK_ARG(gy && a2 && e_in && w0 && b0 && st && (lb || lb_pairs) && ln_g && W2T,
+                "pdg_edge_enc_bwd: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2) && PDG_ALIGNED(w0) && PDG_ALIGNED(b0) && PDG_ALIGNED(ln_g) &&
+                    PDG_ALIGNED(W2T) && PDG_ALIGNED(slabs),
+                "pdg_edge_enc_bwd: misaligned pointer");
+  const size_t shm = 2 * EBW_IMG + EBW_MASK + X6_ROWS * sizeof(float);
+  hipLaunchKernelGGL(edge_enc_bwd_kernel, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gy, a2, e_in, w0,
+                     b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs, narrow_sums, n_edges);
+  PDG_CHECK_LAUNCH("pdg_edge_enc_bwd");
+  return PDG_OK;
+}
+
+extern "C" int pdg_enc_narrow_reduce(const double* narrow_sums, int nslabs, float* grad_w0, float* grad_b0,
+                                     void* stream) {
+  PDG_CHECK_ARG(nslabs > 0 && narrow_sums && grad_w0 && grad_b0, "pdg_enc_narrow_reduce: bad arguments");
+  hipLaunchKernelGGL(enc_narrow_reduce_kernel, dim3(1), dim3(2 * L), 0, (hipStream_t)stream, narrow_sums, nslabs,
+                     grad_w0, grad_b0);
+  PDG_CHECK_LAUNCH("pdg_enc_narrow_reduce");
   return PDG_OK;
 }

@@ -183,7 +183,7 @@ __global__ __launch_bounds__(384, 3) void encoder_kernel(int M, const float* __r
       }
       PDG_FENCE();
     }
-    if (valid) store_frag(a1 + (size_t)row * L, v);
+    if (valid && a1) store_frag(a1 + (size_t)row * L, v);   // a1 == NULL: recomputed by the backward
     Acc acc;
     zero_acc(acc);
     gemm128(acc, lds, v);

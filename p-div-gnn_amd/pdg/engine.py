@@ -174,7 +174,10 @@ class EPDEngine:
                             _p(P["node_encoder.2.weight"]), _p(P["node_encoder.2.bias"]), _p(a1_ne), _p(a2_ne),
                             _p(self._part_a), np_, s)
         self._finalize(self._part_a, N * L, st[0], s)
-        a1_ee, a2_ee = self._empty(E, L), self._empty(E, L)
+        # the edge encoder's layer-1 output is stored only for the unfused backward (pdg_mlp2_bwd);
+        # pdg_edge_enc_bwd recomputes it from the scalar input
+        a1_ee = self._empty(E, L) if (need_grad and not self.fused_edge_wgrad) else None
+        a2_ee = self._empty(E, L)
         if E:
             lib.pdg_encoder_fwd(E, 1, _p(e_in), _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]),
                                 _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]), _p(a1_ee), _p(a2_ee),
@@ -437,14 +440,25 @@ class EPDEngine:
         lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
                              _p(G["node_encoder.0.bias"]), None, s)
         if E:
-            gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
             pp, n_e = edge_ln_pairs(P_EENC, ge_next, ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"])
             pe, ne = src(pp, n_e if not fused else n_edge)
-            lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], None,
-                             _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), pe, ne, s)
-            segs["ee2"].append((gz2e_, ctx.a1_ee, E))
-            lib.pdg_wgrad_narrow(E, _p(gz1e_), _p(ctx.e_in), 1, 0, _p(self._part_narrow),
-                                 _p(G["edge_encoder.0.weight"]), _p(G["edge_encoder.0.bias"]), None, s)
+            if fused:   # one pass: weight gradients in slabs, the 1 -> 128 layer's as per-block sums
+                slabs_ee = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
+                nsum = torch.empty(nse, 2 * L, dtype=torch.float64, device=self.device)
+                self._t("edge_enc_bwd", lib.pdg_edge_enc_bwd, E, _p(ge_next), _p(ctx.a2_ee), _p(ctx.e_in),
+                        _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]), st[1], None, pe, ne,
+                        _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(slabs_ee), _p(nsum), nse, s)
+                lib.pdg_wgrad_reduce(_p(slabs_ee), nse, _p(G["edge_encoder.2.weight"]), L, 0,
+                                     _p(G["edge_encoder.2.bias"]), s)
+                lib.pdg_enc_narrow_reduce(_p(nsum), nse, _p(G["edge_encoder.0.weight"]),
+                                          _p(G["edge_encoder.0.bias"]), s)
+            else:
+                gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
+                lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], None,
+                                 _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(gz2e_), _p(gz1e_), pe, ne, s)
+                segs["ee2"].append((gz2e_, ctx.a1_ee, E))
+                lib.pdg_wgrad_narrow(E, _p(gz1e_), _p(ctx.e_in), 1, 0, _p(self._part_narrow),
+                                     _p(G["edge_encoder.0.weight"]), _p(G["edge_encoder.0.bias"]), None, s)
         # LayerNorm weight / bias gradients: one launch over the four accumulators
         names = ("processor.node_net.4", "processor.edge_net.4", "node_encoder.4", "edge_encoder.4")
         lib.pdg_ln_param_grads(4, (ctypes.c_void_p * 4)(*[_p(acc[i]) for i in range(4)]),

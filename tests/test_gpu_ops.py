@@ -492,3 +492,47 @@ def test_node_pq_rw_fin_equals_finalize_then_pq_rw(env, N, nparts, res):
     assert torch.equal(st_ref, st_fin)
     for u, v in zip(*outs):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("E", [77, 5000])
+def test_edge_enc_bwd_vs_autograd(env, E):
+    """pdg_edge_enc_bwd (edge encoder backward in one pass, layer-1 output recomputed from the scalar
+    input) against torch autograd of Lin(1->128) ReLU Lin(128->128) ReLU LN in fp64: all four
+    weight / bias gradients; the encoder forward is run with a1 == NULL (not stored)."""
+    lib, sh, _ = env
+    s = sh()
+    e_in = rnd(E)
+    W0, b0 = lin(L, 1)
+    W2, b2 = lin(L, L)
+    g = rnd(L) * 0.3 + 1.0
+    beta = rnd(L) * 0.1
+    a2 = torch.empty(E, L, device="cuda")
+    part = torch.empty(4096 * 256, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    lib.pdg_encoder_fwd(E, 1, e_in.data_ptr(), W0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(), None,
+                        a2.data_ptr(), part.data_ptr(), ctypes.byref(n), s)
+    st = finalize(lib, s, part, n.value, E * L)
+    gy = rnd(E, L)
+    acc = torch.zeros(4096 * 256, dtype=torch.float64, device="cuda")
+    pairs = torch.zeros(4096 * 2, dtype=torch.float64, device="cuda")
+    lib.pdg_ln_colsum(E, gy.data_ptr(), None, a2.data_ptr(), st.data_ptr(), acc.data_ptr(), ctypes.byref(n),
+                      g.data_ptr(), pairs.data_ptr(), 1, s)
+    ns = 37
+    slabs = torch.zeros(ns, L * L + L, device="cuda")
+    nsum = torch.empty(ns, 2 * L, dtype=torch.float64, device="cuda")
+    WT = W2.T.contiguous()
+    lib.pdg_edge_enc_bwd(E, gy.data_ptr(), a2.data_ptr(), e_in.data_ptr(), W0.data_ptr(), b0.data_ptr(),
+                         st.data_ptr(), None, pairs.data_ptr(), n.value, g.data_ptr(), WT.data_ptr(),
+                         slabs.data_ptr(), nsum.data_ptr(), ns, s)
+    gW2, gb2 = torch.zeros(L, L, device="cuda"), torch.zeros(L, device="cuda")
+    gW0, gb0 = torch.zeros(L, 1, device="cuda"), torch.zeros(L, device="cuda")
+    lib.pdg_wgrad_reduce(slabs.data_ptr(), ns, gW2.data_ptr(), L, 0, gb2.data_ptr(), s)
+    lib.pdg_enc_narrow_reduce(nsum.data_ptr(), ns, gW0.data_ptr(), gb0.data_ptr(), s)
+    # reference (fp64 autograd)
+    W0d, b0d = W0.double().cpu().requires_grad_(True), b0.double().cpu().requires_grad_(True)
+    W2d, b2d = W2.double().cpu().requires_grad_(True), b2.double().cpu().requires_grad_(True)
+    a1 = torch.relu(e_in.double().cpu()[:, None] @ W0d.T + b0d)
+    out = ln_ref(torch.relu(a1 @ W2d.T + b2d), g.double().cpu(), beta.double().cpu())
+    out.backward(gy.double().cpu())
+    assert rel(gW2, W2d.grad) < 1e-5 and rel(gb2, b2d.grad) < 1e-5
+    assert rel(gW0, W0d.grad) < 1e-5 and rel(gb0, b0d.grad) < 1e-5
