@@ -315,6 +315,13 @@ int pdg_wgrad_reduce(float* slabs, int nslabs, float* grad_W, int ld, int col0,
 #define PDG_MAX_SEGS 32
 int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
                        float* slabs, int nslabs, void* stream);
+/* Two weight gradients sharing an operand in one pass over nseg row segments (the shared array is
+ * read once): shared_x != 0: slabs0 += A0^T A2, slabs1 += A1^T A2 (bias rows: column sums of A0 /
+ * A1); shared_x == 0: slabs0 += A0^T A1, slabs1 += A0^T A2 (bias rows: column sums of A0).  The
+ * slabs are written (not accumulated), nslabs each, reduced with pdg_wgrad_reduce.  Pointer and
+ * row arrays are HOST arrays of nseg <= PDG_MAX_SEGS entries. */
+int pdg_wgrad_pairs(int nseg, const float* const* a0_ptrs, const float* const* a1_ptrs, const float* const* a2_ptrs,
+                    const int* rows, int shared_x, float* slabs0, float* slabs1, int nslabs, void* stream);
 /* Narrow weight gradient: T[c][i] = sum_k Wide[k][c] Narrow[k][i] (c < 128, i < k_narrow <= 8),
  * sums sum_k Wide[k][c] and sum_k Narrow[k][i]; added into grad arrays:
  * transpose == 0: grad_W[c*k_narrow + i] (shape 128 x k), else grad_W[i*128 + c] (k x 128);

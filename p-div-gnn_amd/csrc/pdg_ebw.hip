@@ -52,32 +52,6 @@ constexpr int WSLAB = L * L + L;            // floats per slab (weight + bias su
 // pdg_edge_bwd_w2 the three extra tiles measured +2 % and are not used.
 constexpr int OT_STRIDE = L + 4;
 
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-// A operand of rows 16w .. 16w+15 of a 128x128 matrix WT (o' x k, row-major), K chunk ks
-// (k = 32 ks + 8 (l >> 4) + 0..7), three bf16 terms.
-struct WSlice {
-  bf16x8 a[4][3];
-};
-
-__device__ __forceinline__ void load_wslice(WSlice& ws, const float* __restrict__ WT, int w) {
-  const int l = lane_id();
-  const float* row = WT + (size_t)(16 * w + (l & 15)) * L + 8 * (l >> 4);
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const f32x4 x0 = *reinterpret_cast<const f32x4*>(row + 32 * ks);
-    const f32x4 x1 = *reinterpret_cast<const f32x4*>(row + 32 * ks + 4);
-    unsigned h[4], m[4], lo[4];
-    split3_pair(x0[0], x0[1], h[0], m[0], lo[0]);
-    split3_pair(x0[2], x0[3], h[1], m[1], lo[1]);
-    split3_pair(x1[0], x1[1], h[2], m[2], lo[2]);
-    split3_pair(x1[2], x1[3], h[3], m[3], lo[3]);
-    ws.a[ks][0] = __builtin_bit_cast(bf16x8, (u32x4){h[0], h[1], h[2], h[3]});
-    ws.a[ks][1] = __builtin_bit_cast(bf16x8, (u32x4){m[0], m[1], m[2], m[3]});
-    ws.a[ks][2] = __builtin_bit_cast(bf16x8, (u32x4){lo[0], lo[1], lo[2], lo[3]});
-  }
-}
-
 // Columns 4cg .. 4cg+3 of image row r, split into the three terms.
 __device__ __forceinline__ void img_store4(unsigned char* img, int r, int cg, const f32x4& v) {
   unsigned h0, m0, l0, h1, m1, l1;
@@ -559,14 +533,29 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd_kernel(
   }
 }
 
-// grad_w0 += sum over blocks of the dw0 sums, grad_b0 += the db0 sums (block order: deterministic).
-__global__ void enc_narrow_reduce_kernel(const double* __restrict__ nsums, int nb, float* __restrict__ gw0,
-                                         float* __restrict__ gb0) {
-  const int t = threadIdx.x;
-  double s = 0;
-  for (int b = 0; b < nb; ++b) s += nsums[(size_t)b * 2 * L + t];
-  if (t < L) gw0[t] += (float)s;
-  else gb0[t - L] += (float)s;
+// grad_w0 += sum over blocks of the dw0 sums, grad_b0 += the db0 sums.  Block c (of 2) owns columns
+// 128 c .. 128 c + 127; its 4 thread groups sum every 4th slab row with 4 loads in flight each, then
+// the 4 partial sums are added in group order (deterministic).
+__global__ __launch_bounds__(512) void enc_narrow_reduce_kernel(const double* __restrict__ nsums, int nb,
+                                                                float* __restrict__ gw0, float* __restrict__ gb0) {
+  __shared__ double part[4][L];
+  const int col = threadIdx.x & (L - 1), grp = threadIdx.x >> 7, e = L * blockIdx.x + col;
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  int b = grp;
+  for (; b + 12 < nb; b += 16) {
+    s0 += nsums[(size_t)b * 2 * L + e];
+    s1 += nsums[(size_t)(b + 4) * 2 * L + e];
+    s2 += nsums[(size_t)(b + 8) * 2 * L + e];
+    s3 += nsums[(size_t)(b + 12) * 2 * L + e];
+  }
+  for (; b < nb; b += 4) s0 += nsums[(size_t)b * 2 * L + e];
+  part[grp][col] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (grp == 0) {
+    const double t = ((part[0][col] + part[1][col]) + part[2][col]) + part[3][col];
+    if (blockIdx.x == 0) gw0[col] += (float)t;
+    else gb0[col] += (float)t;
+  }
 }
 
 // ============================================================================ C ABI
@@ -645,7 +634,7 @@ extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, c
 extern "C" int pdg_enc_narrow_reduce(const double* narrow_sums, int nslabs, float* grad_w0, float* grad_b0,
                                      void* stream) {
   PDG_CHECK_ARG(nslabs > 0 && narrow_sums && grad_w0 && grad_b0, "pdg_enc_narrow_reduce: bad arguments");
-  hipLaunchKernelGGL(enc_narrow_reduce_kernel, dim3(1), dim3(2 * L), 0, (hipStream_t)stream, narrow_sums, nslabs,
+  hipLaunchKernelGGL(enc_narrow_reduce_kernel, dim3(2), dim3(4 * L), 0, (hipStream_t)stream, narrow_sums, nslabs,
                      grad_w0, grad_b0);
   PDG_CHECK_LAUNCH("pdg_enc_narrow_reduce");
   return PDG_OK;

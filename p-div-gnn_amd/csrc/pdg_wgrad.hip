@@ -585,3 +585,202 @@ extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const fl
   PDG_CHECK_LAUNCH("pdg_wgrad_segments");
   return PDG_OK;
 }
+
+// ---------------------------------------------------------------------------- pairs
+// Two weight gradients that share an operand in one pass (the shared array is read once):
+//   SHX (shared X):  dW0 = A0^T A2, dW1 = A1^T A2   (edge_net.0's Wa / Wb: gP, gQ against x)
+//   !SHX (shared G): dW0 = A0^T A1, dW1 = A0^T A2   (node_net.0's two halves: gz1n against aggr, x)
+// 8 waves: waves 0-3 the 64x64 quadrants of product 0, waves 4-7 those of product 1, each with the
+// bf16x6 operand reads of wgrad_x6_kernel; 3 x 24 KB of images, two blocks per CU.  Block b writes
+// slab b of slabs0 and of slabs1 (weight + the column sums of that product's G), reduced by
+// pdg_wgrad_reduce like pdg_wgrad_segments' slabs.
+struct WgradSegs3 {
+  const float* A[3][PDG_MAX_SEGS];
+  long start[PDG_MAX_SEGS + 1];
+  int nseg;
+};
+struct WgTable3 {
+  long start[PDG_MAX_SEGS + 1];
+  const float* A[3][PDG_MAX_SEGS];
+};
+constexpr int WG3_TABLE_BYTES = (sizeof(WgTable3) + 15) / 16 * 16;
+
+// Split 2 rows x 4 columns and write them: row i of this thread goes to image row 2 rg + i.
+__device__ __forceinline__ void x6_store2(unsigned char* img, int cg, int rg, const f32x4 (&v)[2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split3_pair(v[i][0], v[i][1], h0, m0, l0);
+    split3_pair(v[i][2], v[i][3], h1, m1, l1);
+    const int off = x6_addr(2 * rg + i, 8 * cg);
+    *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
+    *reinterpret_cast<u32x2*>(img + X6_TERM + off) = u32x2{m0, m1};
+    *reinterpret_cast<u32x2*>(img + 2 * X6_TERM + off) = u32x2{l0, l1};
+  }
+}
+
+__device__ __forceinline__ void x6_load3(const WgTable3* tb, int nseg, long base, long r1, int& seg, int cg,
+                                         f32x4 (&v)[3][2]) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const long vr = base + i;
+    if (vr < r1) {
+      while (seg + 1 < nseg && vr >= tb->start[seg + 1]) ++seg;
+      const long r = vr - tb->start[seg];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) v[a][i] = reinterpret_cast<const f32x4*>(tb->A[a][seg] + r * L)[cg];
+    } else {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) v[a][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+template <bool SHX>
+__global__ __launch_bounds__(512, 1) void wgrad_x6_pair_kernel(WgradSegs3 sg, long total, float* __restrict__ slabs0,
+                                                              float* __restrict__ slabs1) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem3[];   // [table | A0 | A1 | A2 terms]
+  WgTable3* tb = reinterpret_cast<WgTable3*>(smem3);
+  unsigned char* img = smem3 + WG3_TABLE_BYTES;
+  const int nseg = sg.nseg;
+  for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
+  for (int i = threadIdx.x; i < 3 * PDG_MAX_SEGS; i += blockDim.x) tb->A[i / PDG_MAX_SEGS][i % PDG_MAX_SEGS] =
+      sg.A[i / PDG_MAX_SEGS][i % PDG_MAX_SEGS];
+  __syncthreads();
+  const int nb = gridDim.x;
+  long per = (total + nb - 1) / nb;
+  per = (per + X6_ROWS - 1) / X6_ROWS * X6_ROWS;
+  const long r0 = min(total, per * blockIdx.x), r1 = min(total, per * (blockIdx.x + 1));
+  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
+  const int pw = w >> 2, w4 = w & 3;                      // product, quadrant
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;  // loader: rows 2 rg, 2 rg + 1, columns 4 cg ..
+  const int ob = 64 * (w4 >> 1), ib = 64 * (w4 & 1);
+  const unsigned char* gimg = img + (SHX ? pw : 0) * 3 * X6_TERM;
+  const unsigned char* ximg = img + (SHX ? 2 : 1 + pw) * 3 * X6_TERM;
+  const int lrow = 8 * h + ((l & 15) >> 2);
+  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  f32x4 bs0 = f32x4{0.f, 0.f, 0.f, 0.f}, bs1 = f32x4{0.f, 0.f, 0.f, 0.f};   // column sums of A0 (and A1)
+  int seg;
+  {
+    int lo = 0, hi = nseg;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (tb->start[mid] <= r0) lo = mid; else hi = mid;
+    }
+    seg = lo;
+  }
+  f32x4 v[3][2];
+  auto stage = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      bs0 += v[0][i];
+      if (SHX) bs1 += v[1][i];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) x6_store2(img + a * 3 * X6_TERM, cg, rg, v[a]);
+  };
+  if (r0 < r1) {
+    x6_load3(tb, nseg, r0 + 2 * rg, r1, seg, cg, v);
+    stage();
+  }
+  __syncthreads();
+  for (long base = r0; base < r1; base += X6_ROWS) {
+    const bool more = base + X6_ROWS < r1;
+    if (more) x6_load3(tb, nseg, base + X6_ROWS + 2 * rg, r1, seg, cg, v);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 A[2][3], B[2][3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int row = 16 * ks + lrow;
+        const int g0 = x6_addr(row, lcolb + 2 * (ob + 32 * a)), g1 = x6_addr(row + 4, lcolb + 2 * (ob + 32 * a));
+        const int x0 = x6_addr(row, lcolb + 2 * (ib + 32 * a)), x1 = x6_addr(row + 4, lcolb + 2 * (ib + 32 * a));
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          A[a][p] = x6_operand(gimg + p * X6_TERM, g0, g1);
+          B[a][p] = x6_operand(ximg + p * X6_TERM, x0, x1);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          f32x16 t = acc[a][b];
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2], B[b][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][2], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][1], t, 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][0], t, 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (more) stage();
+    __syncthreads();
+  }
+  float* slab = (pw ? slabs1 : slabs0) + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int i = ib + 32 * b + c;
+        slab[o * L + i] = acc[a][b][r];
+      }
+  // bias sums: the 16 row groups of each column group, in row-group order (the images are dead)
+  float* red = reinterpret_cast<float*>(img);
+  *reinterpret_cast<f32x4*>(red + 4 * threadIdx.x) = bs0;
+  *reinterpret_cast<f32x4*>(red + 2048 + 4 * threadIdx.x) = SHX ? bs1 : bs0;
+  __syncthreads();
+  if (threadIdx.x < 2 * L) {
+    const int p = threadIdx.x >> 7, col = threadIdx.x & 127, g = col >> 2, j = col & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += red[2048 * p + 4 * (32 * q + g) + j];
+    (p ? slabs1 : slabs0)[(size_t)blockIdx.x * SLAB + L * L + col] = s;
+  }
+}
+
+extern "C" int pdg_wgrad_pairs(int nseg, const float* const* a0_ptrs, const float* const* a1_ptrs,
+                               const float* const* a2_ptrs, const int* rows, int shared_x, float* slabs0,
+                               float* slabs1, int nslabs, void* stream) {
+  PDG_CHECK_ARG(nseg > 0 && nseg <= PDG_MAX_SEGS, "pdg_wgrad_pairs: 1..%d segments", PDG_MAX_SEGS);
+  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs0 && slabs1 && slabs0 != slabs1,
+                "pdg_wgrad_pairs: bad slabs");
+  WgradSegs3 sg;
+  long tot = 0;
+  for (int i = 0; i < nseg; ++i) {
+    PDG_CHECK_ARG(rows[i] >= 0, "pdg_wgrad_pairs: negative rows");
+    PDG_CHECK_ARG(rows[i] == 0 || (a0_ptrs[i] && a1_ptrs[i] && a2_ptrs[i] && PDG_ALIGNED(a0_ptrs[i]) &&
+                                   PDG_ALIGNED(a1_ptrs[i]) && PDG_ALIGNED(a2_ptrs[i])),
+                  "pdg_wgrad_pairs: null or misaligned pointer");
+    sg.A[0][i] = a0_ptrs[i];
+    sg.A[1][i] = a1_ptrs[i];
+    sg.A[2][i] = a2_ptrs[i];
+    sg.start[i] = tot;
+    tot += rows[i];
+  }
+  for (int i = nseg; i < PDG_MAX_SEGS; ++i) sg.A[0][i] = sg.A[1][i] = sg.A[2][i] = nullptr;
+  sg.start[nseg] = tot;
+  for (int i = nseg + 1; i <= PDG_MAX_SEGS; ++i) sg.start[i] = tot;
+  sg.nseg = nseg;
+  PDG_CHECK_ARG(tot > 0, "pdg_wgrad_pairs: no rows");
+  const size_t shm = WG3_TABLE_BYTES + 9 * X6_TERM;
+  if (shared_x)
+    hipLaunchKernelGGL(wgrad_x6_pair_kernel<true>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot, slabs0,
+                       slabs1);
+  else
+    hipLaunchKernelGGL(wgrad_x6_pair_kernel<false>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
+                       slabs0, slabs1);
+  PDG_CHECK_LAUNCH("pdg_wgrad_pairs");
+  return PDG_OK;
+}

@@ -60,5 +60,30 @@ __device__ __forceinline__ bf16x8 x6_operand(const unsigned char* img, int ofs0,
   return __builtin_bit_cast(bf16x8, r);
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// A operand of rows 16w .. 16w+15 of a 128x128 matrix WT (o' x k, row-major), K chunk ks
+// (k = 32 ks + 8 (l >> 4) + 0..7), three bf16 terms.
+struct WSlice {
+  bf16x8 a[4][3];
+};
+
+__device__ __forceinline__ void load_wslice(WSlice& ws, const float* __restrict__ WT, int w) {
+  const int l = lane_id();
+  const float* row = WT + (size_t)(16 * w + (l & 15)) * L + 8 * (l >> 4);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const f32x4 x0 = *reinterpret_cast<const f32x4*>(row + 32 * ks);
+    const f32x4 x1 = *reinterpret_cast<const f32x4*>(row + 32 * ks + 4);
+    unsigned h[4], m[4], lo[4];
+    split3_pair(x0[0], x0[1], h[0], m[0], lo[0]);
+    split3_pair(x0[2], x0[3], h[1], m[1], lo[1]);
+    split3_pair(x1[0], x1[1], h[2], m[2], lo[2]);
+    split3_pair(x1[2], x1[3], h[3], m[3], lo[3]);
+    ws.a[ks][0] = __builtin_bit_cast(bf16x8, (u32x4){h[0], h[1], h[2], h[3]});
+    ws.a[ks][1] = __builtin_bit_cast(bf16x8, (u32x4){m[0], m[1], m[2], m[3]});
+    ws.a[ks][2] = __builtin_bit_cast(bf16x8, (u32x4){lo[0], lo[1], lo[2], lo[3]});
+  }
+}
 
 }  // namespace pdg

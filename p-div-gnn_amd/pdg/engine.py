@@ -105,6 +105,9 @@ class EPDEngine:
         self._nparts = ctypes.c_int(0)
         # one weight-gradient slab per block of pdg_wgrad_segments: three blocks per CU
         self._nslabs = 3 * torch.cuda.get_device_properties(self.device).multi_processor_count
+        # pdg_wgrad_pairs: two blocks per CU
+        self._nslabs_p = min(2 * torch.cuda.get_device_properties(self.device).multi_processor_count,
+                             lib.pdg_max_blocks())
         self._pair = torch.zeros(2, **f64)
         self.sync = None
         # edge backward with the W2 / Wc weight gradients fused (pdg_edge_bwd_w2 / pdg_edge_gout_wc);
@@ -481,6 +484,29 @@ class EPDEngine:
         ns = self._nslabs
         if getattr(self, "_slabs", None) is None or self._slabs.device != self.device:
             self._slabs = torch.empty(ns, L * L + L, dtype=torch.float32, device=self.device)
+        # the weight pairs that share an operand, one pass each (pdg_wgrad_pairs): Wa / Wb against x
+        # (gP, gQ), node_net.0's halves from gz1n (against aggr, x)
+        nsp = self._nslabs_p
+        if getattr(self, "_slabs_p", None) is None or self._slabs_p.device != self.device:
+            self._slabs_p = torch.empty(2, nsp, L * L + L, dtype=torch.float32, device=self.device)
+        pairs_w = [
+            (1, [(g, q, x, n) for (g, x, n), (q, _, _) in zip(segs.pop("Wa"), segs.pop("Wb"))],
+             ("processor.edge_net.0.weight", 3 * L, 0, None), ("processor.edge_net.0.weight", 3 * L, L, None)),
+            (0, [(g, a, x, n) for (g, a, n), (_, x, _) in zip(segs.pop("Wn1a"), segs.pop("Wn1b"))],
+             ("processor.node_net.0.weight", 2 * L, 0, "processor.node_net.0.bias"),
+             ("processor.node_net.0.weight", 2 * L, L, None)),
+        ]
+        for shx, sl, (w0n, ld0, c00, b0n), (w1n, ld1, c01, b1n) in pairs_w:
+            for c0 in range(0, len(sl), 32):
+                chunk = sl[c0:c0 + 32]
+                n = len(chunk)
+                arr = [(ctypes.c_void_p * n)(*[t[k].data_ptr() for t in chunk]) for k in range(3)]
+                rw = (ctypes.c_int * n)(*[t[3] for t in chunk])
+                self._t("wgrad_pair", lib.pdg_wgrad_pairs, n, arr[0], arr[1], arr[2], rw, shx,
+                        _p(self._slabs_p[0]), _p(self._slabs_p[1]), nsp, s)
+                lib.pdg_wgrad_reduce(_p(self._slabs_p[0]), nsp, _p(G[w0n]), ld0, c00, _p(G[b0n]) if b0n else None, s)
+                lib.pdg_wgrad_reduce(_p(self._slabs_p[1]), nsp, _p(G[w1n]), ld1, c01, _p(G[b1n]) if b1n else None, s)
+        red = [r for r in red if r[0] in segs]
         for key, wname, ld, col0, bname in red:
             sl = segs[key]
             for c0 in range(0, len(sl), 32):

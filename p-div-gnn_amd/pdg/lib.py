@@ -54,6 +54,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_pq_scatter_bwd": [I, P, P, P, P, P, P, P, P],
     "pdg_wgrad_accum": [I, P, P, P, P, P, I, P],
     "pdg_wgrad_reduce": [P, I, P, I, I, P, P],
+    "pdg_wgrad_pairs": [I, P, P, P, P, I, P, P, I, P],
     "pdg_edge_enc_bwd": [I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P],
     "pdg_enc_narrow_reduce": [P, I, P, P, P],
     "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P, I, P],

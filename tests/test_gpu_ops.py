@@ -536,3 +536,32 @@ def test_edge_enc_bwd_vs_autograd(env, E):
     out.backward(gy.double().cpu())
     assert rel(gW2, W2d.grad) < 1e-5 and rel(gb2, b2d.grad) < 1e-5
     assert rel(gW0, W0d.grad) < 1e-5 and rel(gb0, b0d.grad) < 1e-5
+
+
+@pytest.mark.parametrize("shared_x", [1, 0])
+def test_wgrad_pairs_vs_fp64(env, shared_x):
+    """pdg_wgrad_pairs: two weight gradients sharing an operand over ragged segments (rows not
+    multiples of the 32-row rounds, an empty segment), bias rows = column sums of the G operand(s)."""
+    lib, sh, _ = env
+    s = sh()
+    rows = [1000, 0, 77, 4099]
+    A = [[rnd(r, L) for r in rows] for _ in range(3)]
+    ns = 41
+    slabs = torch.empty(2, ns, L * L + L, device="cuda")
+    n = len(rows)
+    P = ctypes.c_void_p
+    arr = [(P * n)(*[t.data_ptr() for t in A[k]]) for k in range(3)]
+    lib.pdg_wgrad_pairs(n, arr[0], arr[1], arr[2], (ctypes.c_int * n)(*rows), shared_x, slabs[0].data_ptr(),
+                        slabs[1].data_ptr(), ns, s)
+    cat = [torch.cat([t.double().cpu() for t in A[k]]) for k in range(3)]
+    if shared_x:
+        refs = [(cat[0].T @ cat[2], cat[0].sum(0)), (cat[1].T @ cat[2], cat[1].sum(0))]
+    else:
+        refs = [(cat[0].T @ cat[1], cat[0].sum(0)), (cat[0].T @ cat[2], cat[0].sum(0))]
+    for k in range(2):
+        gW = torch.zeros(L, 2 * L, device="cuda")
+        gb = torch.zeros(L, device="cuda")
+        lib.pdg_wgrad_reduce(slabs[k].data_ptr(), ns, gW.data_ptr(), 2 * L, L * k, gb.data_ptr(), s)
+        assert rel(gW[:, L * k:L * (k + 1)], refs[k][0]) < 1e-6, k
+        assert float(gW[:, L * (1 - k):L * (2 - k)].abs().max()) == 0.0
+        assert rel(gb, refs[k][1]) < 1e-6
