@@ -313,6 +313,8 @@ int pdg_wgrad_reduce(float* slabs, int nslabs, float* grad_W, int ld, int col0,
  * sum_seg sum_k G_seg[k]^T X_seg[k] and of sum G_seg[k] (written, not accumulated);
  * reduce with pdg_wgrad_reduce.  g_ptrs/x_ptrs/rows are HOST arrays of nseg <= PDG_MAX_SEGS entries. */
 #define PDG_MAX_SEGS 32
+/* Blocks per CU that pdg_wgrad_segments is built for (its nslabs should be this x the CU count). */
+int pdg_wgrad_slabs_per_cu(void);
 int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
                        float* slabs, int nslabs, void* stream);
 /* Two weight gradients sharing an operand in one pass over nseg row segments (the shared array is
@@ -356,6 +358,9 @@ int pdg_div_bwd(int n_graphs, const int* ptr, int n_nodes, const int* at_rowptr,
 /* ---------------------------------------------------------------- utilities */
 /* out (cols x rows, contiguous) = in^T for a (rows x cols) row-major matrix with row stride ld. */
 int pdg_transpose(int rows, int cols, int ld, const float* in, float* out, void* stream);
+/* n <= 16 transposes of 128 x 128 blocks in one launch: out_ptrs[i] (128 x 128, row-major) =
+ * in_ptrs[i]^T, in_ptrs[i] with row stride lds[i]; host arrays. */
+int pdg_transpose128_batch(int n, const float* const* in_ptrs, const int* lds, float* const* out_ptrs, void* stream);
 /* *flag = 1 if any grad element is inf/NaN (GradScaler's skip test, gnn_train.py:205-207). */
 int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream);
 /* Adam as torch.optim.Adam (amsgrad=False, weight_decay=0) stepped by GradScaler.step

@@ -210,6 +210,42 @@ extern "C" int pdg_transpose(int rows, int cols, int ld, const float* in, float*
   return PDG_OK;
 }
 
+// Up to 16 transposes of 128 x 128 blocks in one launch (the backward's W^T copies).
+struct TransposeJobs {
+  const float* in[16];
+  float* out[16];
+  int ld[16];
+};
+
+__global__ void transpose128_batch_kernel(TransposeJobs jobs) {
+  __shared__ float tile[32][33];
+  const int j = blockIdx.z;
+  const float* __restrict__ in = jobs.in[j];
+  float* __restrict__ out = jobs.out[j];
+  const int ld = jobs.ld[j];
+  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  for (int y = ty; y < 32; y += 8) tile[y][tx] = in[(size_t)(by + y) * ld + bx + tx];
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) out[(size_t)(bx + y) * 128 + by + tx] = tile[tx][y];
+}
+
+extern "C" int pdg_transpose128_batch(int n, const float* const* in_ptrs, const int* lds, float* const* out_ptrs,
+                                      void* stream) {
+  PDG_CHECK_ARG(n > 0 && n <= 16 && in_ptrs && lds && out_ptrs, "pdg_transpose128_batch: 1..16 jobs");
+  TransposeJobs jobs;
+  for (int i = 0; i < n; ++i) {
+    PDG_CHECK_ARG(in_ptrs[i] && out_ptrs[i] && lds[i] >= 128 && in_ptrs[i] != out_ptrs[i],
+                  "pdg_transpose128_batch: bad job");
+    jobs.in[i] = in_ptrs[i];
+    jobs.out[i] = out_ptrs[i];
+    jobs.ld[i] = lds[i];
+  }
+  hipLaunchKernelGGL(transpose128_batch_kernel, dim3(4, 4, n), dim3(256), 0, (hipStream_t)stream, jobs);
+  PDG_CHECK_LAUNCH("pdg_transpose128_batch");
+  return PDG_OK;
+}
+
 // GradScaler's skip test (gnn_train.py:205-207).
 __global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* __restrict__ flag) {
   int bad = 0;

@@ -18,6 +18,9 @@
 using namespace pdg;
 
 constexpr int SLAB = L * L + L;   // floats per slab
+#ifndef PDG_WGRAD_GROUPS
+#define PDG_WGRAD_GROUPS 3
+#endif
 
 __device__ __forceinline__ void zero_acc16(f32x16 (&acc)[4]) {
 #pragma unroll
@@ -446,10 +449,16 @@ __device__ __forceinline__ void x6_load(const WgTable* tb, int nseg, long base, 
   }
 }
 
-__global__ __launch_bounds__(256, 3) void wgrad_x6_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem6[];   // [table | G terms | X terms]
+// NG wave groups of 4 per block (NG = 3: one 768-thread block per CU): group g stages and multiplies
+// its own third of the block's rows in its own images, and the groups' accumulators are added in a
+// fixed order at the end, so each CU writes ONE slab (the slab traffic and the reduction that reads
+// it shrink NG-fold).  All groups run the same number of rounds (rows past a group's end are zero).
+template <int NG>
+__global__ __launch_bounds__(256 * NG, 3 / NG) void wgrad_x6_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem6[];   // [table | NG x (G terms | X terms)]
   WgTable* tb = reinterpret_cast<WgTable*>(smem6);
-  unsigned char* gimg = smem6 + WG_TABLE_FLOATS * 4;
+  const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255;
+  unsigned char* gimg = smem6 + WG_TABLE_FLOATS * 4 + grp * 6 * X6_TERM;
   unsigned char* ximg = gimg + 3 * X6_TERM;
   const int nseg = sg.nseg;
   for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
@@ -460,10 +469,12 @@ __global__ __launch_bounds__(256, 3) void wgrad_x6_kernel(WgradSegs sg, long tot
   __syncthreads();
   const int nb = gridDim.x;
   long per = (total + nb - 1) / nb;
-  per = (per + X6_ROWS - 1) / X6_ROWS * X6_ROWS;
-  const long r0 = min(total, per * blockIdx.x), r1 = min(total, per * (blockIdx.x + 1));
-  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
-  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  per = (per + NG * X6_ROWS - 1) / (NG * X6_ROWS) * (NG * X6_ROWS);
+  const long bper = per / NG;                                           // rows per group (whole rounds)
+  const long b0 = min(total, per * blockIdx.x), b1 = min(total, per * (blockIdx.x + 1));
+  const long r0 = min(b1, b0 + bper * grp), r1 = min(b1, r0 + bper);
+  const int l = lane_id(), h = l >> 5, c = l & 31, w = (tid >> 6);
+  const int cg = tid & 31, rg = tid >> 5;
   const int ob = 64 * (w >> 1), ib = 64 * (w & 1);
   // transposed-read row and column byte of this lane inside its 16-lane group (see x6_operand)
   const int lrow = 8 * h + ((l & 15) >> 2);
@@ -485,17 +496,17 @@ __global__ __launch_bounds__(256, 3) void wgrad_x6_kernel(WgradSegs sg, long tot
     }
     seg = lo;
   }
+  const long nrounds = (min(b1, b0 + bper) - b0 + X6_ROWS - 1) / X6_ROWS;   // group 0's count: the most
   f32x4 gr[4], xr[4];
-  if (r0 < r1) {
-    x6_load(tb, nseg, r0 + 4 * rg, r1, seg, cg, gr, xr);
+  x6_load(tb, nseg, r0 + 4 * rg, r1, seg, cg, gr, xr);    // rows past r1 load as zeros
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bsum += gr[i];
-    x6_store(gimg, cg, rg, gr);
-    x6_store(ximg, cg, rg, xr);
-  }
+  for (int i = 0; i < 4; ++i) bsum += gr[i];
+  x6_store(gimg, cg, rg, gr);
+  x6_store(ximg, cg, rg, xr);
   __syncthreads();
-  for (long base = r0; base < r1; base += X6_ROWS) {
-    const bool more = base + X6_ROWS < r1;
+  for (long k = 0; k < nrounds; ++k) {
+    const long base = r0 + k * X6_ROWS;
+    const bool more = k + 1 < nrounds;
     if (more) x6_load(tb, nseg, base + X6_ROWS + 4 * rg, r1, seg, cg, gr, xr);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -533,29 +544,41 @@ __global__ __launch_bounds__(256, 3) void wgrad_x6_kernel(WgradSegs sg, long tot
     }
     __syncthreads();
   }
-  float* slab = slabs + (size_t)blockIdx.x * SLAB;
+  // combine the groups in a fixed order ((g_{NG-1} + ... ) + g_0) through LDS (the images are dead):
+  // element (o, i) at float o * 128 + i, bias sums after the 128 x 128 block
+  float* cmb = reinterpret_cast<float*>(smem6 + WG_TABLE_FLOATS * 4);
+  float* red = NG > 1 ? cmb + L * L : cmb;   // 8 row groups x 128 bias partials (NG = 1: cmb is unused)
+  for (int g = NG - 1; g >= 0; --g) {
+    if (grp == g) {
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int i = ib + 32 * b + c;
-        slab[o * L + i] = acc[a][b][r];
-      }
+          for (int r = 0; r < 16; ++r) {
+            const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int i = ib + 32 * b + c;
+            float v = acc[a][b][r];
+            if (g < NG - 1) v = cmb[o * L + i] + v;
+            if (g == 0) slabs[(size_t)blockIdx.x * SLAB + o * L + i] = v;
+            else cmb[o * L + i] = v;
+          }
+      f32x4* rb = reinterpret_cast<f32x4*>(red + 4 * tid);
+      *rb = (g < NG - 1) ? *rb + bsum : bsum;
+    }
+    __syncthreads();
+  }
   // bias sums: the 8 row groups of each column group, in row-group order
-  float* red = reinterpret_cast<float*>(gimg);   // the images are dead now
-  *reinterpret_cast<f32x4*>(red + 4 * threadIdx.x) = bsum;
-  __syncthreads();
   if (threadIdx.x < 128) {
     const int col = threadIdx.x, g = col >> 2, j = col & 3;
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < 8; ++q) s += red[4 * (32 * q + g) + j];
-    slab[L * L + col] = s;
+    slabs[(size_t)blockIdx.x * SLAB + L * L + col] = s;
   }
 }
+
+extern "C" int pdg_wgrad_slabs_per_cu(void) { return 3 / PDG_WGRAD_GROUPS; }
 
 extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
                                   float* slabs, int nslabs, void* stream) {
@@ -579,8 +602,13 @@ extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const fl
   hipLaunchKernelGGL(wgrad_segments_kernel, dim3(nslabs), dim3(256), (WG_TABLE_FLOATS + 4 * WG_TILE) * sizeof(float),
                      (hipStream_t)stream, sg, tot, slabs);
 #else
-  hipLaunchKernelGGL(wgrad_x6_kernel, dim3(nslabs), dim3(256), WG_TABLE_FLOATS * 4 + 6 * X6_TERM, (hipStream_t)stream,
+#if PDG_WGRAD_GROUPS == 3
+  hipLaunchKernelGGL(wgrad_x6_kernel<3>, dim3(nslabs), dim3(768), WG_TABLE_FLOATS * 4 + 18 * X6_TERM,
+                     (hipStream_t)stream, sg, tot, slabs);
+#else
+  hipLaunchKernelGGL(wgrad_x6_kernel<1>, dim3(nslabs), dim3(256), WG_TABLE_FLOATS * 4 + 6 * X6_TERM, (hipStream_t)stream,
                      sg, tot, slabs);
+#endif
 #endif
   PDG_CHECK_LAUNCH("pdg_wgrad_segments");
   return PDG_OK;

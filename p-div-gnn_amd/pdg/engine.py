@@ -104,7 +104,7 @@ class EPDEngine:
         self._part_narrow = torch.empty(self.max_blocks * (L * 6 + L + 6), **f64)
         self._nparts = ctypes.c_int(0)
         # one weight-gradient slab per block of pdg_wgrad_segments: three blocks per CU
-        self._nslabs = 3 * torch.cuda.get_device_properties(self.device).multi_processor_count
+        self._nslabs = lib.pdg_wgrad_slabs_per_cu() * torch.cuda.get_device_properties(self.device).multi_processor_count
         # pdg_wgrad_pairs: two blocks per CU
         self._nslabs_p = min(2 * torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
@@ -270,12 +270,11 @@ class EPDEngine:
         """W^T copies of every weight block the backward GEMMs read."""
         s = stream_handle(self.device)
         out = {}
+        jobs = []
 
         def tr(name, key, col0, ld):
-            W = P[name]
-            T = self._empty(L, L)
-            lib.pdg_transpose(L, L, ld, W.data_ptr() + 4 * col0, T.data_ptr(), s)
-            out[key] = T
+            out[key] = T = self._empty(L, L)
+            jobs.append((P[name].data_ptr() + 4 * col0, ld, T.data_ptr()))
 
         tr("node_decoder.0.weight", "Wd1T", 0, L)
         tr("processor.edge_net.2.weight", "W2T", 0, L)
@@ -287,6 +286,9 @@ class EPDEngine:
         tr("processor.node_net.0.weight", "Wn1bT", L, 2 * L)
         tr("node_encoder.2.weight", "Wne2T", 0, L)
         tr("edge_encoder.2.weight", "Wee2T", 0, L)
+        n = len(jobs)
+        lib.pdg_transpose128_batch(n, (ctypes.c_void_p * n)(*[j[0] for j in jobs]), (ctypes.c_int * n)(*[j[1] for j in jobs]),
+                                   (ctypes.c_void_p * n)(*[j[2] for j in jobs]), s)
         return out
 
     def backward(self, P: dict, ctx: FwdCtx, gy: torch.Tensor, G: dict) -> None:

@@ -54,6 +54,8 @@ SIGNATURES: dict[str, list] = {
     "pdg_pq_scatter_bwd": [I, P, P, P, P, P, P, P, P],
     "pdg_wgrad_accum": [I, P, P, P, P, P, I, P],
     "pdg_wgrad_reduce": [P, I, P, I, I, P, P],
+    "pdg_transpose128_batch": [I, P, P, P, P],
+    "pdg_wgrad_slabs_per_cu": [],
     "pdg_wgrad_pairs": [I, P, P, P, P, I, P, P, I, P],
     "pdg_edge_enc_bwd": [I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P],
     "pdg_enc_narrow_reduce": [P, I, P, P, P],
@@ -103,7 +105,7 @@ class _Lib:
         if not name.startswith("pdg_"):
             raise AttributeError(name)
         fn = getattr(self.load(), name)
-        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks"):
+        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks", "pdg_wgrad_slabs_per_cu"):
             return fn
 
         def call(*args):

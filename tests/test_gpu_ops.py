@@ -565,3 +565,19 @@ def test_wgrad_pairs_vs_fp64(env, shared_x):
         assert rel(gW[:, L * k:L * (k + 1)], refs[k][0]) < 1e-6, k
         assert float(gW[:, L * (1 - k):L * (2 - k)].abs().max()) == 0.0
         assert rel(gb, refs[k][1]) < 1e-6
+
+
+def test_transpose128_batch(env):
+    """The backward's W^T copies in one launch (strided sources: blocks of edge_net.0's 128 x 384)."""
+    lib, sh, _ = env
+    W = rnd(L, 3 * L)
+    V = rnd(L, L)
+    outs = [torch.empty(L, L, device="cuda") for _ in range(4)]
+    srcs = [W.data_ptr(), W.data_ptr() + 4 * L, W.data_ptr() + 4 * 2 * L, V.data_ptr()]
+    lds = [3 * L, 3 * L, 3 * L, L]
+    P = ctypes.c_void_p
+    lib.pdg_transpose128_batch(4, (P * 4)(*srcs), (ctypes.c_int * 4)(*lds), (P * 4)(*[o.data_ptr() for o in outs]),
+                               sh())
+    refs = [W[:, :L], W[:, L:2 * L], W[:, 2 * L:], V]
+    for o, r in zip(outs, refs):
+        assert torch.equal(o.cpu(), r.T.contiguous().cpu())
