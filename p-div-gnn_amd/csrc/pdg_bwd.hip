@@ -701,8 +701,8 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, int chunk, c
       q += reinterpret_cast<const f32x4*>(gz1m + kk)[j];
       if (gz1e) p += reinterpret_cast<const f32x4*>(gz1e + kk)[j];
     }
-    reinterpret_cast<f32x4*>(gP + (size_t)v * L)[j] = p;
-    reinterpret_cast<f32x4*>(gQ + (size_t)v * L)[j] = q;
+    stg4(gP + (size_t)v * L + 4 * j, p);
+    stg4(gQ + (size_t)v * L + 4 * j, q);
     if (!more) break;
     i += step;
     v = vn;

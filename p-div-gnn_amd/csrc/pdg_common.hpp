@@ -101,6 +101,19 @@ __device__ __forceinline__ void st4(float* __restrict__ p, int T, const f32x4& x
   *reinterpret_cast<f32x4*>(p + 16 * T) = x;
 #endif
 }
+// A 16-byte row store outside the fragment helpers (nontemporal with PDG_NT_ROWS: measured +0.2 ms
+// per config-2 step, the P / Q rows the edge forward gathers and the gaggr rows the edge backward
+// gathers then miss the caches; off).
+#ifndef PDG_NT_ROWS
+#define PDG_NT_ROWS 0
+#endif
+__device__ __forceinline__ void stg4(float* __restrict__ p, const f32x4& x) {
+#if PDG_NT_ROWS
+  __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
+#else
+  *reinterpret_cast<f32x4*>(p) = x;
+#endif
+}
 // Feature index of fragment element s in lane quarter q.
 __device__ __forceinline__ int frag_feature(int s, int q) { return 16 * (s >> 2) + 4 * q + (s & 3); }
 

@@ -298,11 +298,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
 #pragma unroll
         for (int j = 0; j < 4; ++j) ze[j] = (me >> (8 * j)) & 1u ? d[NI - 1][nb][j] : 0.f;
         c = zm + ze;
-        if (row < r1) *reinterpret_cast<f32x4*>(gz1e + (size_t)row * L + oc) = ze;
+        if (row < r1) stg4(gz1e + (size_t)row * L + oc, ze);
       }
       if (row < r1) {
-        *reinterpret_cast<f32x4*>(gz1m + (size_t)row * L + oc) = zm;
-        *reinterpret_cast<f32x4*>(gC + (size_t)row * L + oc) = c;
+        stg4(gz1m + (size_t)row * L + oc, zm);
+        stg4(gC + (size_t)row * L + oc, c);
       }
     }
     __syncthreads();   // the images are rewritten by the next round
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
       if (row < r1) {
         const f32x4 dv = *reinterpret_cast<const f32x4*>(t_o + r * OT_STRIDE + 4 * cg);
         const f32x4 go = RES ? res[u] + dv : dv;
-        *reinterpret_cast<f32x4*>(ge_out + (size_t)row * L + 4 * cg) = go;
+        stg4(ge_out + (size_t)row * L + 4 * cg, go);
         if (ln) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {

@@ -621,8 +621,8 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __re
         acc += x[u];
       }
     }
-    reinterpret_cast<f32x4*>(out + (size_t)v * L)[j] = acc;
-    if (xsum) reinterpret_cast<f32x4*>(xsum + (size_t)v * L)[j] = xs;
+    stg4(out + (size_t)v * L + 4 * j, acc);
+    if (xsum) stg4(xsum + (size_t)v * L + 4 * j, xs);
   }
 }
 

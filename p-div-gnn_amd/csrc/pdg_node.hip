@@ -144,7 +144,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
       for (int c = 0; c < 4; ++c) a1[c] = fmaxf(acc[c] + bias1[c], 0.f);
       // D row 4q + c of this wave's block = feature 16w + 4q + c of node row r
       *reinterpret_cast<f32x4*>(a1t + (i & 1) * TILE * AS + r * AS + 16 * w + 4 * q) = a1;
-      if (valid && a1_out) *reinterpret_cast<f32x4*>(a1_out + (size_t)row * L + 16 * w + 4 * q) = a1;
+      if (valid && a1_out) stg4(a1_out + (size_t)row * L + 16 * w + 4 * q, a1);
     }
     __syncthreads();
     if (loader) {
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
 #pragma unroll
       for (int c = 0; c < 4; ++c) a2[c] = fmaxf(acc[c] + bias2[c], 0.f);
       if (valid) {
-        *reinterpret_cast<f32x4*>(a2_out + (size_t)row * L + 16 * w + 4 * q) = a2;
+        stg4(a2_out + (size_t)row * L + 16 * w + 4 * q, a2);
         const float p1 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
         const float p2 = (a2[0] * a2[0] + a2[1] * a2[1]) + (a2[2] * a2[2] + a2[3] * a2[3]);
         s1 += (double)p1;
@@ -243,7 +243,7 @@ __device__ __forceinline__ void store_gz2(float* __restrict__ buf, int t, int N,
       z[e] = rg.av[u][e] > 0.f ? ga : 0.f;
     }
     *reinterpret_cast<f32x4*>(buf + rr * GS + 4 * j) = z;
-    if (node < N) reinterpret_cast<f32x4*>(gz2_out + (size_t)node * L)[j] = z;
+    if (node < N) stg4(gz2_out + (size_t)node * L + 4 * j, z);
   }
 }
 
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
 #pragma unroll
       for (int c = 0; c < 4; ++c) z1[c] = a1v[c] > 0.f ? acc[c] : 0.f;   // relu_mask_acc
       *reinterpret_cast<f32x4*>(g1 + r * GS + oc) = z1;
-      if (valid) *reinterpret_cast<f32x4*>(gz1_out + (size_t)row * L + oc) = z1;
+      if (valid) stg4(gz1_out + (size_t)row * L + oc, z1);
     }
     __syncthreads();
     if (loader) {
@@ -331,8 +331,8 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
       }
       acc_b += res;
       if (valid) {
-        *reinterpret_cast<f32x4*>(gaggr + (size_t)row * L + oc) = acc_a;
-        *reinterpret_cast<f32x4*>(gx_part + (size_t)row * L + oc) = acc_b;
+        stg4(gaggr + (size_t)row * L + oc, acc_a);
+        stg4(gx_part + (size_t)row * L + oc, acc_b);
       }
     }
   }
@@ -396,7 +396,7 @@ __device__ __forceinline__ void store_xt(float* __restrict__ buf, int t, int N, 
       y[e] = v;
     }
     *reinterpret_cast<f32x4*>(buf + rr * GS + 4 * j) = y;
-    if (node < N) reinterpret_cast<f32x4*>(xout + (size_t)node * L)[j] = y;
+    if (node < N) stg4(xout + (size_t)node * L + 4 * j, y);
   }
 }
 
@@ -462,8 +462,8 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
         }
       }
       if (row < N) {
-        *reinterpret_cast<f32x4*>(P + (size_t)row * L + oc) = acc_p;
-        *reinterpret_cast<f32x4*>(Q + (size_t)row * L + oc) = acc_q;
+        stg4(P + (size_t)row * L + oc, acc_p);
+        stg4(Q + (size_t)row * L + oc, acc_q);
       }
     }
     __syncthreads();
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void gemm_sum2_rw_kernel(
       }
       if (res) acc += rv;
       if (row < N) {
-        *reinterpret_cast<f32x4*>(out + (size_t)row * L + oc) = acc;
+        stg4(out + (size_t)row * L + oc, acc);
         if (COLS) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {   // the pdg_ln_colsum formulas
