@@ -234,6 +234,15 @@ int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* 
  * ge_out = ge_next + WcT gC.  Writes gz2m, gz1m, gz2e, gz1e, gC, ge_out.
  * ge_next == NULL: the edge-update branch had no consumer (last step): gz2e/gz1e are not
  * written, gC = gz1m, ge_out = WcT gC. */
+/* pdg_edge_fwd in the block-cooperative layout (pdg_ebw.hip): nblocks blocks of 512 threads, one
+ * contiguous row range each, Wc (fp32) and W2 (bf16 terms) stationary in registers, whole-row HBM
+ * access.  Same outputs (C bitwise, the W2 products to fp32 rounding); part_m / part_e get nblocks
+ * partials. */
+int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                      const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
+                      const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
+                      const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
+                      double* part_e, int with_edge_update, int nblocks, void* stream);
 int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                  const float* a2m, const float* a1m, const float* a2e, const float* a1e,
                  const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,

@@ -114,6 +114,8 @@ __device__ __forceinline__ void stg4(float* __restrict__ p, const f32x4& x) {
   *reinterpret_cast<f32x4*>(p) = x;
 #endif
 }
+// A 16-byte row store with the fragment stores' policy (nontemporal with PDG_NT_ST).
+__device__ __forceinline__ void stnt4(float* __restrict__ p, const f32x4& x) { st4(p, 0, x); }
 // Feature index of fragment element s in lane quarter q.
 __device__ __forceinline__ int frag_feature(int s, int q) { return 16 * (s >> 2) + 4 * q + (s & 3); }
 

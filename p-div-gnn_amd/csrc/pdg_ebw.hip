@@ -558,6 +558,200 @@ __global__ __launch_bounds__(512) void enc_narrow_reduce_kernel(const double* __
   }
 }
 
+// ============================================================================ edge forward, cooperative
+// pdg_edge_fwd in the block-cooperative layout of the edge backward (one block of 8 waves per CU,
+// contiguous row ranges, 32-row rounds): wave w owns output features [16w, 16w + 16) of both
+// products with Wc and W2 stationary in registers as bf16 terms, the operands are 32-row bf16x6
+// images in LDS, and every HBM row access is whole-row (outputs through fp32 row tiles).  Per round:
+//   stage    e_t = LN(a2_prev) [+ e_res] (whole rows) -> HBM and the e image
+//   | barrier | next round's rows issued
+//   product  C = Wc e + b1; message a1m = relu(C + P[dst] + Q[src]), edge update
+//            a1e = relu(C + P[src] + Q[dst]) (P / Q rows gathered at the wave's 16 features)
+//            -> a1 images and row tiles
+//   | barrier | a1 rows stored (training)
+//   product  a2 = relu(W2 a1 + b2) -> LayerNorm partials, row tiles
+//   | barrier | a2 rows stored; the next round's stage
+// C = Wc e is an exact fp32 product (v_mfma_f32_16x16x4_f32, Wc rows as register A fragments, e
+// from an fp32 row tile): bitwise edge_fwd_kernel's C.  (C in bf16x6 biased the LayerNorm statistics
+// the way bf16x6 node_net did: parameter gradients 2e-4 from fp64 instead of 2.5e-6, measured.)
+constexpr int EFC_TILE = X6_ROWS * OT_STRIDE;   // floats per fp32 row tile
+constexpr int EFC_ES = L + 8;                    // e tile row stride: the C operand reads are conflict free
+
+template <bool RES, bool EU>
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
+    int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
+    const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
+    const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ P,
+    const float* __restrict__ Q, const float* __restrict__ W1, const float* __restrict__ b1,
+    const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ a1m, float* __restrict__ a2m,
+    float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m, double* __restrict__ part_e) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img_m = sm;                                   // a1m
+  unsigned char* img_x = sm + EBW_IMG;                         // a1e (EU)
+  float* t_m = reinterpret_cast<float*>(sm + 2 * EBW_IMG);     // fp32 row tiles: a1m / a2m
+  float* t_x = t_m + EFC_TILE;                                 //                 a1e / a2e
+  float* t_e = t_x + EFC_TILE;                                 //                 e_t
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(E, r0, r1);
+  // the weights as A operands, rows = output features 16w .. 16w + 15 (W is out x in, row-major):
+  // Wc = W1[:, 256:384] (row stride 384), W2
+  f32x4 wcf[8];   // Wc rows 16w + (l & 15), inputs 16T + 4(l >> 4) .. +3 (node_pq_rw's A fragments)
+  {
+    const float* pc = W1 + (size_t)(16 * w + (l & 15)) * (3 * L) + 2 * L + 4 * (l >> 4);
+#pragma unroll
+    for (int T = 0; T < 8; ++T) wcf[T] = *reinterpret_cast<const f32x4*>(pc + 16 * T);
+  }
+  WSlice ws2;
+  load_wslice(ws2, W2, w);
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg), bb4 = *reinterpret_cast<const f32x4*>(lb + 4 * cg);
+  const f32x4 b1o = *reinterpret_cast<const f32x4*>(b1 + oc), b2o = *reinterpret_cast<const f32x4*>(b2 + oc);
+  double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
+  f32x4 xa[2], xr[2];
+  int dq[2], sq[2];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
+      xa[u] = *reinterpret_cast<const f32x4*>(a2p + rc);
+      if (RES) xr[u] = *reinterpret_cast<const f32x4*>(eres + rc);
+      const int pr = clamp_row(base + 16 * u + (l & 15), r1);   // this lane's product rows
+      dq[u] = dst[pr];
+      sq[u] = src[pr];
+    }
+  };
+  auto stage = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const bool ok = base + r < r1;
+      f32x4 e;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {   // ln_apply (pdg_fwd.hip), element by element
+        float y = div_den(xa[u][j] - st.mean, st.den, st.rstd) * g4[j] + bb4[j];
+        if (RES) y += xr[u][j];
+        e[j] = y;
+      }
+      if (ok) stnt4(eout + (size_t)(base + r) * L + 4 * cg, e);
+      *reinterpret_cast<f32x4*>(t_e + r * EFC_ES + 4 * cg) = ok ? e : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  if (r0 < r1) {
+    issue(r0);
+    stage(r0);
+  }
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    __syncthreads();   // e tile complete
+    int dc[2] = {dq[0], dq[1]}, sc[2] = {sq[0], sq[1]};
+    const bool more = base + X6_ROWS < r1;
+    if (more) issue(base + X6_ROWS);
+    // ---- C = Wc e + b1 and the two first layers at this wave's 16 features
+    f32x4 gpd[2], gqs[2], gps[2], gqd[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      gpd[nb] = *reinterpret_cast<const f32x4*>(P + (size_t)dc[nb] * L + oc);
+      gqs[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)sc[nb] * L + oc);
+      if (EU) {
+        gps[nb] = *reinterpret_cast<const f32x4*>(P + (size_t)sc[nb] * L + oc);
+        gqd[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)dc[nb] * L + oc);
+      }
+    }
+    f32x4 d[2];
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {   // the MFMA order of gemm128: step (T, jj) sums inputs 16T + 4k + jj
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      const float* er = t_e + (16 * nb + (l & 15)) * EFC_ES + 4 * (l >> 4);
+#pragma unroll
+      for (int T = 0; T < 8; ++T) {
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(er + 16 * T);
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wcf[T][jj], bv[jj], acc, 0, 0, 0);
+      }
+      d[nb] = acc;
+    }
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = 16 * nb + (l & 15);
+      f32x4 am, ae;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float c = d[nb][j] + b1o[j];
+        am[j] = fmaxf((c + gpd[nb][j]) + gqs[nb][j], 0.f);
+        if (EU) ae[j] = fmaxf((c + gps[nb][j]) + gqd[nb][j], 0.f);
+      }
+      img_store4(img_m, r, 4 * w + (l >> 4), am);
+      if (a1m) *reinterpret_cast<f32x4*>(t_m + r * OT_STRIDE + oc) = am;
+      if (EU) {
+        img_store4(img_x, r, 4 * w + (l >> 4), ae);
+        if (a1e) *reinterpret_cast<f32x4*>(t_x + r * OT_STRIDE + oc) = ae;
+      }
+    }
+    __syncthreads();   // a1 images and tiles complete
+    if (a1m) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = rg + 16 * u;
+        if (base + r < r1) {
+          stnt4(a1m + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_m + r * OT_STRIDE + 4 * cg));
+          if (EU) stnt4(a1e + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
+        }
+      }
+    }
+    // ---- a2 = relu(W2 a1 + b2) for both evaluations
+    constexpr int NI = EU ? 2 : 1;
+    f32x4 d2[NI][2];
+    const unsigned char* ia[NI];
+    ia[0] = img_m;
+    if (EU) ia[NI - 1] = img_x;
+    gemm_round<NI>(d2, ws2, ia);
+    __syncthreads();   // the a1 tiles are read; reuse them for a2
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = 16 * nb + (l & 15);
+      const bool ok = base + r < r1;
+#pragma unroll
+      for (int u = 0; u < NI; ++u) {
+        f32x4 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = fmaxf(d2[u][nb][j] + b2o[j], 0.f);
+        *reinterpret_cast<f32x4*>((u ? t_x : t_m) + r * OT_STRIDE + oc) = a;
+        if (ok) {
+          const double p1 = (double)((a[0] + a[1]) + (a[2] + a[3]));
+          const double p2 = (double)((a[0] * a[0] + a[1] * a[1]) + (a[2] * a[2] + a[3] * a[3]));
+          if (u) { se1 += p1; se2 += p2; } else { sm1 += p1; sm2 += p2; }
+        }
+      }
+    }
+    __syncthreads();   // a2 tiles complete
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      if (base + r < r1) {
+        stnt4(a2m + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_m + r * OT_STRIDE + 4 * cg));
+        if (EU) stnt4(a2e + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
+      }
+    }
+    if (more) stage(base + X6_ROWS);   // the e tile was last read before the second barrier
+  }
+  double* red = reinterpret_cast<double*>(sm);
+  __syncthreads();
+  block_sum2(sm1, sm2, red);
+  if (threadIdx.x == 0) {
+    part_m[2 * blockIdx.x] = sm1;
+    part_m[2 * blockIdx.x + 1] = sm2;
+  }
+  if (EU) {
+    block_sum2(se1, se2, red + 32);
+    if (threadIdx.x == 0) {
+      part_e[2 * blockIdx.x] = se1;
+      part_e[2 * blockIdx.x + 1] = se2;
+    }
+  }
+}
+
 // ============================================================================ C ABI
 extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
@@ -637,5 +831,34 @@ extern "C" int pdg_enc_narrow_reduce(const double* narrow_sums, int nslabs, floa
   hipLaunchKernelGGL(enc_narrow_reduce_kernel, dim3(2), dim3(4 * L), 0, (hipStream_t)stream, narrow_sums, nslabs,
                      grad_w0, grad_b0);
   PDG_CHECK_LAUNCH("pdg_enc_narrow_reduce");
+  return PDG_OK;
+}
+
+extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                                 const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
+                                 const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
+                                 const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
+                                 double* part_e, int with_edge_update, int nblocks, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd_coop: n_edges must be > 0");
+  PDG_CHECK_ARG(nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_fwd_coop: bad nblocks");
+  PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
+                    PDG_ALIGNED(a1m) && PDG_ALIGNED(a2m) && PDG_ALIGNED(W1) && PDG_ALIGNED(W2) &&
+                    PDG_ALIGNED(b1) && PDG_ALIGNED(b2) && PDG_ALIGNED(ln_g) && PDG_ALIGNED(ln_b) &&
+                    (!e_res || PDG_ALIGNED(e_res)),
+                "pdg_edge_fwd_coop: misaligned pointer");
+  PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
+                "pdg_edge_fwd_coop: edge-update outputs missing or misaligned");
+  const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float);
+  hipStream_t s = (hipStream_t)stream;
+#define PDG_EFC(R, U)                                                                                              \
+  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U>), dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
+                     ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e)
+  if (e_res) {
+    if (with_edge_update) PDG_EFC(true, true); else PDG_EFC(true, false);
+  } else {
+    if (with_edge_update) PDG_EFC(false, true); else PDG_EFC(false, false);
+  }
+#undef PDG_EFC
+  PDG_CHECK_LAUNCH("pdg_edge_fwd_coop");
   return PDG_OK;
 }

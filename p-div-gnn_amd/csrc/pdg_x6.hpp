@@ -68,9 +68,9 @@ struct WSlice {
   bf16x8 a[4][3];
 };
 
-__device__ __forceinline__ void load_wslice(WSlice& ws, const float* __restrict__ WT, int w) {
+__device__ __forceinline__ void load_wslice(WSlice& ws, const float* __restrict__ WT, int w, int ld = L) {
   const int l = lane_id();
-  const float* row = WT + (size_t)(16 * w + (l & 15)) * L + 8 * (l >> 4);
+  const float* row = WT + (size_t)(16 * w + (l & 15)) * ld + 8 * (l >> 4);
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     const f32x4 x0 = *reinterpret_cast<const f32x4*>(row + 32 * ks);

@@ -581,3 +581,51 @@ def test_transpose128_batch(env):
     refs = [W[:, :L], W[:, L:2 * L], W[:, 2 * L:], V]
     for o, r in zip(outs, refs):
         assert torch.equal(o.cpu(), r.T.contiguous().cpu())
+
+
+@pytest.mark.parametrize("E,eu,res", [(1000, 1, 1), (4099, 0, 1), (77, 1, 0)])
+def test_edge_fwd_coop_matches_edge_fwd(env, E, eu, res):
+    """pdg_edge_fwd_coop (block-cooperative layout) against pdg_edge_fwd on the same inputs: e_t and
+    the layer-1 outputs bitwise (C = Wc e is the same fp32 MFMA sequence), the W2 outputs and the
+    LayerNorm partials to fp32 rounding (bf16x6 products over a different K order)."""
+    lib, sh, _ = env
+    s = sh()
+    N = 300
+    g = torch.Generator().manual_seed(E)
+    src = torch.randint(0, N, (E,), generator=g).int().cuda()
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values.int().cuda()
+    a2p, eres = torch.relu(rnd(E, L)), rnd(E, L)
+    Pn, Qn = rnd(N, L), rnd(N, L)
+    W1, b1 = lin(L, 3 * L)
+    W2, b2 = lin(L, L)
+    lg, lbv = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
+    part = torch.empty(4096, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    tmp = torch.empty(E, L, device="cuda")
+    lib.pdg_mlp2_fwd(E, a2p.data_ptr(), W2.data_ptr(), b2.data_ptr(), tmp.data_ptr(), part.data_ptr(),
+                     ctypes.byref(n), s)
+    st = finalize(lib, s, part, n.value, E * L)
+    outs = {}
+    for name in ("ref", "coop"):
+        o = {k: torch.full((E, L), float("nan"), device="cuda") for k in ("e", "a1m", "a2m", "a1e", "a2e")}
+        pm = torch.zeros(4096, dtype=torch.float64, device="cuda")
+        pe = torch.zeros(4096, dtype=torch.float64, device="cuda")
+        args = (E, a2p.data_ptr(), st.data_ptr(), lg.data_ptr(), lbv.data_ptr(), eres.data_ptr() if res else None,
+                o["e"].data_ptr(), src.data_ptr(), dst.data_ptr(), Pn.data_ptr(), Qn.data_ptr(), W1.data_ptr(),
+                b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), o["a1m"].data_ptr(), o["a2m"].data_ptr(),
+                o["a1e"].data_ptr() if eu else None, o["a2e"].data_ptr() if eu else None)
+        if name == "ref":
+            lib.pdg_edge_fwd(*args, pm.data_ptr(), pe.data_ptr() if eu else None, eu, ctypes.byref(n), s)
+            np_ = n.value
+        else:
+            np_ = 37
+            lib.pdg_edge_fwd_coop(*args, pm.data_ptr(), pe.data_ptr() if eu else None, eu, np_, s)
+        outs[name] = (o, pm[: 2 * np_].view(np_, 2).sum(0), pe[: 2 * np_].view(np_, 2).sum(0))
+    (o0, pm0, pe0), (o1, pm1, pe1) = outs["ref"], outs["coop"]
+    for k in ("e", "a1m") + (("a1e",) if eu else ()):
+        assert torch.equal(o0[k], o1[k]), k
+    for k in ("a2m",) + (("a2e",) if eu else ()):
+        assert rel(o1[k], o0[k]) < 1e-6, k
+    assert rel(pm1, pm0) < 1e-6
+    if eu:
+        assert rel(pe1, pe0) < 1e-6
