@@ -50,8 +50,10 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PMC_FILE = ROOT / "profiles" / "r02_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
-PMC_NAMES = {"edge_fwd": "void edge_fwd_kernel<true, true>", "edge_bwd": "void edge_bwd_kernel<true>",
-             "segment_sum": "segment_sum_kernel", "node_net": "node_net_kernel", "pq_scatter_bwd": "pq_scatter_bwd_kernel",
+PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
+             "edge_bwd": "void edge_bwd_kernel<true>",
+             "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": "node_net_kernel",
+             "pq_scatter_bwd": "pq_scatter_bwd_kernel",
              "wgrad_W2": "wgrad_x6_kernel", "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
              "edge_gout": "void edge_gout_wc_kernel<true>"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
@@ -181,7 +183,7 @@ def cpu_baseline(cfg, samples, reps: int = 3, one_thread_graphs: int = 1, one_th
 
 
 # ---------------------------------------------------------------------------------- roofline
-def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool) -> dict:
+def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, seg: bool = False) -> dict:
     """Algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops with the peak of their
     instruction type, and the bytes the kernel must read/write (inputs once, outputs once, int32
     indices).  An fp32-accurate 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA,
@@ -189,9 +191,11 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
     g = 2 * L * L
     return {
         # W_c product (fp32 MFMA) + 2 W2 products (bf16x6) per edge; reads a2e_prev, e_prev, 4 gathered
-        # P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e
+        # P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e; seg: also the N message
+        # sums rows, and a2m only when training
         "edge_fwd": ([(E * g, PEAK_FP32_MFMA), (E * 2 * g * X6, PEAK_BF16_MFMA)],
-                     E * ((9 if infer else 11) * 4 * L + 8)),
+                     E * ((9 if infer else 11) * 4 * L + 8) - (E * 4 * L if (seg and infer) else 0)
+                     + (8 * L * N if seg else 0)),
         # fused (pdg_edge_bwd_w2): 2 W2^T products + 2 weight-gradient products per edge (bf16x6);
         # reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gz1e, gC; one slab
         # read+write per block.  unfused (pdg_edge_bwd): W2^T x2 (bf16x6) + Wc^T (fp32); writes
@@ -203,8 +207,10 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
         "edge_gout": ([(E * 2 * g * X6, PEAK_BF16_MFMA)], E * 5 * 4 * L + 2 * nslab_bytes),
         # all steps' W2 segments: 2E rows per step of (G, X) 512-byte rows, one 64 KB slab per block
         "wgrad_W2": ([(S * 2 * E * g * X6, PEAK_BF16_MFMA)], S * 2 * E * 2 * 4 * L + 512 * (L * L + L) * 4),
-        # dst-segment sum of LN(a2m): reads a2m (E rows) and rowptr, writes aggr (+ x-hat sums)
-        "segment_sum": ([], 4 * L * E + 4 * (N + 1) + (1 if infer else 2) * 4 * L * N),
+        # dst-segment sum of LN(a2m): reads a2m (E rows) and rowptr, writes aggr (+ x-hat sums); seg
+        # (pdg_segsum_finish): reads the fp64 message sums and rowptr, writes aggr
+        "segment_sum": ([], (8 * L * N + 4 * (N + 1) + 4 * L * N) if seg
+                        else 4 * L * E + 4 * (N + 1) + (1 if infer else 2) * 4 * L * N),
         # node_net, 2 fp32 GEMMs (K = 256, 128) per node: reads aggr, x; writes a2n (+ a1n)
         "node_net": ([(N * 2 * L * (2 * L + L), PEAK_FP32_MFMA)], 2 * 4 * L * N + (1 if infer else 2) * 4 * L * N),
         "pq_scatter_bwd": ([], 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
@@ -218,7 +224,7 @@ def load_pmc(fused: bool) -> dict:
         for k, prefix in PMC_NAMES.items():
             if fused and k == "edge_bwd":
                 prefix = PMC_NAMES["edge_bwd_w2"]
-            hit = [v for name, v in data.items() if name.startswith(prefix)]
+            hit = [v for name, v in data.items() if name.startswith(prefix if isinstance(prefix, tuple) else (prefix,))]
             if hit:
                 pmc[k] = round(hit[0]["total"])
     return pmc
@@ -330,7 +336,7 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
     fused = eng.fused_edge_wgrad
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
-    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused)
+    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, getattr(eng, "seg_sums", False))
     pmc = load_pmc(fused) if with_pmc else {}
     step_s = el * ev_steps / args.steps
     dominant = max([k for k in ("edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])

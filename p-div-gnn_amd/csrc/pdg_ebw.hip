@@ -574,23 +574,48 @@ __global__ __launch_bounds__(512) void enc_narrow_reduce_kernel(const double* __
 // C = Wc e is an exact fp32 product (v_mfma_f32_16x16x4_f32, Wc rows as register A fragments, e
 // from an fp32 row tile): bitwise edge_fwd_kernel's C.  (C in bf16x6 biased the LayerNorm statistics
 // the way bf16x6 node_net did: parameter gradients 2e-4 from fp64 instead of 2.5e-6, measured.)
+//
+// With SEG the kernel also forms the message sums of the aggregation (models.py:215-217) from
+// the a2m row tile: sums[v] = sum over v's incoming edges of a2m (raw, before the message
+// LayerNorm, whose statistics are known only after this launch; the consumer applies it:
+// sum LN(a2m) = g (sums - deg mean) / den + deg b).  The rows are dst-sorted and a block owns a
+// contiguous range, so a node's segment is cut only at block ends: segments ending inside the
+// range are summed row by row in edge order (a round's piece added to the previous round's
+// carry) and stored; a segment running across a block end leaves a head / tail partial for
+// pdg_segsum_fixup.  In inference a2m is then not stored at all.  The a2m tiles and the dst ids
+// are double-buffered (by round parity) so a round's sums are formed during the next round's W2
+// product, off the barrier-to-barrier critical path, and their stores are not waited for by the
+// next gathers; after the last round once more.  Config 5 (inference), per call: 551 us + 71 us
+// pdg_segment_sum become 565 + 29 us pdg_segsum_finish; of the 565, the sums walk costs ~20 us and
+// its stores ~28 us (the same with fp32 stores: not bandwidth), against 40 us saved on a2m.  In
+// training a2m is stored for the backward anyway and the fused sums do not pay (engine: off).
 constexpr int EFC_TILE = X6_ROWS * OT_STRIDE;   // floats per fp32 row tile
 constexpr int EFC_ES = L + 8;                    // e tile row stride: the C operand reads are conflict free
+// segment sums (LDS, after the tiles): two a2m tiles, two rounds' dst ids, two fp64 carry rows
+constexpr int EFC_SEG_BYTES = 2 * EFC_TILE * 4 + 2 * X6_ROWS * 4 + 2 * L * 8;
+typedef double d64x4 __attribute__((ext_vector_type(4)));
+typedef double d64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-template <bool RES, bool EU>
+
+template <bool RES, bool EU, bool SEG>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
     const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ P,
     const float* __restrict__ Q, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ a1m, float* __restrict__ a2m,
-    float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m, double* __restrict__ part_e) {
+    float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m, double* __restrict__ part_e,
+    double* __restrict__ sums, double* __restrict__ seg_part, int* __restrict__ seg_info) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img_m = sm;                                   // a1m
   unsigned char* img_x = sm + EBW_IMG;                         // a1e (EU)
   float* t_m = reinterpret_cast<float*>(sm + 2 * EBW_IMG);     // fp32 row tiles: a1m / a2m
   float* t_x = t_m + EFC_TILE;                                 //                 a1e / a2e
   float* t_e = t_x + EFC_TILE;                                 //                 e_t
+  float* t_s = t_e + X6_ROWS * EFC_ES;                         // SEG: a2m tiles (by round parity)
+  int* sdst0 = reinterpret_cast<int*>(t_s + 2 * EFC_TILE);     //      dst of the rounds' rows
+  double* carry = reinterpret_cast<double*>(sdst0 + 2 * X6_ROWS);   // open segment's sum, 2 rows
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
@@ -639,6 +664,64 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       *reinterpret_cast<f32x4*>(t_e + r * EFC_ES + 4 * cg) = ok ? e : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
+  // SEG: the node of the previous block's last edge (a segment of it here is a head partial),
+  // of the next block's first edge, and of the previous round's last row
+  int headnode = -1, after = -1, prev_last = -1;
+  if (SEG && r0 < r1) {
+    headnode = r0 > 0 ? dst[r0 - 1] : -1;
+    after = r1 < E ? dst[r1] : -1;
+  }
+  // the sums of round bk (parity pk, a2m tile ts): its segment pieces start at row 0 and wherever
+  // dst changes; wave w takes pieces w, w + 8, ... with lane l on features 2l, 2l + 1 (all the
+  // segment bookkeeping is wave-uniform: scalar instructions, no divergence)
+  auto walk = [&](int bk, int pk, int next_dst, bool more_k) {
+    const int nr = min(X6_ROWS, r1 - bk);
+    const int* sdst = sdst0 + pk * X6_ROWS;
+    const float* ts = t_s + pk * EFC_TILE;
+    const int rv = l < nr ? sdst[l] : -1;
+    const int pv = (l > 0 && l < nr) ? sdst[l - 1] : -1;
+    const unsigned mask = (unsigned)__ballot(l < nr && (l == 0 || rv != pv));
+    const int nseg = __popc(mask);
+    unsigned m = mask;
+    for (int i = 0; i < w; ++i) m &= m - 1;   // m's lowest set bit: piece w's first row
+    for (int s = w; s < nseg; s += EBW_WAVES) {
+      const int k0 = __builtin_ctz(m);
+      const unsigned m2 = m & (m - 1);
+      const int k1 = m2 ? __builtin_ctz(m2) : nr;
+      const int v = __builtin_amdgcn_readfirstlane(sdst[k0]);
+      double acc0 = 0., acc1 = 0.;
+      if (s == 0 && v == prev_last) {
+        const d64x2 cv = *reinterpret_cast<const d64x2*>(carry + (pk ^ 1) * L + 2 * l);
+        acc0 = cv[0];
+        acc1 = cv[1];
+      }
+      for (int k = k0; k < k1; k += 8) {   // 8 rows in flight, added in row order
+        f32x2 x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = *reinterpret_cast<const f32x2*>(ts + min(k + u, k1 - 1) * OT_STRIDE + 2 * l);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const bool in = k + u < k1;   // rows past the piece add exactly 0
+          acc0 += in ? (double)x[u][0] : 0.;
+          acc1 += in ? (double)x[u][1] : 0.;
+        }
+      }
+      const d64x2 acc = {acc0, acc1};
+      const bool open = s == nseg - 1 && v == next_dst;   // the segment goes on past this round
+      if (open && more_k) {   // through an LDS-typed pointer: merged with the global store below, the
+                              // compiler emitted one flat store
+        typedef __attribute__((address_space(3))) d64x2 lds_d64x2;
+        *(lds_d64x2*)(carry + pk * L + 2 * l) = acc;
+      } else {
+        double* dstp = v == headnode ? seg_part + (size_t)(2 * blockIdx.x) * L
+                       : open        ? seg_part + (size_t)(2 * blockIdx.x + 1) * L
+                                     : sums + (size_t)v * L;
+        __builtin_nontemporal_store(acc, reinterpret_cast<d64x2*>(dstp + 2 * l));
+      }
+      for (int i = 0; i < EBW_WAVES && m; ++i) m &= m - 1;
+    }
+    prev_last = sdst[nr - 1];
+  };
   if (r0 < r1) {
     issue(r0);
     stage(r0);
@@ -646,6 +729,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   for (int base = r0; base < r1; base += X6_ROWS) {
     __syncthreads();   // e tile complete
     int dc[2] = {dq[0], dq[1]}, sc[2] = {sq[0], sq[1]};
+    const int par = ((base - r0) / X6_ROWS) & 1;
+    if (SEG && w == 0 && l < X6_ROWS) sdst0[par * X6_ROWS + l] = dc[l >> 4];   // lane l: row l
     const bool more = base + X6_ROWS < r1;
     if (more) issue(base + X6_ROWS);
     // ---- C = Wc e + b1 and the two first layers at this wave's 16 features
@@ -700,7 +785,10 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         }
       }
     }
+    // the previous round's sums (the row after its last is this round's row 0)
+    if (SEG && base > r0) walk(base - X6_ROWS, par ^ 1, sdst0[par * X6_ROWS], true);
     // ---- a2 = relu(W2 a1 + b2) for both evaluations
+    float* t_a2 = SEG ? t_s + par * EFC_TILE : t_m;
     constexpr int NI = EU ? 2 : 1;
     f32x4 d2[NI][2];
     const unsigned char* ia[NI];
@@ -717,7 +805,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         f32x4 a;
 #pragma unroll
         for (int j = 0; j < 4; ++j) a[j] = fmaxf(d2[u][nb][j] + b2o[j], 0.f);
-        *reinterpret_cast<f32x4*>((u ? t_x : t_m) + r * OT_STRIDE + oc) = a;
+        *reinterpret_cast<f32x4*>((u ? t_x : t_a2) + r * OT_STRIDE + oc) = a;
         if (ok) {
           const double p1 = (double)((a[0] + a[1]) + (a[2] + a[3]));
           const double p2 = (double)((a[0] * a[0] + a[1] * a[1]) + (a[2] * a[2] + a[3] * a[3]));
@@ -730,11 +818,26 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
       if (base + r < r1) {
-        stnt4(a2m + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_m + r * OT_STRIDE + 4 * cg));
+        if (a2m) stnt4(a2m + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_a2 + r * OT_STRIDE + 4 * cg));
         if (EU) stnt4(a2e + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
       }
     }
     if (more) stage(base + X6_ROWS);   // the e tile was last read before the second barrier
+  }
+  if (SEG && r0 < r1) walk(r0 + (r1 - 1 - r0) / X6_ROWS * X6_ROWS, ((r1 - 1 - r0) / X6_ROWS) & 1, after, false);
+  if (SEG && threadIdx.x == 0) {   // the block's partials: head (+ whether it also runs past r1), tail
+    int hd = -1, hc = 0, td = -1;
+    if (r0 < r1) {
+      if (headnode >= 0 && dst[r0] == headnode) {
+        hd = headnode;
+        hc = dst[r1 - 1] == headnode && after == headnode;
+      }
+      if (after >= 0 && dst[r1 - 1] == after && !hc) td = after;
+    }
+    seg_info[4 * blockIdx.x] = hd;
+    seg_info[4 * blockIdx.x + 1] = hc;
+    seg_info[4 * blockIdx.x + 2] = td;
+    seg_info[4 * blockIdx.x + 3] = 0;
   }
   double* red = reinterpret_cast<double*>(sm);
   __syncthreads();
@@ -839,6 +942,17 @@ extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln
                                  const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                                  const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                                  double* part_e, int with_edge_update, int nblocks, void* stream) {
+  return pdg_edge_fwd_coop_seg(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m,
+                               a2m, a1e, a2e, part_m, part_e, with_edge_update, nullptr, nullptr, nullptr, nblocks,
+                               stream);
+}
+
+extern "C" int pdg_edge_fwd_coop_seg(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                                     const float* ln_b, const float* e_res, float* e_out, const int* src,
+                                     const int* dst, const float* P, const float* Q, const float* W1, const float* b1,
+                                     const float* W2, const float* b2, float* a1m, float* a2m, float* a1e, float* a2e,
+                                     double* part_m, double* part_e, int with_edge_update, double* sums,
+                                     double* seg_part, int* seg_info, int nblocks, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd_coop: n_edges must be > 0");
   PDG_CHECK_ARG(nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_fwd_coop: bad nblocks");
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
@@ -848,17 +962,100 @@ extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln
                 "pdg_edge_fwd_coop: misaligned pointer");
   PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd_coop: edge-update outputs missing or misaligned");
-  const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float);
+  const bool seg = sums != nullptr;
+  PDG_CHECK_ARG(seg || a2m, "pdg_edge_fwd_coop: a2m may be omitted only with the segment sums");
+  PDG_CHECK_ARG(!seg || (seg_part && seg_info && PDG_ALIGNED(sums) && PDG_ALIGNED(seg_part)),
+                "pdg_edge_fwd_coop_seg: sums / seg_part / seg_info missing or misaligned");
+  const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float) + (seg ? EFC_SEG_BYTES : 0);
   hipStream_t s = (hipStream_t)stream;
-#define PDG_EFC(R, U)                                                                                              \
-  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U>), dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
-                     ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e)
-  if (e_res) {
-    if (with_edge_update) PDG_EFC(true, true); else PDG_EFC(true, false);
-  } else {
-    if (with_edge_update) PDG_EFC(false, true); else PDG_EFC(false, false);
+#define PDG_EFC(R, U, S)                                                                                              \
+  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S>), dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
+                     ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e,  \
+                     sums, seg_part, seg_info)
+#define PDG_EFC2(S)                                                \
+  if (e_res) {                                                     \
+    if (with_edge_update) PDG_EFC(true, true, S); else PDG_EFC(true, false, S);   \
+  } else {                                                         \
+    if (with_edge_update) PDG_EFC(false, true, S); else PDG_EFC(false, false, S); \
   }
+  if (seg) {
+    PDG_EFC2(true)
+  } else {
+    PDG_EFC2(false)
+  }
+#undef PDG_EFC2
 #undef PDG_EFC
   PDG_CHECK_LAUNCH("pdg_edge_fwd_coop");
+  return PDG_OK;
+}
+
+// Message sums of the nodes whose incoming edges run across a block end of
+// pdg_edge_fwd_coop_seg: the span's first block left a tail partial, the others head partials
+// (a block entirely inside the span: head with the continue flag); the block where the span
+// ends adds them in block order.  One block per edge-forward block, thread = feature.
+__global__ __launch_bounds__(L) void segsum_fixup_kernel(const double* __restrict__ seg_part,
+                                                         const int* __restrict__ seg_info, double* __restrict__ sums) {
+  const int b = blockIdx.x, c = threadIdx.x;
+  const int hd = seg_info[4 * b], hc = seg_info[4 * b + 1];
+  if (hd < 0 || hc) return;
+  int b0 = b - 1;
+  while (b0 >= 0 && seg_info[4 * b0] == hd && seg_info[4 * b0 + 1]) --b0;
+  if (b0 < 0 || seg_info[4 * b0 + 2] != hd) return;   // malformed partials (unreachable): the test sees it
+  double acc = seg_part[(size_t)(2 * b0 + 1) * L + c];
+  for (int k = b0 + 1; k <= b; ++k) acc += seg_part[(size_t)(2 * k) * L + c];
+  sums[(size_t)hd * L + c] = acc;
+}
+
+extern "C" int pdg_segsum_fixup(int nblocks, const double* seg_part, const int* seg_info, double* sums,
+                                void* stream) {
+  PDG_CHECK_ARG(nblocks > 0 && nblocks <= MAX_BLOCKS && seg_part && seg_info && sums, "pdg_segsum_fixup: bad arguments");
+  hipLaunchKernelGGL(segsum_fixup_kernel, dim3(nblocks), dim3(L), 0, (hipStream_t)stream, seg_part, seg_info, sums);
+  PDG_CHECK_LAUNCH("pdg_segsum_fixup");
+  return PDG_OK;
+}
+
+// aggr[v] = sum over v's deg edges of LN(a2m) = g (sums[v] - deg mean) / den + deg b and (xhat_sum
+// != NULL, training) xhat_sum[v] = (sums[v] - deg mean) / den, the backward's per-node sum of xhat
+// (pdg_segment_sum's outputs), evaluated in fp64 from the fp64 sums with the call's fp32 statistics
+// and rounded once; 0 for deg = 0 (those sums rows were never written).  Half-wave (32 lanes x 4
+// features) per node.
+__global__ __launch_bounds__(256) void segsum_finish_kernel(int N, const double* __restrict__ sums,
+                                                            const int* __restrict__ rowptr,
+                                                            const pdg_ln_stat* __restrict__ stp,
+                                                            const float* __restrict__ lg, const float* __restrict__ lb,
+                                                            float* __restrict__ aggr, float* __restrict__ xsum) {
+  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
+  const int nhw = blockDim.x >> 5;
+  const double mean = stp->mean, rden = 1.0 / (double)stp->den;
+  const f32x4 g = reinterpret_cast<const f32x4*>(lg)[j], b = reinterpret_cast<const f32x4*>(lb)[j];
+  for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
+    const int deg = rowptr[v + 1] - rowptr[v];
+    f32x4 a = {0.f, 0.f, 0.f, 0.f}, xs = {0.f, 0.f, 0.f, 0.f};
+    if (deg > 0) {
+      const d64x4 sv = reinterpret_cast<const d64x4*>(sums + (size_t)v * L)[j];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double h = (sv[c] - deg * mean) * rden;
+        a[c] = (float)(h * (double)g[c] + deg * (double)b[c]);
+        xs[c] = (float)h;
+      }
+    }
+    stg4(aggr + (size_t)v * L + 4 * j, a);
+    if (xsum) stg4(xsum + (size_t)v * L + 4 * j, xs);
+  }
+}
+
+extern "C" int pdg_segsum_finish(int n_nodes, const double* sums, const int* rowptr, const pdg_ln_stat* st,
+                                 const float* ln_g, const float* ln_b, float* aggr, float* xhat_sum, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0 && sums && rowptr && st && ln_g && ln_b && aggr, "pdg_segsum_finish: bad arguments");
+  PDG_CHECK_ARG(PDG_ALIGNED(sums) && PDG_ALIGNED(aggr) && PDG_ALIGNED(ln_g) && PDG_ALIGNED(ln_b) &&
+                    PDG_ALIGNED(xhat_sum),
+                "pdg_segsum_finish: misaligned pointer");
+  long want = (n_nodes + 7) / 8;
+  long cap = (long)device_cus() * 8;
+  const int grid = (int)(want < cap ? want : cap);
+  hipLaunchKernelGGL(segsum_finish_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, sums, rowptr, st,
+                     ln_g, ln_b, aggr, xhat_sum);
+  PDG_CHECK_LAUNCH("pdg_segsum_finish");
   return PDG_OK;
 }

@@ -13,7 +13,8 @@ Per message-passing step t (weights shared across steps, models.py:313-314):
   x_t = LN_n(a2n_{t-1}) + x_{t-1}           pdg_node_pq      (also P = Wa x_t, Q = Wb x_t)
   e_t = LN_e(a2e_{t-1}) + e_{t-1}           pdg_edge_fwd     (C = Wc e_t + b1, both edge_net
   a1m,a2m (message), a1e,a2e (edge upd.)                      evaluations, LN partials)
-  aggr = sum_dst LN_m(a2m)                  pdg_segment_sum
+  aggr = sum_dst LN_m(a2m)                  pdg_segment_sum (inference: sums formed in pdg_edge_fwd_coop_seg,
+                                            pdg_segsum_fixup + pdg_segsum_finish)
   a1n = relu(Wn1 [aggr, x_t] + bn1)         pdg_node_mlp1
   a2n = relu(Wn2 a1n + bn2)                 pdg_mlp2_fwd
 
@@ -122,6 +123,17 @@ class EPDEngine:
         self.coop_fwd = os.environ.get("PDG_EDGE_FWD_COOP", "1") == "1"
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
+        # inference: the cooperative edge forward also forms the aggregation's message sums in fp64
+        # (pdg_edge_fwd_coop_seg + pdg_segsum_fixup; pdg_segsum_finish applies the message LayerNorm)
+        # instead of pdg_segment_sum re-reading a2m, and a2m is not stored (config 5: 11.8 -> 11.5 ms
+        # per step, same box).  Training keeps pdg_segment_sum: a2m is stored for the backward anyway
+        # and the in-kernel sums cost more than the re-read they save (9.91 vs 10.12 ms, config 2).
+        # fp64, because fp32 raw sums (sum a2m - deg mean cancels) flipped a relu mask bit against the
+        # fp64 reference in a golden test.  PDG_SEG_SUMS=0 / PDG_SEG_SUMS_TRAIN=1 for A/B and tests.
+        self.seg_sums = self.coop_fwd and os.environ.get("PDG_SEG_SUMS", "1") == "1"
+        self.seg_sums_train = self.coop_fwd and os.environ.get("PDG_SEG_SUMS_TRAIN", "0") == "1"
+        self._seg_part = torch.empty(2 * self._nslabs_e * L, dtype=torch.float64, device=self.device)
+        self._seg_info = torch.empty(4 * self._nslabs_e, dtype=torch.int32, device=self.device)
         # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
         self.timed: dict | None = None
 
@@ -222,11 +234,21 @@ class EPDEngine:
             # the last step's edge update has no consumer (models.py:316 decodes nodes only)
             eu = t < steps - 1
             e_t = self._empty(E, L)
-            a2m = self._empty(E, L)
+            seg = bool(E) and (self.seg_sums_train if need_grad else self.seg_sums)
+            a2m = self._empty(E, L) if (need_grad or not seg) else None   # seg: a backward-only output
+            sums = torch.empty(N, L, dtype=torch.float64, device=self.device) if seg else None
             a1m = self._empty(E, L) if need_grad else None          # layer-1 outputs: backward only
             a2e = self._empty(E, L) if eu else None
             a1e = self._empty(E, L) if (eu and need_grad) else None
-            if E and self.coop_fwd:
+            if seg:
+                self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop_seg, E, _p(a2e_prev),
+                        ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm),
+                        _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e),
+                        _p(self._part_a), _p(self._part_b), int(eu), _p(sums), _p(self._seg_part),
+                        _p(self._seg_info), self._nslabs_e, s)
+                self._nparts.value = self._nslabs_e
+                lib.pdg_segsum_fixup(self._nslabs_e, _p(self._seg_part), _p(self._seg_info), _p(sums), s)
+            elif E and self.coop_fwd:
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop, E, _p(a2e_prev), ste_prev,
                         _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm),
                         _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a),
@@ -245,7 +267,14 @@ class EPDEngine:
                     if eu:
                         self._finalize(self._part_b, E * L, st[i_e], s, True)
             # aggregation (models.py:215-217) and node_net (:240-243)
-            if E:
+            a1n = self._empty(N, L) if need_grad else None
+            a2n = self._empty(N, L)
+            if seg:
+                aggr = self._empty(N, L)
+                xs = self._empty(N, L) if need_grad else None
+                self._t("segment_sum", lib.pdg_segsum_finish, N, _p(sums), _p(plan.rowptr_dst), st[i_m], _p(ge),
+                        _p(be), _p(aggr), _p(xs), s)
+            elif E:
                 aggr = self._empty(N, L)
                 xs = self._empty(N, L) if need_grad else None
                 self._t("segment_sum", lib.pdg_segment_sum, N, _p(plan.rowptr_dst), _p(a2m), st[i_m], _p(ge),
@@ -253,8 +282,6 @@ class EPDEngine:
             else:
                 aggr = torch.zeros(N, L, dtype=torch.float32, device=self.device)
                 xs = torch.zeros(N, L, dtype=torch.float32, device=self.device) if need_grad else None
-            a1n = self._empty(N, L) if need_grad else None
-            a2n = self._empty(N, L)
             self._t("node_net", lib.pdg_node_net, N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(Wn2), _p(bn2), _p(a1n),
                     _p(a2n), _p(self._part_a), np_, s)
             if t < steps - 1 and self.sync is None:
