@@ -114,6 +114,13 @@ __device__ __forceinline__ void stg4(float* __restrict__ p, const f32x4& x) {
   *reinterpret_cast<f32x4*>(p) = x;
 #endif
 }
+// A 16-byte load through a global-address-space pointer: for row pointers the compiler cannot
+// place (read from an LDS table), which it would otherwise load with FLAT instructions; those
+// count in both vmcnt and lgkmcnt, so every later LDS wait also waits for them.
+__device__ __forceinline__ f32x4 ldg4(const float* p) {
+  typedef __attribute__((address_space(1))) const f32x4 g_f32x4;
+  return *(g_f32x4*)p;
+}
 // A 16-byte row store with the fragment stores' policy (nontemporal with PDG_NT_ST).
 __device__ __forceinline__ void stnt4(float* __restrict__ p, const f32x4& x) { st4(p, 0, x); }
 // Feature index of fragment element s in lane quarter q.

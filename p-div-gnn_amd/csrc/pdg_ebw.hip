@@ -160,12 +160,23 @@ __device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const 
                                                 float* red) {
   const int l = lane_id(), w = wave_id(), h = l >> 5, c = l & 31;
   const int ob = 32 * (w & 3), ib = 64 * (w >> 2);
+  // every load before any store: vmcnt counts loads and stores together in issue order, so a
+  // load behind a store cannot be waited for alone; interleaved (slab[] += acc), the compiler
+  // emitted ~25 load -> wait -> store round trips, one slab line at a time
+  float old[2][16];
 #pragma unroll
   for (int b = 0; b < 2; ++b)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h, i = ib + 32 * b + c;
-      slab[o * L + i] += acc[b][r];
+      old[b][r] = slab[o * L + i];
+    }
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h, i = ib + 32 * b + c;
+      slab[o * L + i] = old[b][r] + acc[b][r];
     }
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   *reinterpret_cast<f32x4*>(red + rg * L + 4 * cg) = bsum;

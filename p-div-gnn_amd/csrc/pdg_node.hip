@@ -228,9 +228,9 @@ __device__ __forceinline__ void fetch_gz2(Gz2Regs& rg, int t, int N, int lt, con
   }
 }
 
-__device__ __forceinline__ void store_gz2(float* __restrict__ buf, int t, int N, int lt, const Gz2Regs& rg,
-                                          const LNStat& st, const pdg_ln_bwd& lb, const float* __restrict__ g,
-                                          float* __restrict__ gz2_out) {
+__device__ __forceinline__ void store_gz2(float* __restrict__ buf, float* __restrict__ gybuf, int t, int N, int lt,
+                                          const Gz2Regs& rg, const LNStat& st, const pdg_ln_bwd& lb,
+                                          const float* __restrict__ g, float* __restrict__ gz2_out) {
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
     const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
@@ -243,6 +243,7 @@ __device__ __forceinline__ void store_gz2(float* __restrict__ buf, int t, int N,
       z[e] = rg.av[u][e] > 0.f ? ga : 0.f;
     }
     *reinterpret_cast<f32x4*>(buf + rr * GS + 4 * j) = z;
+    *reinterpret_cast<f32x4*>(gybuf + rr * GS + 4 * j) = rg.gv[u];   // the residual term, for the compute waves
     if (node < N) stg4(gz2_out + (size_t)node * L + 4 * j, z);
   }
 }
@@ -255,8 +256,11 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
     const float* __restrict__ W2T, const float* __restrict__ W1aT, const float* __restrict__ W1bT,
     float* __restrict__ gz2_out, float* __restrict__ gz1_out, float* __restrict__ gaggr,
     float* __restrict__ gx_part, const double* __restrict__ lb_pairs, int lb_npairs) {
-  __shared__ __attribute__((aligned(16))) float gz2t[3 * TILE * GS];
-  __shared__ __attribute__((aligned(16))) float gz1t[2 * TILE * GS];
+  // LDS (dynamic, 69.6 KB): gz2 tiles and the loaders' gy rows (3 buffers each), gz1 tiles (2)
+  extern __shared__ __attribute__((aligned(16))) float nbw_sm[];
+  float* gz2t = nbw_sm;
+  float* gyt = gz2t + 3 * TILE * GS;
+  float* gz1t = gyt + 3 * TILE * GS;
   const int w = wave_id(), l = lane_id();
   const bool loader = w >= NU_COMPUTE;
   const int ntiles = tiles_of(N);
@@ -283,8 +287,16 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
     for (int k = 0; k < 2; ++k)
       if (nu_tile(k) < ntiles) {
         fetch_gz2(rg, nu_tile(k), N, lt, gy, a2);
-        store_gz2(gz2t + k * TILE * GS, nu_tile(k), N, lt, rg, st, lb, lg, gz2_out);
+        store_gz2(gz2t + k * TILE * GS, gyt + k * TILE * GS, nu_tile(k), N, lt, rg, st, lb, lg, gz2_out);
       }
+  }
+  // compute waves: the relu-mask rows of a1 are loaded one tile ahead, before the previous tile's
+  // stores (vmcnt counts loads and stores together in issue order: a load issued behind the stores
+  // is waited for together with them)
+  f32x4 a1v = {0.f, 0.f, 0.f, 0.f};
+  if (!loader && nu_tile(0) < ntiles) {
+    const int row0 = nu_tile(0) * TILE + r;
+    a1v = *reinterpret_cast<const f32x4*>(a1 + (size_t)(row0 < N ? row0 : N - 1) * L + oc);
   }
   __syncthreads();
   for (int i = 0;; ++i) {
@@ -292,13 +304,11 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
     if (tile >= ntiles) break;   // uniform across the block
     const int row = tile * TILE + r;
     const bool valid = row < N;
-    const int rc = valid ? row : N - 1;
     const bool ahead = nu_tile(i + 2) < ntiles;
     float* g1 = gz1t + (i & 1) * TILE * GS;
     if (loader) {
       if (ahead) fetch_gz2(rg, nu_tile(i + 2), N, lt, gy, a2);
     } else {
-      const f32x4 a1v = *reinterpret_cast<const f32x4*>(a1 + (size_t)rc * L + oc);
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       const float* zr = gz2t + (i % 3) * TILE * GS + r * GS + 4 * q;
 #pragma unroll
@@ -315,9 +325,11 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
     }
     __syncthreads();
     if (loader) {
-      if (ahead) store_gz2(gz2t + ((i + 2) % 3) * TILE * GS, nu_tile(i + 2), N, lt, rg, st, lb, lg, gz2_out);
+      if (ahead)
+        store_gz2(gz2t + ((i + 2) % 3) * TILE * GS, gyt + ((i + 2) % 3) * TILE * GS, nu_tile(i + 2), N, lt, rg, st,
+                  lb, lg, gz2_out);
     } else {
-      const f32x4 res = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + oc);
+      const f32x4 res = *reinterpret_cast<const f32x4*>(gyt + (i % 3) * TILE * GS + r * GS + oc);
       f32x4 acc_a = {0.f, 0.f, 0.f, 0.f}, acc_b = {0.f, 0.f, 0.f, 0.f};
       const float* zr = g1 + r * GS + 4 * q;
 #pragma unroll
@@ -330,6 +342,10 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_bwd_kernel(
         }
       }
       acc_b += res;
+      if (nu_tile(i + 1) < ntiles) {
+        const int rn = nu_tile(i + 1) * TILE + r;
+        a1v = *reinterpret_cast<const f32x4*>(a1 + (size_t)(rn < N ? rn : N - 1) * L + oc);
+      }
       if (valid) {
         stg4(gaggr + (size_t)row * L + oc, acc_a);
         stg4(gx_part + (size_t)row * L + oc, acc_b);
@@ -352,7 +368,8 @@ extern "C" int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, cons
   const int tiles = tiles_of(n_nodes);
   const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
   const int grid = tiles < cap ? tiles : cap;
-  hipLaunchKernelGGL(node_bwd_kernel, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes, gy, a2n, a1n,
+  const size_t shm = (size_t)8 * TILE * GS * sizeof(float);
+  hipLaunchKernelGGL(node_bwd_kernel, dim3(grid), dim3(NU_THREADS), shm, (hipStream_t)stream, n_nodes, gy, a2n, a1n,
                      st, lb, ln_g, Wn2T, Wn1aT, Wn1bT, gz2, gz1, gaggr, gx_part, lb_pairs, lb_npairs);
   PDG_CHECK_LAUNCH("pdg_node_bwd");
   return PDG_OK;

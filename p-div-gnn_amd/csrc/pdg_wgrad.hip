@@ -293,8 +293,8 @@ __device__ __forceinline__ void wg_load(const WgTable* tb, int nseg, long base, 
     if (vr < r1) {
       while (seg[i] + 1 < nseg && vr >= tb->start[seg[i] + 1]) ++seg[i];
       const long r = vr - tb->start[seg[i]];
-      gr[i] = reinterpret_cast<const f32x4*>(tb->G[seg[i]] + r * L)[c4];
-      xr[i] = reinterpret_cast<const f32x4*>(tb->X[seg[i]] + r * L)[c4];
+      gr[i] = ldg4(tb->G[seg[i]] + r * L + 4 * c4);
+      xr[i] = ldg4(tb->X[seg[i]] + r * L + 4 * c4);
     } else {
       gr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -440,8 +440,8 @@ __device__ __forceinline__ void x6_load(const WgTable* tb, int nseg, long base, 
     if (vr < r1) {
       while (seg + 1 < nseg && vr >= tb->start[seg + 1]) ++seg;
       const long r = vr - tb->start[seg];
-      gr[i] = reinterpret_cast<const f32x4*>(tb->G[seg] + r * L)[cg];
-      xr[i] = reinterpret_cast<const f32x4*>(tb->X[seg] + r * L)[cg];
+      gr[i] = ldg4(tb->G[seg] + r * L + 4 * cg);
+      xr[i] = ldg4(tb->X[seg] + r * L + 4 * cg);
     } else {
       gr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -656,7 +656,7 @@ __device__ __forceinline__ void x6_load3(const WgTable3* tb, int nseg, long base
       while (seg + 1 < nseg && vr >= tb->start[seg + 1]) ++seg;
       const long r = vr - tb->start[seg];
 #pragma unroll
-      for (int a = 0; a < 3; ++a) v[a][i] = reinterpret_cast<const f32x4*>(tb->A[a][seg] + r * L)[cg];
+      for (int a = 0; a < 3; ++a) v[a][i] = ldg4(tb->A[a][seg] + r * L + 4 * cg);
     } else {
 #pragma unroll
       for (int a = 0; a < 3; ++a) v[a][i] = f32x4{0.f, 0.f, 0.f, 0.f};
