@@ -385,6 +385,11 @@ int pdg_div_bwd(int n_graphs, const int* ptr, int n_nodes, const int* at_rowptr,
 int pdg_transpose(int rows, int cols, int ld, const float* in, float* out, void* stream);
 /* n <= 16 transposes of 128 x 128 blocks in one launch: out_ptrs[i] (128 x 128, row-major) =
  * in_ptrs[i]^T, in_ptrs[i] with row stride lds[i]; host arrays. */
+/* Several pdg_wgrad_reduce calls in one launch (njobs <= 16): job i adds the sum of its nslabs[i]
+ * slabs into grad_W[i] (row stride ld[i], column offset col0[i]) and, when grad_b[i] != NULL,
+ * the bias sums into grad_b[i].  Slab sets must be distinct buffers. */
+int pdg_wgrad_reduce_batch(int njobs, const float* const* slabs, const int* nslabs, float* const* grad_W,
+                           const int* ld, const int* col0, float* const* grad_b, void* stream);
 int pdg_transpose128_batch(int n, const float* const* in_ptrs, const int* lds, float* const* out_ptrs, void* stream);
 /* *flag = 1 if any grad element is inf/NaN (GradScaler's skip test, gnn_train.py:205-207). */
 int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream);

@@ -154,6 +154,72 @@ extern "C" int pdg_wgrad_reduce(float* slabs, int nslabs, float* grad_W, int ld,
   return PDG_OK;
 }
 
+// Every weight's slab reduction of a backward pass in one launch (the two-pass pdg_wgrad_reduce
+// per weight cost 2 launches of ~6 us each, mostly fixed cost).  Block (x, job): elements
+// 32 x .. 32 x + 31 of the job's slab; thread (e = t & 31, group g = t >> 5) sums slabs g, g + 8, ..
+// (8 loads in flight), then the 8 group sums are added in group order and added into gW / gb.
+constexpr int WRB_MAX = 16;
+struct WgradReduceJobs {
+  const float* slabs[WRB_MAX];
+  float* gW[WRB_MAX];
+  float* gb[WRB_MAX];
+  int nslabs[WRB_MAX], ld[WRB_MAX], col0[WRB_MAX];
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(WgradReduceJobs jobs) {
+  __shared__ float red[8][33];
+  const int j = blockIdx.y;
+  const float* __restrict__ slabs = jobs.slabs[j];
+  const int n = jobs.nslabs[j];
+  const int el = threadIdx.x & 31, g = threadIdx.x >> 5;
+  const int e = blockIdx.x * 32 + el;
+  float acc = 0.f;
+  if (e < SLAB) {
+    for (int b0 = g; b0 < n; b0 += 64) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = b0 + 8 * u < n ? slabs[(size_t)(b0 + 8 * u) * SLAB + e] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+  }
+  red[g][el] = acc;
+  __syncthreads();
+  if (g == 0 && e < SLAB) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += red[k][el];
+    if (e < L * L) {
+      const int o = e / L, i = e % L;
+      jobs.gW[j][(size_t)o * jobs.ld[j] + jobs.col0[j] + i] += s;
+    } else if (jobs.gb[j]) {
+      jobs.gb[j][e - L * L] += s;
+    }
+  }
+}
+
+extern "C" int pdg_wgrad_reduce_batch(int njobs, const float* const* slabs, const int* nslabs, float* const* grad_W,
+                                      const int* ld, const int* col0, float* const* grad_b, void* stream) {
+  PDG_CHECK_ARG(njobs > 0 && njobs <= WRB_MAX && slabs && nslabs && grad_W && ld && col0 && grad_b,
+                "pdg_wgrad_reduce_batch: bad arguments");
+  WgradReduceJobs jobs;
+  for (int i = 0; i < njobs; ++i) {
+    PDG_CHECK_ARG(slabs[i] && grad_W[i] && nslabs[i] > 0 && nslabs[i] <= MAX_BLOCKS && ld[i] >= L &&
+                      col0[i] >= 0 && col0[i] + L <= ld[i],
+                  "pdg_wgrad_reduce_batch: bad job");
+    jobs.slabs[i] = slabs[i];
+    jobs.gW[i] = grad_W[i];
+    jobs.gb[i] = grad_b[i];
+    jobs.nslabs[i] = nslabs[i];
+    jobs.ld[i] = ld[i];
+    jobs.col0[i] = col0[i];
+  }
+  hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3((SLAB + 31) / 32, njobs), dim3(256), 0, (hipStream_t)stream,
+                     jobs);
+  PDG_CHECK_LAUNCH("pdg_wgrad_reduce_batch");
+  return PDG_OK;
+}
+
 // ============================================================================ narrow weight gradient
 // T[c][i] = sum_k Wide[k][c] * Narrow[k][i], c < 128, i < K <= 8.  Half-wave per row.
 template <int K>

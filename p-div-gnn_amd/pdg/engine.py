@@ -356,6 +356,7 @@ class EPDEngine:
         # kernel reduces the pairs (include/pdivgnn.h, pdg_ln_colsum)
         acc = self._ln_acc
         acc.zero_()
+        reds = []   # deferred slab reductions (one pdg_wgrad_reduce_batch launch at the end)
         ACC_N, ACC_E, ACC_NE, ACC_EE = (acc[i] for i in range(4))
         S = ctx.steps
         pairs = torch.empty(3 * S + 2, self.max_blocks * 2, dtype=torch.float64, device=self.device)
@@ -498,8 +499,7 @@ class EPDEngine:
                 self._t("edge_enc_bwd", lib.pdg_edge_enc_bwd, E, _p(ge_next), _p(ctx.a2_ee), _p(ctx.e_in),
                         _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]), st[1], None, pe, ne,
                         _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(slabs_ee), _p(nsum), nse, s)
-                lib.pdg_wgrad_reduce(_p(slabs_ee), nse, _p(G["edge_encoder.2.weight"]), L, 0,
-                                     _p(G["edge_encoder.2.bias"]), s)
+                reds.append((slabs_ee, nse, G["edge_encoder.2.weight"], L, 0, G["edge_encoder.2.bias"]))
                 lib.pdg_enc_narrow_reduce(_p(nsum), nse, _p(G["edge_encoder.0.weight"]),
                                           _p(G["edge_encoder.0.bias"]), s)
             else:
@@ -530,12 +530,13 @@ class EPDEngine:
         ]
         ns = self._nslabs
         if getattr(self, "_slabs", None) is None or self._slabs.device != self.device:
-            self._slabs = torch.empty(ns, L * L + L, dtype=torch.float32, device=self.device)
+            # one slab set per deferred weight (the reductions run batched at the end)
+            self._slabs = torch.empty(len(red), ns, L * L + L, dtype=torch.float32, device=self.device)
         # the weight pairs that share an operand, one pass each (pdg_wgrad_pairs): Wa / Wb against x
         # (gP, gQ), node_net.0's halves from gz1n (against aggr, x)
         nsp = self._nslabs_p
         if getattr(self, "_slabs_p", None) is None or self._slabs_p.device != self.device:
-            self._slabs_p = torch.empty(2, nsp, L * L + L, dtype=torch.float32, device=self.device)
+            self._slabs_p = torch.empty(2, 2, nsp, L * L + L, dtype=torch.float32, device=self.device)
         pairs_w = [
             (1, [(g, q, x, n) for (g, x, n), (q, _, _) in zip(segs.pop("Wa"), segs.pop("Wb"))],
              ("processor.edge_net.0.weight", 3 * L, 0, None), ("processor.edge_net.0.weight", 3 * L, L, None)),
@@ -543,29 +544,46 @@ class EPDEngine:
              ("processor.node_net.0.weight", 2 * L, 0, "processor.node_net.0.bias"),
              ("processor.node_net.0.weight", 2 * L, L, None)),
         ]
-        for shx, sl, (w0n, ld0, c00, b0n), (w1n, ld1, c01, b1n) in pairs_w:
+        def reduce_now_or_later(slabs, n, wname, ld, col0, bname, later):
+            job = (slabs, n, G[wname], ld, col0, G[bname] if bname else None)
+            if later:
+                reds.append(job)
+            else:   # a slab set reused by the next chunk: reduce before it is overwritten
+                lib.pdg_wgrad_reduce(_p(slabs), n, _p(job[2]), ld, col0, _p(job[5]), s)
+
+        for gi, (shx, sl, (w0n, ld0, c00, b0n), (w1n, ld1, c01, b1n)) in enumerate(pairs_w):
+            sp0, sp1 = self._slabs_p[gi]
             for c0 in range(0, len(sl), 32):
                 chunk = sl[c0:c0 + 32]
                 n = len(chunk)
                 arr = [(ctypes.c_void_p * n)(*[t[k].data_ptr() for t in chunk]) for k in range(3)]
                 rw = (ctypes.c_int * n)(*[t[3] for t in chunk])
-                self._t("wgrad_pair", lib.pdg_wgrad_pairs, n, arr[0], arr[1], arr[2], rw, shx,
-                        _p(self._slabs_p[0]), _p(self._slabs_p[1]), nsp, s)
-                lib.pdg_wgrad_reduce(_p(self._slabs_p[0]), nsp, _p(G[w0n]), ld0, c00, _p(G[b0n]) if b0n else None, s)
-                lib.pdg_wgrad_reduce(_p(self._slabs_p[1]), nsp, _p(G[w1n]), ld1, c01, _p(G[b1n]) if b1n else None, s)
-        red = [r for r in red if r[0] in segs]
-        for key, wname, ld, col0, bname in red:
+                self._t("wgrad_pair", lib.pdg_wgrad_pairs, n, arr[0], arr[1], arr[2], rw, shx, _p(sp0), _p(sp1), nsp,
+                        s)
+                later = len(sl) <= 32
+                reduce_now_or_later(sp0, nsp, w0n, ld0, c00, b0n, later)
+                reduce_now_or_later(sp1, nsp, w1n, ld1, c01, b1n, later)
+        red_k = [r for r in red if r[0] in segs]
+        for key, wname, ld, col0, bname in red_k:
             sl = segs[key]
+            slabs_k = self._slabs[[r[0] for r in red].index(key)]
             for c0 in range(0, len(sl), 32):
                 chunk = sl[c0:c0 + 32]
                 n = len(chunk)
                 gp = (ctypes.c_void_p * n)(*[g.data_ptr() for g, _, _ in chunk])
                 xp = (ctypes.c_void_p * n)(*[x.data_ptr() for _, x, _ in chunk])
                 rw = (ctypes.c_int * n)(*[r for _, _, r in chunk])
-                self._t("wgrad_" + key, lib.pdg_wgrad_segments, n, gp, xp, rw, _p(self._slabs), ns, s)
-                lib.pdg_wgrad_reduce(_p(self._slabs), ns, _p(G[wname]), ld, col0, _p(G[bname]) if bname else None, s)
+                self._t("wgrad_" + key, lib.pdg_wgrad_segments, n, gp, xp, rw, _p(slabs_k), ns, s)
+                reduce_now_or_later(slabs_k, ns, wname, ld, col0, bname, len(sl) <= 32)
         if fused:   # the slabs of the fused edge backward, accumulated over all steps
-            lib.pdg_wgrad_reduce(_p(slabs_w2), nse, _p(G["processor.edge_net.2.weight"]), L, 0,
-                                 _p(G["processor.edge_net.2.bias"]), s)
-            lib.pdg_wgrad_reduce(_p(slabs_wc), nse, _p(G["processor.edge_net.0.weight"]), 3 * L, 2 * L,
-                                 _p(G["processor.edge_net.0.bias"]), s)
+            reds.append((slabs_w2, nse, G["processor.edge_net.2.weight"], L, 0, G["processor.edge_net.2.bias"]))
+            reds.append((slabs_wc, nse, G["processor.edge_net.0.weight"], 3 * L, 2 * L,
+                         G["processor.edge_net.0.bias"]))
+        # every deferred slab reduction in one launch
+        for c0 in range(0, len(reds), 16):
+            jb = reds[c0:c0 + 16]
+            n = len(jb)
+            VP, IA = ctypes.c_void_p * n, ctypes.c_int * n
+            lib.pdg_wgrad_reduce_batch(n, VP(*[_p(j[0]) for j in jb]), IA(*[j[1] for j in jb]),
+                                       VP(*[_p(j[2]) for j in jb]), IA(*[j[3] for j in jb]),
+                                       IA(*[j[4] for j in jb]), VP(*[_p(j[5]) for j in jb]), s)

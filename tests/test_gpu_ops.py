@@ -723,3 +723,39 @@ def test_edge_fwd_coop_seg_sums(env, kind, eu):
     lib.pdg_segsum_finish(N, s1.data_ptr(), rowptr.data_ptr(), st.data_ptr(), lg.data_ptr(), lbv.data_ptr(),
                           aggr.data_ptr(), xs.data_ptr(), s)
     assert bool((xs.cpu()[~has] == 0).all()) and rel(xs, xh) < 1e-7
+
+
+def test_wgrad_reduce_batch_matches_single(env):
+    """pdg_wgrad_reduce_batch (every deferred slab reduction of a backward in one launch) against one
+    pdg_wgrad_reduce per job and an fp64 sum: column offsets, accumulation into the existing gradient
+    and the optional bias honoured, distinct slab counts per job."""
+    lib, sh, _ = env
+    s = sh()
+    SL = L * L + L
+    jobs = [(256, 3 * L, 2 * L, True), (512, 2 * L, L, False), (37, L, 0, True)]
+    slabs = [rnd(n, SL) for n, _, _, _ in jobs]
+    gW0 = [rnd(L, ld) for _, ld, _, _ in jobs]      # pre-existing gradients (accumulated into)
+    gb0 = [rnd(L) if hb else None for _, _, _, hb in jobs]
+    outs = {}
+    for mode in ("single", "batch"):
+        gW = [w.clone() for w in gW0]
+        gb = [b.clone() if b is not None else None for b in gb0]
+        if mode == "single":
+            for (n, ld, c0, hb), sl, w, b in zip(jobs, [t.clone() for t in slabs], gW, gb):   # reduces in place
+                lib.pdg_wgrad_reduce(sl.data_ptr(), n, w.data_ptr(), ld, c0, b.data_ptr() if hb else None, s)
+        else:
+            k = len(jobs)
+            VP, IA = ctypes.c_void_p * k, ctypes.c_int * k
+            lib.pdg_wgrad_reduce_batch(k, VP(*[t.data_ptr() for t in slabs]), IA(*[j[0] for j in jobs]),
+                                       VP(*[w.data_ptr() for w in gW]), IA(*[j[1] for j in jobs]),
+                                       IA(*[j[2] for j in jobs]),
+                                       VP(*[b.data_ptr() if b is not None else None for b in gb]), s)
+        outs[mode] = (gW, gb)
+    for i, (n, ld, c0, hb) in enumerate(jobs):
+        ref = slabs[i].double().sum(0).cpu()
+        w0, w1 = outs["single"][0][i], outs["batch"][0][i]
+        assert rel(w1, w0) < 1e-6, i
+        assert torch.equal(w1[:, :c0], gW0[i][:, :c0]) and torch.equal(w1[:, c0 + L:], gW0[i][:, c0 + L:])
+        assert rel(w1[:, c0:c0 + L].double().cpu() - gW0[i][:, c0:c0 + L].double().cpu(), ref[:L * L].view(L, L)) < 1e-5
+        if hb:
+            assert rel(outs["batch"][1][i].double().cpu() - gb0[i].double().cpu(), ref[L * L:]) < 1e-5
