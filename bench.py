@@ -251,7 +251,7 @@ def roofline(k, work, kt, ktot, step_s, pmc):
 
 
 # ---------------------------------------------------------------------------------- timing
-TIMED_KERNELS = ["edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2", "segment_sum", "node_net", "node_bwd",
+TIMED_KERNELS = ["edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2", "segment_sum", "node_net", "node_bwd", "edge_enc_fwd",
                  "node_pq", "gemm_sum2", "pq_scatter_bwd"]
 
 

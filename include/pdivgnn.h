@@ -233,6 +233,11 @@ int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* 
  * ge_out = ge_next + WcT gC.  Writes gz2m, gz1m, gz2e, gz1e, gC, ge_out.
  * ge_next == NULL: the edge-update branch had no consumer (last step): gz2e/gz1e are not
  * written, gC = gz1m, ge_out = WcT gC. */
+/* Edge encoder forward (models.py:264-275, 1 -> 128 -> 128) in the block-cooperative layout: a2 =
+ * relu(W2 relu(w0 e_in + b0) + b2) with the W2 product in bf16x6 (as pdg_edge_fwd's), and the
+ * LayerNorm partials of a2 (nblocks pairs).  a1 is not stored (pdg_edge_enc_bwd recomputes it). */
+int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0, const float* b0, const float* W2,
+                     const float* b2, float* a2, double* partials, int nblocks, void* stream);
 /* pdg_edge_fwd in the block-cooperative layout (pdg_ebw.hip): nblocks blocks of 512 threads, one
  * contiguous row range each, Wc (fp32) and W2 (bf16 terms) stationary in registers, whole-row HBM
  * access.  Same outputs (C bitwise, the W2 products to fp32 rounding); part_m / part_e get nblocks

@@ -866,6 +866,80 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   }
 }
 
+// ============================================================================ edge encoder forward
+// The edge encoder (models.py:264-275, input 1 -> 128 -> 128 + the LayerNorm partials of the
+// output) in the cooperative layout: a1 = relu(w0 e + b0) formed per element (encoder_kernel's
+// formula, bitwise), W2 a1 as a bf16x6 product with W2 stationary in registers (the W2 products
+// of the edge forward), a2 rows stored whole through an fp32 row tile.  Replaces the fp32-MFMA
+// encoder_kernel<1> (LDS weights), which the W2 product's matrix time bounded.  a1 is not stored
+// (pdg_edge_enc_bwd recomputes it).
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_fwd_kernel(
+    int E, const float* __restrict__ e_in, const float* __restrict__ w0, const float* __restrict__ b0,
+    const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ a2,
+    double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img = sm;                                     // a1 (bf16x6)
+  float* t_a = reinterpret_cast<float*>(sm + EBW_IMG);         // a2 row tile
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(E, r0, r1);
+  WSlice ws2;
+  load_wslice(ws2, W2, w);
+  const f32x4 w04 = *reinterpret_cast<const f32x4*>(w0 + 4 * cg);
+  const f32x4 b04 = *reinterpret_cast<const f32x4*>(b0 + 4 * cg);
+  const f32x4 b2o = *reinterpret_cast<const f32x4*>(b2 + oc);
+  double s1 = 0, s2 = 0;
+  float pe[2];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) pe[u] = e_in[clamp_row(base + rg + 16 * u, r1)];
+  };
+  if (r0 < r1) issue(r0);
+  for (int base = r0; base < r1; base += X6_ROWS) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      f32x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = fmaxf(fmaf(w04[j], pe[u], 0.f) + b04[j], 0.f);
+      img_store4(img, r, cg, base + r < r1 ? a : f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+    __syncthreads();   // the a1 image is complete
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    f32x4 d[1][2];
+    const unsigned char* imgs[1] = {img};
+    gemm_round<1>(d, ws2, imgs);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = 16 * nb + (l & 15);
+      f32x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = fmaxf(d[0][nb][j] + b2o[j], 0.f);
+      *reinterpret_cast<f32x4*>(t_a + r * OT_STRIDE + oc) = a;
+      if (base + r < r1) {
+        s1 += (double)((a[0] + a[1]) + (a[2] + a[3]));
+        s2 += (double)((a[0] * a[0] + a[1] * a[1]) + (a[2] * a[2] + a[3] * a[3]));
+      }
+    }
+    __syncthreads();   // the a2 tile is complete; the image is free
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      if (base + r < r1)
+        stnt4(a2 + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_a + r * OT_STRIDE + 4 * cg));
+    }
+  }
+  double* red = reinterpret_cast<double*>(sm);
+  __syncthreads();
+  block_sum2(s1, s2, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s1;
+    part[2 * blockIdx.x + 1] = s2;
+  }
+}
+
 // ============================================================================ C ABI
 extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
@@ -1068,5 +1142,18 @@ extern "C" int pdg_segsum_finish(int n_nodes, const double* sums, const int* row
   hipLaunchKernelGGL(segsum_finish_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, sums, rowptr, st,
                      ln_g, ln_b, aggr, xhat_sum);
   PDG_CHECK_LAUNCH("pdg_segsum_finish");
+  return PDG_OK;
+}
+
+extern "C" int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0, const float* b0, const float* W2,
+                                const float* b2, float* a2, double* partials, int nblocks, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_enc_fwd: bad sizes");
+  PDG_CHECK_ARG(e_in && w0 && b0 && W2 && b2 && a2 && partials, "pdg_edge_enc_fwd: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(w0) && PDG_ALIGNED(b0) && PDG_ALIGNED(W2) && PDG_ALIGNED(b2) && PDG_ALIGNED(a2),
+                "pdg_edge_enc_fwd: misaligned pointer");
+  const size_t shm = EBW_IMG + (size_t)EFC_TILE * sizeof(float);
+  hipLaunchKernelGGL(edge_enc_fwd_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, n_edges, e_in,
+                     w0, b0, W2, b2, a2, partials);
+  PDG_CHECK_LAUNCH("pdg_edge_enc_fwd");
   return PDG_OK;
 }

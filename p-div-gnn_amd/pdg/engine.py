@@ -132,6 +132,9 @@ class EPDEngine:
         # fp64 reference in a golden test.  PDG_SEG_SUMS=0 / PDG_SEG_SUMS_TRAIN=1 for A/B and tests.
         self.seg_sums = self.coop_fwd and os.environ.get("PDG_SEG_SUMS", "1") == "1"
         self.seg_sums_train = self.coop_fwd and os.environ.get("PDG_SEG_SUMS_TRAIN", "0") == "1"
+        # edge encoder forward blocks (pdg_edge_enc_fwd: 104 VGPRs, 41 KB LDS per 8-wave block)
+        self._enc_blocks = min(int(os.environ.get("PDG_ENC_BLOCKS_PER_CU", "2")) *
+                               torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
         self._seg_part = torch.empty(2 * self._nslabs_e * L, dtype=torch.float64, device=self.device)
         self._seg_info = torch.empty(4 * self._nslabs_e, dtype=torch.int32, device=self.device)
         # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
@@ -200,7 +203,14 @@ class EPDEngine:
         # pdg_edge_enc_bwd recomputes it from the scalar input
         a1_ee = self._empty(E, L) if (need_grad and not self.fused_edge_wgrad) else None
         a2_ee = self._empty(E, L)
-        if E:
+        if E and a1_ee is None:   # bf16x6 W2 product, register-stationary (pdg_edge_enc_fwd)
+            nb = self._enc_blocks
+            self._t("edge_enc_fwd", lib.pdg_edge_enc_fwd, E, _p(e_in), _p(P["edge_encoder.0.weight"]),
+                    _p(P["edge_encoder.0.bias"]), _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]),
+                    _p(a2_ee), _p(self._part_a), nb, s)
+            self._nparts.value = nb
+            self._finalize(self._part_a, E * L, st[1], s, True)
+        elif E:
             lib.pdg_encoder_fwd(E, 1, _p(e_in), _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]),
                                 _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]), _p(a1_ee), _p(a2_ee),
                                 _p(self._part_a), np_, s)

@@ -759,3 +759,24 @@ def test_wgrad_reduce_batch_matches_single(env):
         assert rel(w1[:, c0:c0 + L].double().cpu() - gW0[i][:, c0:c0 + L].double().cpu(), ref[:L * L].view(L, L)) < 1e-5
         if hb:
             assert rel(outs["batch"][1][i].double().cpu() - gb0[i].double().cpu(), ref[L * L:]) < 1e-5
+
+
+@pytest.mark.parametrize("E,nb", [(77, 37), (4099, 37), (20000, 512)])
+def test_edge_enc_fwd_vs_fp64(env, E, nb):
+    """pdg_edge_enc_fwd (edge encoder, W2 product in bf16x6, register-stationary) against an fp64
+    restatement: a2 to fp32 rounding, the LayerNorm partials' (sum, sum of squares) to 1e-6."""
+    lib, sh, _ = env
+    s = sh()
+    e_in = rnd(E)
+    w0, b0 = lin(L, 1)
+    W2, b2 = lin(L, L)
+    a2 = torch.full((E, L), float("nan"), device="cuda")
+    part = torch.zeros(2 * nb, dtype=torch.float64, device="cuda")
+    lib.pdg_edge_enc_fwd(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                         a2.data_ptr(), part.data_ptr(), nb, s)
+    a1 = torch.relu(e_in.double()[:, None] * w0.double()[:, 0][None, :] + b0.double())
+    ref = torch.relu(a1 @ W2.double().T + b2.double())
+    assert rel(a2, ref) < TOL
+    p = part.view(nb, 2).sum(0).cpu()
+    assert abs(float(p[0]) - float(ref.sum())) <= 1e-6 * float(ref.abs().sum())
+    assert abs(float(p[1]) - float((ref * ref).sum())) <= 1e-6 * float((ref * ref).sum())
