@@ -238,6 +238,14 @@ int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* 
  * LayerNorm partials of a2 (nblocks pairs).  a1 is not stored (pdg_edge_enc_bwd recomputes it). */
 int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0, const float* b0, const float* W2,
                      const float* b2, float* a2, double* partials, int nblocks, void* stream);
+/* pdg_gemm_sum2_rw in the block-cooperative layout (nblocks blocks of 512 threads, contiguous row
+ * ranges): out = W0T in0 + W1T in1 [+ res], both products in bf16x6 with the weights stationary in
+ * registers; partials != NULL: the LayerNorm column partials and pairs as pdg_gemm_sum2_rw (nblocks
+ * rows of 256 doubles). */
+int pdg_gemm_sum2_coop(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
+                       const float* res, float* out, const float* ln_a2, const pdg_ln_stat* ln_st,
+                       double* partials, const float* ln_g, double* pairs, int accumulate, int nblocks,
+                       void* stream);
 /* pdg_edge_fwd in the block-cooperative layout (pdg_ebw.hip): nblocks blocks of 512 threads, one
  * contiguous row range each, Wc (fp32) and W2 (bf16 terms) stationary in registers, whole-row HBM
  * access.  Same outputs (C bitwise, the W2 products to fp32 rounding); part_m / part_e get nblocks

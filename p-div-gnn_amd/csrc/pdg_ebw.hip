@@ -940,6 +940,144 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_fwd_kernel(
   }
 }
 
+// ============================================================================ node input gradient
+// pdg_gemm_sum2_rw in the cooperative layout: out = W0T in0 + W1T in1 + res (the input gradient of
+// x_t through P = Wa x, Q = Wb x plus the node_net path: in0 = gP, in1 = gQ, W0T = Wa^T, W1T = Wb^T)
+// with both weights stationary in registers as bf16 terms and the two products in bf16x6 (the
+// edge backward's W^T products), 32-row rounds, whole-row HBM access; COLS: the column partials of
+// the backward of the LayerNorm LN(ln_a2) whose upstream gradient is `out` (as gemm_sum2_rw).  The
+// fp32-MFMA kernel was bound by its matrix time (about half the fp32 MFMA rate at 12 waves / 168
+// VGPRs); this one does 2.7x less matrix work.
+__device__ __forceinline__ void gemm_sum2_round(f32x4 (&d)[2], const WSlice& ws0, const unsigned char* img0,
+                                                const WSlice& ws1, const unsigned char* img1) {
+  const int l = lane_id(), n = l & 15, kg = l >> 4;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) d[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int off = x6_addr(16 * nb + n, 64 * ks + 16 * kg);
+      bf16x8 B[3], C[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        B[p] = *reinterpret_cast<const bf16x8*>(img0 + p * X6_TERM + off);
+        C[p] = *reinterpret_cast<const bf16x8*>(img1 + p * X6_TERM + off);
+      }
+      f32x4 t = d[nb];
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws0.a[ks][2], B[0], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws0.a[ks][1], B[1], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws0.a[ks][0], B[2], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws1.a[ks][2], C[0], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws1.a[ks][1], C[1], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws1.a[ks][0], C[2], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws0.a[ks][1], B[0], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws0.a[ks][0], B[1], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws1.a[ks][1], C[0], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws1.a[ks][0], C[1], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws0.a[ks][0], B[0], t, 0, 0, 0);
+      d[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws1.a[ks][0], C[0], t, 0, 0, 0);
+    }
+}
+
+template <bool COLS>
+__global__ __launch_bounds__(EBW_THREADS, 1) void gemm_sum2_coop_kernel(
+    int N, const float* __restrict__ in0, const float* __restrict__ in1, const float* __restrict__ W0T,
+    const float* __restrict__ W1T, const float* __restrict__ res, float* __restrict__ out,
+    const float* __restrict__ ln_a2, const pdg_ln_stat* __restrict__ ln_st, double* __restrict__ part,
+    const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img0 = sm;
+  unsigned char* img1 = sm + EBW_IMG;
+  float* t_o = reinterpret_cast<float*>(sm + 2 * EBW_IMG);
+  LNStat stln;
+  if (COLS) stln = *reinterpret_cast<const LNStat*>(ln_st);
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(N, r0, r1);
+  WSlice ws0, ws1;
+  load_wslice(ws0, W0T, w);
+  load_wslice(ws1, W1T, w);
+  double cs_g[4] = {0, 0, 0, 0}, cs_x[4] = {0, 0, 0, 0};
+  f32x4 p0[2], p1[2], pres[2], pa2[2];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
+      p0[u] = *reinterpret_cast<const f32x4*>(in0 + rc);
+      p1[u] = *reinterpret_cast<const f32x4*>(in1 + rc);
+      if (res) pres[u] = *reinterpret_cast<const f32x4*>(res + rc);
+      if (COLS) pa2[u] = *reinterpret_cast<const f32x4*>(ln_a2 + rc);
+    }
+  };
+  if (r0 < r1) issue(r0);
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 rv[2], av[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const bool ok = base + r < r1;
+      img_store4(img0, r, cg, ok ? p0[u] : zero);
+      img_store4(img1, r, cg, ok ? p1[u] : zero);
+      rv[u] = res ? pres[u] : zero;
+      av[u] = COLS ? pa2[u] : zero;
+    }
+    __syncthreads();   // images complete
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    f32x4 d[2];
+    gemm_sum2_round(d, ws0, img0, ws1, img1);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) *reinterpret_cast<f32x4*>(t_o + (16 * nb + (l & 15)) * OT_STRIDE + oc) = d[nb];
+    __syncthreads();   // tile complete; the images are free for the next round
+    f32x4 sg = zero, sx = zero;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const int row = base + r;
+      if (row < r1) {
+        const f32x4 o = *reinterpret_cast<const f32x4*>(t_o + r * OT_STRIDE + 4 * cg) + rv[u];
+        stg4(out + (size_t)row * L + 4 * cg, o);
+        if (COLS) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {   // the pdg_ln_colsum formulas
+            sg[j] += o[j];
+            sx[j] += o[j] * div_den(av[u][j] - stln.mean, stln.den, stln.rstd);
+          }
+        }
+      }
+    }
+    if (COLS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cs_g[j] += (double)sg[j];
+        cs_x[j] += (double)sx[j];
+      }
+    }
+  }
+  if (COLS) {
+    // block partial = the 16 row groups' column sums, reduced in order through LDS
+    double* red = reinterpret_cast<double*>(sm);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[rg * 2 * L + 4 * cg + j] = cs_g[j];
+      red[rg * 2 * L + L + 4 * cg + j] = cs_x[j];
+    }
+    __syncthreads();
+    double* row = red + EBW_THREADS / 32 * 2 * L;
+    for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) {
+      double v = 0;
+      for (int g = 0; g < EBW_THREADS / 32; ++g) v += red[g * 2 * L + i];
+      row[i] = v;
+    }
+    __syncthreads();
+    lnb_emit(row, ln_g, part, accumulate, pairs, row + 2 * L);
+  }
+}
+
 // ============================================================================ C ABI
 extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
@@ -1155,5 +1293,32 @@ extern "C" int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0,
   hipLaunchKernelGGL(edge_enc_fwd_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, n_edges, e_in,
                      w0, b0, W2, b2, a2, partials);
   PDG_CHECK_LAUNCH("pdg_edge_enc_fwd");
+  return PDG_OK;
+}
+
+extern "C" int pdg_gemm_sum2_coop(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
+                                  const float* res, float* out, const float* ln_a2, const pdg_ln_stat* ln_st,
+                                  double* partials, const float* ln_g, double* pairs, int accumulate, int nblocks,
+                                  void* stream) {
+  PDG_CHECK_ARG(rows > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_gemm_sum2_coop: bad sizes");
+  PDG_CHECK_ARG(in0 && in1 && W0T && W1T && out, "pdg_gemm_sum2_coop: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(in0) && PDG_ALIGNED(in1) && PDG_ALIGNED(out) && PDG_ALIGNED(W0T) && PDG_ALIGNED(W1T) &&
+                    PDG_ALIGNED(res),
+                "pdg_gemm_sum2_coop: misaligned pointer");
+  // LDS: the two images, then the row tile / (COLS) the row groups' sums + one row + its scratch
+  const size_t tile = (size_t)EFC_TILE * sizeof(float);
+  const size_t cols = ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
+  if (partials) {
+    PDG_CHECK_ARG(ln_a2 && ln_st && PDG_ALIGNED(ln_a2) && (!pairs || ln_g),
+                  "pdg_gemm_sum2_coop: column partials need an aligned ln_a2, ln_st (and ln_g for pairs)");
+    const size_t shm = 2 * EBW_IMG + tile > cols ? 2 * EBW_IMG + tile : cols;
+    hipLaunchKernelGGL(gemm_sum2_coop_kernel<true>, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, rows,
+                       in0, in1, W0T, W1T, res, out, ln_a2, ln_st, partials, ln_g, pairs, accumulate);
+  } else {
+    hipLaunchKernelGGL(gemm_sum2_coop_kernel<false>, dim3(nblocks), dim3(EBW_THREADS), 2 * EBW_IMG + tile,
+                       (hipStream_t)stream, rows, in0, in1, W0T, W1T, res, out, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, 0);
+  }
+  PDG_CHECK_LAUNCH("pdg_gemm_sum2_coop");
   return PDG_OK;
 }

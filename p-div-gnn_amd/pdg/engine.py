@@ -132,6 +132,9 @@ class EPDEngine:
         # fp64 reference in a golden test.  PDG_SEG_SUMS=0 / PDG_SEG_SUMS_TRAIN=1 for A/B and tests.
         self.seg_sums = self.coop_fwd and os.environ.get("PDG_SEG_SUMS", "1") == "1"
         self.seg_sums_train = self.coop_fwd and os.environ.get("PDG_SEG_SUMS_TRAIN", "0") == "1"
+        # the backward's input gradient of x (gP, gQ -> gx) in bf16x6 (pdg_gemm_sum2_coop) instead of the
+        # fp32-MFMA pdg_gemm_sum2_rw (PDG_GSUM2_COOP=0)
+        self.gsum2_coop = os.environ.get("PDG_GSUM2_COOP", "1") == "1"
         # edge encoder forward blocks (pdg_edge_enc_fwd: 104 VGPRs, 41 KB LDS per 8-wave block)
         self._enc_blocks = min(int(os.environ.get("PDG_ENC_BLOCKS_PER_CU", "2")) *
                                torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
@@ -477,8 +480,13 @@ class EPDEngine:
                                                    g_node, PN(t - 1))
             else:
                 a2n_prev, st_prev, accb, gl, pp = ctx.a2_ne, st[0], ACC_NE, P["node_encoder.4.weight"], P_NENC
-            self._t("gemm_sum2", lib.pdg_gemm_sum2_rw, N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]), _p(gx_part),
-                    _p(gx_t), _p(a2n_prev), st_prev, _p(accb), np_, _p(gl), _p(pp), 1, s)
+            if self.gsum2_coop:
+                self._t("gemm_sum2", lib.pdg_gemm_sum2_coop, N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]),
+                        _p(gx_part), _p(gx_t), _p(a2n_prev), st_prev, _p(accb), _p(gl), _p(pp), 1, self._nslabs_e, s)
+                self._nparts.value = self._nslabs_e
+            else:
+                self._t("gemm_sum2", lib.pdg_gemm_sum2_rw, N, _p(gP), _p(gQ), _p(T["WaT"]), _p(T["WbT"]),
+                        _p(gx_part), _p(gx_t), _p(a2n_prev), st_prev, _p(accb), np_, _p(gl), _p(pp), 1, s)
             n_node = self._nparts.value
             if not fused and E:
                 segs["W2"].append((gz2m, d["a1m"], E))

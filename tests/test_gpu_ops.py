@@ -780,3 +780,45 @@ def test_edge_enc_fwd_vs_fp64(env, E, nb):
     p = part.view(nb, 2).sum(0).cpu()
     assert abs(float(p[0]) - float(ref.sum())) <= 1e-6 * float(ref.abs().sum())
     assert abs(float(p[1]) - float((ref * ref).sum())) <= 1e-6 * float((ref * ref).sum())
+
+
+@pytest.mark.parametrize("N,nb,res", [(7, 37, True), (1031, 37, False), (40328, 256, True)])
+def test_gemm_sum2_coop_vs_fp64(env, N, nb, res):
+    """pdg_gemm_sum2_coop (bf16x6, register-stationary, cooperative layout) against an fp64
+    restatement of W0T in0 + W1T in1 + res, and its LayerNorm column partials / pairs against the
+    pdg_ln_colsum formulas on the fp64 output."""
+    import struct
+    lib, sh, _ = env
+    s = sh()
+    i0, i1 = rnd(N, L), rnd(N, L)
+    W0T, _ = lin(L, L)
+    W1T, _ = lin(L, L)
+    rr = rnd(N, L) if res else None
+    a2 = torch.relu(rnd(N, L))
+    g = rnd(L) * 0.3 + 1.0
+    r64 = a2.double()
+    mean, sd = float(r64.mean()), float(r64.std(unbiased=False))
+    den = float(torch.tensor(sd, dtype=torch.float32) + 1e-5)
+    st = torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, N * L)),
+                          dtype=torch.uint8).cuda()
+    ref = i0.double() @ W0T.double().T + i1.double() @ W1T.double().T
+    if res:
+        ref = ref + rr.double()
+    for cols in (False, True):
+        out = torch.full((N, L), float("nan"), device="cuda")
+        part = torch.zeros(nb * 256, dtype=torch.float64, device="cuda")
+        pairs = torch.zeros(nb * 2, dtype=torch.float64, device="cuda")
+        lib.pdg_gemm_sum2_coop(N, i0.data_ptr(), i1.data_ptr(), W0T.data_ptr(), W1T.data_ptr(),
+                               rr.data_ptr() if res else None, out.data_ptr(), a2.data_ptr() if cols else None,
+                               st.data_ptr() if cols else None, part.data_ptr() if cols else None,
+                               g.data_ptr() if cols else None, pairs.data_ptr() if cols else None, 0, nb, s)
+        assert rel(out, ref) < TOL
+        if cols:
+            got = part.view(nb, 256).sum(0).cpu()
+            gyv = out.double().cpu()   # the sums of the kernel's own output (the output is checked above)
+            xhat = ((a2.double() - mean) / den).cpu()
+            want = torch.cat([gyv.sum(0), (gyv * xhat).sum(0)])
+            assert rel(got, want) < 1e-6
+            sp = pairs.view(nb, 2).sum(0).cpu()
+            gd = g.double().cpu()
+            assert rel(sp, torch.stack([(gd * got[:L]).sum(), (gd * got[L:]).sum()])) < 1e-9
