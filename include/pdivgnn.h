@@ -246,6 +246,12 @@ int pdg_gemm_sum2_coop(int rows, const float* in0, const float* in1, const float
                        const float* res, float* out, const float* ln_a2, const pdg_ln_stat* ln_st,
                        double* partials, const float* ln_g, double* pairs, int accumulate, int nblocks,
                        void* stream);
+/* pdg_node_bwd in the block-cooperative layout (nblocks blocks of 512 threads): the same outputs with
+ * the three W^T products in bf16x6, weights stationary in registers. */
+int pdg_node_bwd_coop(int n_nodes, const float* gy, const float* a2n, const float* a1n, const pdg_ln_stat* st,
+                      const pdg_ln_bwd* lb, const float* ln_g, const float* Wn2T, const float* Wn1aT,
+                      const float* Wn1bT, float* gz2, float* gz1, float* gaggr, float* gx_part,
+                      const double* lb_pairs, int lb_npairs, int nblocks, void* stream);
 /* pdg_edge_fwd in the block-cooperative layout (pdg_ebw.hip): nblocks blocks of 512 threads, one
  * contiguous row range each, Wc (fp32) and W2 (bf16 terms) stationary in registers, whole-row HBM
  * access.  Same outputs (C bitwise, the W2 products to fp32 rounding); part_m / part_e get nblocks

@@ -1078,6 +1078,135 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void gemm_sum2_coop_kernel(
   }
 }
 
+// ============================================================================ node_net backward
+// pdg_node_bwd in the cooperative layout (models.py:240-243 backward; gy = d loss / d x_{t+1}):
+//   gz2 = LN_bwd(gy) [a2 > 0]                      (whole rows -> HBM and a bf16x6 image)
+//   gz1 = (W2^T gz2) [a1 > 0]                      (image -> product -> masked -> second image)
+//   gaggr = W1a^T gz1,  gx_part = W1b^T gz1 + gy   (one image, two weight slices)
+// with the three 128x128 weights stationary in registers as bf16 terms and the products in
+// bf16x6 (the edge backward's W^T products); outputs stored whole-row through fp32 row tiles.
+__device__ __forceinline__ void gemm_round_2w(f32x4 (&da)[2], f32x4 (&db)[2], const WSlice& wa, const WSlice& wb,
+                                              const unsigned char* img) {
+  const int l = lane_id(), n = l & 15, kg = l >> 4;
+#pragma unroll
+  for (int nb = 0; nb < 2; ++nb) da[nb] = db[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int off = x6_addr(16 * nb + n, 64 * ks + 16 * kg);
+      bf16x8 B[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(img + p * X6_TERM + off);
+      f32x4 t = da[nb], u = db[nb];
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa.a[ks][2], B[0], t, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb.a[ks][2], B[0], u, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa.a[ks][1], B[1], t, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb.a[ks][1], B[1], u, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa.a[ks][0], B[2], t, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb.a[ks][0], B[2], u, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa.a[ks][1], B[0], t, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb.a[ks][1], B[0], u, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa.a[ks][0], B[1], t, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb.a[ks][0], B[1], u, 0, 0, 0);
+      da[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa.a[ks][0], B[0], t, 0, 0, 0);
+      db[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb.a[ks][0], B[0], u, 0, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(EBW_THREADS, 1) void node_bwd_coop_kernel(
+    int N, const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ a1,
+    const pdg_ln_stat* __restrict__ stp, const pdg_ln_bwd* __restrict__ lbp, const double* __restrict__ lb_pairs,
+    int lb_npairs, const float* __restrict__ lg, const float* __restrict__ W2T, const float* __restrict__ W1aT,
+    const float* __restrict__ W1bT, float* __restrict__ gz2_out, float* __restrict__ gz1_out,
+    float* __restrict__ gaggr, float* __restrict__ gx_part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img2 = sm;                                    // gz2
+  unsigned char* img1 = sm + EBW_IMG;                          // gz1
+  unsigned char* msk = sm + 2 * EBW_IMG;                       // [a1 > 0]
+  float* t_z = reinterpret_cast<float*>(msk + EBW_MASK);       // gz1 rows
+  float* t_a = t_z + EFC_TILE;                                 // W1a^T gz1
+  float* t_b = t_a + EFC_TILE;                                 // W1b^T gz1
+  float* t_g = t_b + EFC_TILE;                                 // gy rows (the residual; no registers)
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(N, r0, r1);
+  WSlice w2, wa, wb;
+  load_wslice(w2, W2T, w);
+  load_wslice(wa, W1aT, w);
+  load_wslice(wb, W1bT, w);
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const pdg_ln_bwd lb = lnb_resolve(lbp, lb_pairs, lb_npairs, stp);
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+  f32x4 pg[2], pa2[2], pa1[2];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
+      pg[u] = *reinterpret_cast<const f32x4*>(gy + rc);
+      pa2[u] = *reinterpret_cast<const f32x4*>(a2 + rc);
+      pa1[u] = *reinterpret_cast<const f32x4*>(a1 + rc);
+    }
+  };
+  if (r0 < r1) issue(r0);
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const bool ok = base + r < r1;
+      const f32x4 z2 = ok ? ln_relu_bwd4(pg[u], pa2[u], st, lb, g4) : zero;
+      if (ok) stnt4(gz2_out + (size_t)(base + r) * L + 4 * cg, z2);
+      img_store4(img2, r, cg, z2);
+      *reinterpret_cast<unsigned*>(msk + r * MSK_STRIDE + 4 * cg) = relu_mask4(pa1[u]);
+      *reinterpret_cast<f32x4*>(t_g + r * OT_STRIDE + 4 * cg) = pg[u];
+    }
+    __syncthreads();   // gz2 image and the a1 mask complete
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    {
+      f32x4 d[1][2];
+      const unsigned char* imgs[1] = {img2};
+      gemm_round<1>(d, w2, imgs);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int r = 16 * nb + (l & 15);
+        const unsigned mm = *reinterpret_cast<const unsigned*>(msk + r * MSK_STRIDE + oc);
+        f32x4 z1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) z1[j] = (mm >> (8 * j)) & 1u ? d[0][nb][j] : 0.f;   // relu_mask_acc
+        img_store4(img1, r, 4 * w + (l >> 4), z1);
+        *reinterpret_cast<f32x4*>(t_z + r * OT_STRIDE + oc) = z1;
+      }
+    }
+    __syncthreads();   // gz1 image complete
+    {
+      f32x4 da[2], db[2];
+      gemm_round_2w(da, db, wa, wb, img1);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int r = 16 * nb + (l & 15);
+        *reinterpret_cast<f32x4*>(t_a + r * OT_STRIDE + oc) = da[nb];
+        *reinterpret_cast<f32x4*>(t_b + r * OT_STRIDE + oc) = db[nb];
+      }
+    }
+    __syncthreads();   // tiles complete; images and mask free for the next round
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const int row = base + r;
+      if (row < r1) {
+        const size_t o = (size_t)row * L + 4 * cg;
+        stnt4(gz1_out + o, *reinterpret_cast<const f32x4*>(t_z + r * OT_STRIDE + 4 * cg));
+        stg4(gaggr + o, *reinterpret_cast<const f32x4*>(t_a + r * OT_STRIDE + 4 * cg));
+        stg4(gx_part + o, *reinterpret_cast<const f32x4*>(t_b + r * OT_STRIDE + 4 * cg) +
+                              *reinterpret_cast<const f32x4*>(t_g + r * OT_STRIDE + 4 * cg));
+      }
+    }
+  }
+}
+
 // ============================================================================ C ABI
 extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
@@ -1320,5 +1449,24 @@ extern "C" int pdg_gemm_sum2_coop(int rows, const float* in0, const float* in1, 
                        nullptr, 0);
   }
   PDG_CHECK_LAUNCH("pdg_gemm_sum2_coop");
+  return PDG_OK;
+}
+
+extern "C" int pdg_node_bwd_coop(int n_nodes, const float* gy, const float* a2n, const float* a1n,
+                                 const pdg_ln_stat* st, const pdg_ln_bwd* lb, const float* ln_g, const float* Wn2T,
+                                 const float* Wn1aT, const float* Wn1bT, float* gz2, float* gz1, float* gaggr,
+                                 float* gx_part, const double* lb_pairs, int lb_npairs, int nblocks, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_node_bwd_coop: bad sizes");
+  PDG_CHECK_ARG(gy && a2n && a1n && st && (lb || lb_pairs) && ln_g && Wn2T && Wn1aT && Wn1bT && gz2 && gz1 && gaggr &&
+                    gx_part,
+                "pdg_node_bwd_coop: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2n) && PDG_ALIGNED(a1n) && PDG_ALIGNED(Wn2T) &&
+                    PDG_ALIGNED(Wn1aT) && PDG_ALIGNED(Wn1bT) && PDG_ALIGNED(gz2) && PDG_ALIGNED(gz1) &&
+                    PDG_ALIGNED(gaggr) && PDG_ALIGNED(gx_part) && PDG_ALIGNED(ln_g),
+                "pdg_node_bwd_coop: misaligned pointer");
+  const size_t shm = 2 * EBW_IMG + EBW_MASK + (size_t)4 * EFC_TILE * sizeof(float);
+  hipLaunchKernelGGL(node_bwd_coop_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, n_nodes, gy,
+                     a2n, a1n, st, lb, lb_pairs, lb_npairs, ln_g, Wn2T, Wn1aT, Wn1bT, gz2, gz1, gaggr, gx_part);
+  PDG_CHECK_LAUNCH("pdg_node_bwd_coop");
   return PDG_OK;
 }

@@ -135,6 +135,8 @@ class EPDEngine:
         # the backward's input gradient of x (gP, gQ -> gx) in bf16x6 (pdg_gemm_sum2_coop) instead of the
         # fp32-MFMA pdg_gemm_sum2_rw (PDG_GSUM2_COOP=0)
         self.gsum2_coop = os.environ.get("PDG_GSUM2_COOP", "1") == "1"
+        # node_net backward likewise (pdg_node_bwd_coop, three W^T products in bf16x6; PDG_NODE_BWD_COOP=0)
+        self.nbwd_coop = os.environ.get("PDG_NODE_BWD_COOP", "1") == "1"
         # edge encoder forward blocks (pdg_edge_enc_fwd: 104 VGPRs, 41 KB LDS per 8-wave block)
         self._enc_blocks = min(int(os.environ.get("PDG_ENC_BLOCKS_PER_CU", "2")) *
                                torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
@@ -432,9 +434,14 @@ class EPDEngine:
             ge_out = ge_bufs[t % 2]
             # node_net backward (n_t = LN_n(a2n_t), gy = gx_next; x_{t+1} = n_t + x_t)
             pn, nn = src(PN(t), n_node)
-            self._t("node_bwd", lib.pdg_node_bwd, N, _p(gx_next), _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]], None,
-                    _p(g_node), _p(T["Wn2T"]), _p(T["Wn1aT"]), _p(T["Wn1bT"]), _p(gz2n), _p(gz1n), _p(gaggr),
-                    _p(gx_part), pn, nn, s)
+            if self.nbwd_coop:
+                self._t("node_bwd", lib.pdg_node_bwd_coop, N, _p(gx_next), _p(d["a2n"]), _p(d["a1n"]),
+                        st[d["i_n"]], None, _p(g_node), _p(T["Wn2T"]), _p(T["Wn1aT"]), _p(T["Wn1bT"]), _p(gz2n),
+                        _p(gz1n), _p(gaggr), _p(gx_part), pn, nn, self._nslabs_e, s)
+            else:
+                self._t("node_bwd", lib.pdg_node_bwd, N, _p(gx_next), _p(d["a2n"]), _p(d["a1n"]), st[d["i_n"]],
+                        None, _p(g_node), _p(T["Wn2T"]), _p(T["Wn1aT"]), _p(T["Wn1bT"]), _p(gz2n), _p(gz1n),
+                        _p(gaggr), _p(gx_part), pn, nn, s)
             if E == 0:             # no edge: P and Q feed nothing (models.py:215-222 on empty tensors)
                 gP.zero_()
                 gQ.zero_()

@@ -822,3 +822,42 @@ def test_gemm_sum2_coop_vs_fp64(env, N, nb, res):
             sp = pairs.view(nb, 2).sum(0).cpu()
             gd = g.double().cpu()
             assert rel(sp, torch.stack([(gd * got[:L]).sum(), (gd * got[L:]).sum()])) < 1e-9
+
+
+@pytest.mark.parametrize("N,nb", [(7, 37), (1031, 37), (40328, 256)])
+def test_node_bwd_coop_vs_node_bwd(env, N, nb):
+    """pdg_node_bwd_coop (bf16x6 W^T products, cooperative layout) against pdg_node_bwd (fp32 MFMA):
+    gz2 bitwise (the same elementwise LayerNorm backward), gz1 / gaggr / gx_part to fp32 rounding
+    against an fp64 restatement, with the backward scalars from producer pairs."""
+    import struct
+    lib, sh, _ = env
+    s = sh()
+    gy = rnd(N, L)
+    a1 = torch.relu(rnd(N, L))
+    a2 = torch.relu(rnd(N, L))
+    g = rnd(L) * 0.3 + 1.0
+    W2T, _ = lin(L, L)
+    WaT, _ = lin(L, L)
+    WbT, _ = lin(L, L)
+    r64 = a2.double()
+    mean, sd = float(r64.mean()), float(r64.std(unbiased=False))
+    den = float(torch.tensor(sd, dtype=torch.float32) + 1e-5)
+    st = torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, N * L)),
+                          dtype=torch.uint8).cuda()
+    S1, S2 = 37.25, -12.5
+    pairs = torch.tensor([[S1 / 2, S2 / 4], [S1 / 4, S2 / 2], [S1 / 4, S2 / 4]], dtype=torch.float64).cuda()
+    o0 = [torch.empty(N, L, device="cuda") for _ in range(4)]
+    o1 = [torch.full((N, L), float("nan"), device="cuda") for _ in range(4)]
+    assert lib.pdg_node_bwd(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None, g.data_ptr(),
+                            W2T.data_ptr(), WaT.data_ptr(), WbT.data_ptr(), *[o.data_ptr() for o in o0],
+                            pairs.data_ptr(), 3, s) == 0
+    lib.pdg_node_bwd_coop(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None, g.data_ptr(),
+                          W2T.data_ptr(), WaT.data_ptr(), WbT.data_ptr(), *[o.data_ptr() for o in o1],
+                          pairs.data_ptr(), 3, nb, s)
+    assert torch.equal(o0[0], o1[0])                       # gz2
+    z2 = o0[0].double()
+    z1 = torch.where(a1 > 0, z2 @ W2T.double().T, torch.zeros_like(z2))
+    assert rel(o1[1], z1) < TOL and rel(o0[1], z1) < TOL
+    z1c = o1[1].double()                                    # the next products from the kernel's own gz1
+    assert rel(o1[2], z1c @ WaT.double().T) < TOL
+    assert rel(o1[3], z1c @ WbT.double().T + gy.double()) < TOL
