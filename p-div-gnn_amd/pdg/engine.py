@@ -106,9 +106,10 @@ class EPDEngine:
         self._nparts = ctypes.c_int(0)
         # one weight-gradient slab per block of pdg_wgrad_segments: three blocks per CU
         self._nslabs = lib.pdg_wgrad_slabs_per_cu() * torch.cuda.get_device_properties(self.device).multi_processor_count
-        # pdg_wgrad_pairs: two blocks per CU
-        self._nslabs_p = min(2 * torch.cuda.get_device_properties(self.device).multi_processor_count,
-                             lib.pdg_max_blocks())
+        # pdg_wgrad_pairs: one block per CU (2 per CU ran as two sequential block waves at 166 VGPRs:
+        # 9.07-9.12 vs 9.14-9.23 ms per config-2 step, same box)
+        self._nslabs_p = min(int(os.environ.get("PDG_PAIR_BLOCKS_PER_CU", "1")) *
+                             torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
         self._pair = torch.zeros(2, **f64)
         self.sync = None
         # edge backward with the W2 / Wc weight gradients fused (pdg_edge_bwd_w2 / pdg_edge_gout_wc);
