@@ -404,6 +404,10 @@ int pdg_div_bwd(int n_graphs, const int* ptr, int n_nodes, const int* at_rowptr,
 int pdg_transpose(int rows, int cols, int ld, const float* in, float* out, void* stream);
 /* n <= 16 transposes of 128 x 128 blocks in one launch: out_ptrs[i] (128 x 128, row-major) =
  * in_ptrs[i]^T, in_ptrs[i] with row stride lds[i]; host arrays. */
+/* Up to 3 pdg_wgrad_segments passes in one launch: job j has nseg[j] segments (its entries of g_ptrs /
+ * x_ptrs / rows follow job j-1's) and its own slab set slabs[j] (nslabs slabs each). */
+int pdg_wgrad_segments_batch(int njobs, const int* nseg, const float* const* g_ptrs, const float* const* x_ptrs,
+                             const int* rows, float* const* slabs, int nslabs, void* stream);
 /* Several pdg_wgrad_reduce calls in one launch (njobs <= 16): job i adds the sum of its nslabs[i]
  * slabs into grad_W[i] (row stride ld[i], column offset col0[i]) and, when grad_b[i] != NULL,
  * the bias sums into grad_b[i].  Slab sets must be distinct buffers. */

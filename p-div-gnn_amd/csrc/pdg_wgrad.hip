@@ -520,7 +520,7 @@ __device__ __forceinline__ void x6_load(const WgTable* tb, int nseg, long base, 
 // fixed order at the end, so each CU writes ONE slab (the slab traffic and the reduction that reads
 // it shrink NG-fold).  All groups run the same number of rounds (rows past a group's end are zero).
 template <int NG>
-__global__ __launch_bounds__(256 * NG, 3 / NG) void wgrad_x6_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {
+__device__ __forceinline__ void wgrad_x6_body(const WgradSegs& sg, long total, float* __restrict__ slabs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem6[];   // [table | NG x (G terms | X terms)]
   WgTable* tb = reinterpret_cast<WgTable*>(smem6);
   const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255;
@@ -644,6 +644,27 @@ __global__ __launch_bounds__(256 * NG, 3 / NG) void wgrad_x6_kernel(WgradSegs sg
   }
 }
 
+template <int NG>
+__global__ __launch_bounds__(256 * NG, 3 / NG) void wgrad_x6_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {
+  wgrad_x6_body<NG>(sg, total, slabs);
+}
+
+// Several weights' segment passes in one launch (blockIdx.y = job; each job its own slab set):
+// the node_net.2 / decoder / node encoder passes were three launches, the two single-segment ones
+// ~19 us each for 41 MB (fill / drain).
+constexpr int WGJ_MAX = 3;
+struct WgradJobs {
+  WgradSegs s[WGJ_MAX];
+  long total[WGJ_MAX];
+  float* slabs[WGJ_MAX];
+};
+
+template <int NG>
+__global__ __launch_bounds__(256 * NG, 3 / NG) void wgrad_x6_jobs_kernel(WgradJobs jobs) {
+  const int j = blockIdx.y;
+  wgrad_x6_body<NG>(jobs.s[j], jobs.total[j], jobs.slabs[j]);
+}
+
 extern "C" int pdg_wgrad_slabs_per_cu(void) { return 3 / PDG_WGRAD_GROUPS; }
 
 extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
@@ -678,6 +699,47 @@ extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const fl
 #endif
   PDG_CHECK_LAUNCH("pdg_wgrad_segments");
   return PDG_OK;
+}
+
+extern "C" int pdg_wgrad_segments_batch(int njobs, const int* nseg, const float* const* g_ptrs,
+                                        const float* const* x_ptrs, const int* rows, float* const* slabs, int nslabs,
+                                        void* stream) {
+  PDG_CHECK_ARG(njobs > 0 && njobs <= WGJ_MAX && nseg && g_ptrs && x_ptrs && rows && slabs,
+                "pdg_wgrad_segments_batch: 1..%d jobs", WGJ_MAX);
+  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS, "pdg_wgrad_segments_batch: bad nslabs");
+#if defined(PDG_WGRAD_F32) || PDG_WGRAD_GROUPS != 3
+  for (int j = 0, k = 0; j < njobs; k += nseg[j], ++j) {
+    const int rc = pdg_wgrad_segments(nseg[j], g_ptrs + k, x_ptrs + k, rows + k, slabs[j], nslabs, stream);
+    if (rc != PDG_OK) return rc;
+  }
+  return PDG_OK;
+#else
+  WgradJobs jobs;
+  int k = 0;
+  for (int j = 0; j < njobs; ++j) {
+    PDG_CHECK_ARG(nseg[j] > 0 && nseg[j] <= PDG_MAX_SEGS && slabs[j], "pdg_wgrad_segments_batch: bad job");
+    WgradSegs& sg = jobs.s[j];
+    long tot = 0;
+    for (int i = 0; i < nseg[j]; ++i, ++k) {
+      PDG_CHECK_ARG(rows[k] >= 0, "pdg_wgrad_segments_batch: negative rows");
+      PDG_CHECK_ARG(PDG_ALIGNED(g_ptrs[k]) && PDG_ALIGNED(x_ptrs[k]), "pdg_wgrad_segments_batch: misaligned pointer");
+      sg.G[i] = g_ptrs[k];
+      sg.X[i] = x_ptrs[k];
+      sg.start[i] = tot;
+      tot += rows[k];
+    }
+    sg.start[nseg[j]] = tot;
+    for (int i = nseg[j] + 1; i <= PDG_MAX_SEGS; ++i) sg.start[i] = tot;
+    sg.nseg = nseg[j];
+    PDG_CHECK_ARG(tot > 0, "pdg_wgrad_segments_batch: a job has no rows");
+    jobs.total[j] = tot;
+    jobs.slabs[j] = slabs[j];
+  }
+  hipLaunchKernelGGL(wgrad_x6_jobs_kernel<3>, dim3(nslabs, njobs), dim3(768), WG_TABLE_FLOATS * 4 + 18 * X6_TERM,
+                     (hipStream_t)stream, jobs);
+  PDG_CHECK_LAUNCH("pdg_wgrad_segments_batch");
+  return PDG_OK;
+#endif
 }
 
 // ---------------------------------------------------------------------------- pairs

@@ -590,8 +590,26 @@ class EPDEngine:
                 reduce_now_or_later(sp0, nsp, w0n, ld0, c00, b0n, later)
                 reduce_now_or_later(sp1, nsp, w1n, ld1, c01, b1n, later)
         red_k = [r for r in red if r[0] in segs]
+        # weights of at most 32 segments: up to three passes per launch (pdg_wgrad_segments_batch)
+        small = [r for r in red_k if 0 < len(segs[r[0]]) <= 32]
+        for c0 in range(0, len(small), 3):
+            grp = small[c0:c0 + 3]
+            segl = [segs[r[0]] for r in grp]
+            flat = [t for sl in segl for t in sl]
+            n = len(flat)
+            self._t("wgrad_batch", lib.pdg_wgrad_segments_batch, len(grp),
+                    (ctypes.c_int * len(grp))(*[len(sl) for sl in segl]),
+                    (ctypes.c_void_p * n)(*[g.data_ptr() for g, _, _ in flat]),
+                    (ctypes.c_void_p * n)(*[x.data_ptr() for _, x, _ in flat]),
+                    (ctypes.c_int * n)(*[r for _, _, r in flat]),
+                    (ctypes.c_void_p * len(grp))(*[_p(self._slabs[[r[0] for r in red].index(k[0])]) for k in grp]),
+                    ns, s)
+            for key, wname, ld, col0, bname in grp:
+                reduce_now_or_later(self._slabs[[r[0] for r in red].index(key)], ns, wname, ld, col0, bname, True)
         for key, wname, ld, col0, bname in red_k:
             sl = segs[key]
+            if len(sl) <= 32:
+                continue
             slabs_k = self._slabs[[r[0] for r in red].index(key)]
             for c0 in range(0, len(sl), 32):
                 chunk = sl[c0:c0 + 32]

@@ -56,6 +56,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_reduce": [P, I, P, I, I, P, P],
     "pdg_transpose128_batch": [I, P, P, P, P],
     "pdg_wgrad_reduce_batch": [I, P, P, P, P, P, P, P],
+    "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_edge_fwd_coop_seg": [I] + [P] * 20 + [I, P, P, P, I, P],
     "pdg_segsum_fixup": [I, P, P, P, P],

@@ -861,3 +861,32 @@ def test_node_bwd_coop_vs_node_bwd(env, N, nb):
     z1c = o1[1].double()                                    # the next products from the kernel's own gz1
     assert rel(o1[2], z1c @ WaT.double().T) < TOL
     assert rel(o1[3], z1c @ WbT.double().T + gy.double()) < TOL
+
+
+def test_wgrad_segments_batch_matches_single(env):
+    """pdg_wgrad_segments_batch (three weights' segment passes in one launch) == one
+    pdg_wgrad_segments per weight, slab for slab (the same kernel body per job)."""
+    lib, sh, _ = env
+    s = sh()
+    SL = L * L + L
+    ns = 37
+    jobs = [[(rnd(1000, L), rnd(1000, L), 1000), (rnd(77, L), rnd(77, L), 77)], [(rnd(4099, L), rnd(4099, L), 4099)],
+            [(rnd(31, L), rnd(31, L), 31), (rnd(500, L), rnd(500, L), 500), (rnd(64, L), rnd(64, L), 64)]]
+    single = []
+    for sl in jobs:
+        out = torch.full((ns, SL), float("nan"), device="cuda")
+        n = len(sl)
+        lib.pdg_wgrad_segments(n, (ctypes.c_void_p * n)(*[g.data_ptr() for g, _, _ in sl]),
+                               (ctypes.c_void_p * n)(*[x.data_ptr() for _, x, _ in sl]),
+                               (ctypes.c_int * n)(*[r for _, _, r in sl]), out.data_ptr(), ns, s)
+        single.append(out)
+    batch = [torch.full((ns, SL), float("nan"), device="cuda") for _ in jobs]
+    flat = [t for sl in jobs for t in sl]
+    n = len(flat)
+    lib.pdg_wgrad_segments_batch(len(jobs), (ctypes.c_int * 3)(*[len(sl) for sl in jobs]),
+                                 (ctypes.c_void_p * n)(*[g.data_ptr() for g, _, _ in flat]),
+                                 (ctypes.c_void_p * n)(*[x.data_ptr() for _, x, _ in flat]),
+                                 (ctypes.c_int * n)(*[r for _, _, r in flat]),
+                                 (ctypes.c_void_p * 3)(*[b.data_ptr() for b in batch]), ns, s)
+    for a, b in zip(single, batch):
+        torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
