@@ -201,6 +201,12 @@ int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a
                  const pdg_ln_stat* st, const pdg_ln_bwd* lb, const float* ln_g, const float* W2T,
                  float* gz2, float* gz1, const double* lb_pairs, int lb_npairs, void* stream);
 
+/* pdg_mlp2_bwd (gidx = NULL) in the block-cooperative layout: the W2^T product in bf16x6 with W2^T
+ * stationary in registers, whole-row access (the node encoder's backward). */
+int pdg_mlp2_bwd_coop(int rows, const float* gy, const float* a2, const float* a1, const pdg_ln_stat* st,
+                      const pdg_ln_bwd* lb, const float* ln_g, const float* W2T, float* gz2, float* gz1,
+                      const double* lb_pairs, int lb_npairs, int nblocks, void* stream);
+
 /* Fused node_net backward of one step (the work of pdg_mlp2_bwd + pdg_gemm_dual with
  * res0 = NULL, res1 = gy): gz2 = LN_bwd(gy) * [a2n > 0]; gz1 = (Wn2^T gz2) * [a1n > 0];
  * gaggr = Wn1a^T gz1; gx_part = Wn1b^T gz1 + gy.  Weights held in registers; bitwise the

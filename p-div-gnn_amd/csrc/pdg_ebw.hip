@@ -1207,6 +1207,76 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void node_bwd_coop_kernel(
   }
 }
 
+// ============================================================================ encoder backward
+// pdg_mlp2_bwd in the cooperative layout (the node encoder's backward, models.py:264-275 for the
+// 6-input encoder): gz2 = LN_bwd(gy) [a2 > 0] (whole rows -> HBM and a bf16x6 image),
+// gz1 = (W2^T gz2) [a1 > 0] (the product in bf16x6 with W2^T in registers) -> row tile -> HBM.
+// node_bwd_coop_kernel's first half.
+__global__ __launch_bounds__(EBW_THREADS, 1) void mlp2_bwd_coop_kernel(
+    int N, const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ a1,
+    const pdg_ln_stat* __restrict__ stp, const pdg_ln_bwd* __restrict__ lbp, const double* __restrict__ lb_pairs,
+    int lb_npairs, const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ gz2_out,
+    float* __restrict__ gz1_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img2 = sm;                                    // gz2
+  unsigned char* msk = sm + EBW_IMG;                           // [a1 > 0]
+  float* t_z = reinterpret_cast<float*>(msk + EBW_MASK);       // gz1 rows
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(N, r0, r1);
+  WSlice w2;
+  load_wslice(w2, W2T, w);
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const pdg_ln_bwd lb = lnb_resolve(lbp, lb_pairs, lb_npairs, stp);
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+  f32x4 pg[2], pa2[2], pa1[2];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
+      pg[u] = *reinterpret_cast<const f32x4*>(gy + rc);
+      pa2[u] = *reinterpret_cast<const f32x4*>(a2 + rc);
+      pa1[u] = *reinterpret_cast<const f32x4*>(a1 + rc);
+    }
+  };
+  if (r0 < r1) issue(r0);
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const bool ok = base + r < r1;
+      const f32x4 z2 = ok ? ln_relu_bwd4(pg[u], pa2[u], st, lb, g4) : zero;
+      if (ok) stnt4(gz2_out + (size_t)(base + r) * L + 4 * cg, z2);
+      img_store4(img2, r, cg, z2);
+      *reinterpret_cast<unsigned*>(msk + r * MSK_STRIDE + 4 * cg) = relu_mask4(pa1[u]);
+    }
+    __syncthreads();   // gz2 image and the a1 mask complete
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    f32x4 d[1][2];
+    const unsigned char* imgs[1] = {img2};
+    gemm_round<1>(d, w2, imgs);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = 16 * nb + (l & 15);
+      const unsigned mm = *reinterpret_cast<const unsigned*>(msk + r * MSK_STRIDE + oc);
+      f32x4 z1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) z1[j] = (mm >> (8 * j)) & 1u ? d[0][nb][j] : 0.f;   // relu_mask_acc
+      *reinterpret_cast<f32x4*>(t_z + r * OT_STRIDE + oc) = z1;
+    }
+    __syncthreads();   // the gz1 tile is complete; image and mask free for the next round
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      if (base + r < r1)
+        stnt4(gz1_out + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_z + r * OT_STRIDE + 4 * cg));
+    }
+  }
+}
+
 // ============================================================================ C ABI
 extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
@@ -1468,5 +1538,21 @@ extern "C" int pdg_node_bwd_coop(int n_nodes, const float* gy, const float* a2n,
   hipLaunchKernelGGL(node_bwd_coop_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, n_nodes, gy,
                      a2n, a1n, st, lb, lb_pairs, lb_npairs, ln_g, Wn2T, Wn1aT, Wn1bT, gz2, gz1, gaggr, gx_part);
   PDG_CHECK_LAUNCH("pdg_node_bwd_coop");
+  return PDG_OK;
+}
+
+extern "C" int pdg_mlp2_bwd_coop(int rows, const float* gy, const float* a2, const float* a1, const pdg_ln_stat* st,
+                                 const pdg_ln_bwd* lb, const float* ln_g, const float* W2T, float* gz2, float* gz1,
+                                 const double* lb_pairs, int lb_npairs, int nblocks, void* stream) {
+  PDG_CHECK_ARG(rows > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_mlp2_bwd_coop: bad sizes");
+  PDG_CHECK_ARG(gy && a2 && a1 && st && (lb || lb_pairs) && ln_g && W2T && gz2 && gz1,
+                "pdg_mlp2_bwd_coop: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2) && PDG_ALIGNED(a1) && PDG_ALIGNED(W2T) && PDG_ALIGNED(gz2) &&
+                    PDG_ALIGNED(gz1) && PDG_ALIGNED(ln_g),
+                "pdg_mlp2_bwd_coop: misaligned pointer");
+  const size_t shm = EBW_IMG + EBW_MASK + (size_t)EFC_TILE * sizeof(float);
+  hipLaunchKernelGGL(mlp2_bwd_coop_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, rows, gy, a2,
+                     a1, st, lb, lb_pairs, lb_npairs, ln_g, W2T, gz2, gz1);
+  PDG_CHECK_LAUNCH("pdg_mlp2_bwd_coop");
   return PDG_OK;
 }

@@ -511,8 +511,12 @@ class EPDEngine:
         # encoders
         gz2, gz1 = self._empty(N, L), self._empty(N, L)
         pn, nn = src(P_NENC, n_node)
-        lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], None,
-                         _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), pn, nn, s)
+        if self.nbwd_coop:   # the node encoder's backward, bf16x6 (pdg_mlp2_bwd_coop)
+            self._t("node_enc_bwd", lib.pdg_mlp2_bwd_coop, N, _p(gx_next), _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], None,
+                    _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), pn, nn, self._nslabs_e, s)
+        else:
+            lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], None,
+                             _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), pn, nn, s)
         segs["ne2"].append((gz2, ctx.a1_ne, N))
         lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
                              _p(G["node_encoder.0.bias"]), None, s)

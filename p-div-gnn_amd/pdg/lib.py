@@ -63,6 +63,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_node_bwd_coop": [I] + [P] * 14 + [I, I, P],
+    "pdg_mlp2_bwd_coop": [I] + [P] * 10 + [I, I, P],
     "pdg_segsum_finish": [I, P, P, P, P, P, P, P, P],
     "pdg_wgrad_slabs_per_cu": [],
     "pdg_wgrad_pairs": [I, P, P, P, P, I, P, P, I, P],

@@ -863,6 +863,35 @@ def test_node_bwd_coop_vs_node_bwd(env, N, nb):
     assert rel(o1[3], z1c @ WbT.double().T + gy.double()) < TOL
 
 
+@pytest.mark.parametrize("N,nb", [(1, 1), (33, 2), (5000, 7), (70000, 256)])
+def test_mlp2_bwd_coop_vs_mlp2_bwd(env, N, nb):
+    """pdg_mlp2_bwd_coop (the node encoder's backward, bf16x6 W2^T product) against pdg_mlp2_bwd:
+    gz2 bitwise (the same elementwise LayerNorm backward), gz1 to fp32 rounding against fp64."""
+    import struct
+    lib, sh, _ = env
+    s = sh()
+    gy = rnd(N, L)
+    a1 = torch.relu(rnd(N, L))
+    a2 = torch.relu(rnd(N, L))
+    g = rnd(L) * 0.3 + 1.0
+    W2T, _ = lin(L, L)
+    r64 = a2.double()
+    mean, sd = float(r64.mean()), float(r64.std(unbiased=False))
+    den = float(torch.tensor(sd, dtype=torch.float32) + 1e-5)
+    st = torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, N * L)),
+                          dtype=torch.uint8).cuda()
+    pairs = torch.tensor([[3.5, -1.25], [1.0, 0.5]], dtype=torch.float64).cuda()
+    o0 = [torch.empty(N, L, device="cuda") for _ in range(2)]
+    o1 = [torch.full((N, L), float("nan"), device="cuda") for _ in range(2)]
+    assert lib.pdg_mlp2_bwd(N, gy.data_ptr(), None, a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None, g.data_ptr(),
+                            W2T.data_ptr(), o0[0].data_ptr(), o0[1].data_ptr(), pairs.data_ptr(), 2, s) == 0
+    assert lib.pdg_mlp2_bwd_coop(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None, g.data_ptr(),
+                                 W2T.data_ptr(), o1[0].data_ptr(), o1[1].data_ptr(), pairs.data_ptr(), 2, nb, s) == 0
+    assert torch.equal(o0[0], o1[0])                       # gz2
+    z1 = torch.where(a1 > 0, o0[0].double() @ W2T.double().T, torch.zeros(N, L, dtype=torch.float64, device="cuda"))
+    assert rel(o1[1], z1) < TOL and rel(o0[1], z1) < TOL
+
+
 def test_wgrad_segments_batch_matches_single(env):
     """pdg_wgrad_segments_batch (three weights' segment passes in one launch) == one
     pdg_wgrad_segments per weight, slab for slab (the same kernel body per job)."""
