@@ -201,6 +201,13 @@ int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a
                  const pdg_ln_stat* st, const pdg_ln_bwd* lb, const float* ln_g, const float* W2T,
                  float* gz2, float* gz1, const double* lb_pairs, int lb_npairs, void* stream);
 
+/* pdg_decoder_bwd in the block-cooperative layout (the Wd1^T product in bf16x6). With partials != NULL
+ * it also forms pdg_ln_colsum's column partials / (S1, S2) pairs of gx for the LayerNorm with output
+ * statistics ln_st over ln_a2 (one partial per block: *nparts = nblocks), as pdg_gemm_sum2_coop. */
+int pdg_decoder_bwd_coop(int rows, const float* gy, const float* a1d, const float* Wd2, const float* Wd1T,
+                         float* gz1d, float* gx, const float* ln_a2, const pdg_ln_stat* ln_st, double* partials,
+                         const float* ln_g, double* pairs, int accumulate, int nblocks, void* stream);
+
 /* pdg_mlp2_bwd (gidx = NULL) in the block-cooperative layout: the W2^T product in bf16x6 with W2^T
  * stationary in registers, whole-row access (the node encoder's backward). */
 int pdg_mlp2_bwd_coop(int rows, const float* gy, const float* a2, const float* a1, const pdg_ln_stat* st,

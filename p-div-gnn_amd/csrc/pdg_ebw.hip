@@ -1277,6 +1277,117 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void mlp2_bwd_coop_kernel(
   }
 }
 
+// ============================================================================ decoder backward
+// pdg_decoder_bwd in the cooperative layout (models.py:316-321 backward; gy = d loss / d y, 3 wide):
+//   gz1d = (gy Wd2) [a1d > 0]   (the 3-wide product in fp32 FMAs, pdg_decoder_bwd's order)
+//   gx   = Wd1^T gz1d           (bf16x6, Wd1^T stationary in registers)
+// COLS: gx is the upstream gradient of the last node LayerNorm; its pdg_ln_colsum column sums /
+// (S1, S2) pairs are formed from the row tile (gemm_sum2_coop_kernel's reduction).
+template <bool COLS>
+__global__ __launch_bounds__(EBW_THREADS, 1) void decoder_bwd_coop_kernel(
+    int N, const float* __restrict__ gy, const float* __restrict__ a1d, const float* __restrict__ Wd2,
+    const float* __restrict__ Wd1T, float* __restrict__ gz1d, float* __restrict__ gx,
+    const float* __restrict__ ln_a2, const pdg_ln_stat* __restrict__ ln_st, double* __restrict__ part,
+    const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img = sm;
+  float* t_o = reinterpret_cast<float*>(sm + EBW_IMG);
+  LNStat stln;
+  if (COLS) stln = *reinterpret_cast<const LNStat*>(ln_st);
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(N, r0, r1);
+  WSlice ws;
+  load_wslice(ws, Wd1T, w);
+  f32x4 wd[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) wd[k] = *reinterpret_cast<const f32x4*>(Wd2 + k * L + 4 * cg);
+  double cs_g[4] = {0, 0, 0, 0}, cs_x[4] = {0, 0, 0, 0};
+  f32x4 pa1[2], pa2[2];
+  float pg[2][3];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int rc = clamp_row(base + rg + 16 * u, r1);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) pg[u][k] = gy[(size_t)rc * 3 + k];
+      pa1[u] = *reinterpret_cast<const f32x4*>(a1d + (size_t)rc * L + 4 * cg);
+      if (COLS) pa2[u] = *reinterpret_cast<const f32x4*>(ln_a2 + (size_t)rc * L + 4 * cg);
+    }
+  };
+  if (r0 < r1) issue(r0);
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 av[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const bool ok = base + r < r1;
+      f32x4 z;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float ga = fmaf(pg[u][2], wd[2][j], fmaf(pg[u][1], wd[1][j], pg[u][0] * wd[0][j]));
+        z[j] = ok && pa1[u][j] > 0.f ? ga : 0.f;
+      }
+      if (ok) stnt4(gz1d + (size_t)(base + r) * L + 4 * cg, z);
+      img_store4(img, r, cg, z);
+      av[u] = COLS ? pa2[u] : zero;
+    }
+    __syncthreads();   // image complete
+    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    f32x4 d[1][2];
+    const unsigned char* imgs[1] = {img};
+    gemm_round<1>(d, ws, imgs);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) *reinterpret_cast<f32x4*>(t_o + (16 * nb + (l & 15)) * OT_STRIDE + oc) = d[0][nb];
+    __syncthreads();   // tile complete; the image is free for the next round
+    f32x4 sg = zero, sx = zero;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      const int row = base + r;
+      if (row < r1) {
+        const f32x4 o = *reinterpret_cast<const f32x4*>(t_o + r * OT_STRIDE + 4 * cg);
+        stg4(gx + (size_t)row * L + 4 * cg, o);
+        if (COLS) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {   // the pdg_ln_colsum formulas
+            sg[j] += o[j];
+            sx[j] += o[j] * div_den(av[u][j] - stln.mean, stln.den, stln.rstd);
+          }
+        }
+      }
+    }
+    if (COLS) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cs_g[j] += (double)sg[j];
+        cs_x[j] += (double)sx[j];
+      }
+    }
+  }
+  if (COLS) {
+    double* red = reinterpret_cast<double*>(sm);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[rg * 2 * L + 4 * cg + j] = cs_g[j];
+      red[rg * 2 * L + L + 4 * cg + j] = cs_x[j];
+    }
+    __syncthreads();
+    double* row = red + EBW_THREADS / 32 * 2 * L;
+    for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) {
+      double v = 0;
+      for (int g = 0; g < EBW_THREADS / 32; ++g) v += red[g * 2 * L + i];
+      row[i] = v;
+    }
+    __syncthreads();
+    lnb_emit(row, ln_g, part, accumulate, pairs, row + 2 * L);
+  }
+}
+
 // ============================================================================ C ABI
 extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
@@ -1554,5 +1665,30 @@ extern "C" int pdg_mlp2_bwd_coop(int rows, const float* gy, const float* a2, con
   hipLaunchKernelGGL(mlp2_bwd_coop_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, rows, gy, a2,
                      a1, st, lb, lb_pairs, lb_npairs, ln_g, W2T, gz2, gz1);
   PDG_CHECK_LAUNCH("pdg_mlp2_bwd_coop");
+  return PDG_OK;
+}
+
+extern "C" int pdg_decoder_bwd_coop(int rows, const float* gy, const float* a1d, const float* Wd2, const float* Wd1T,
+                                    float* gz1d, float* gx, const float* ln_a2, const pdg_ln_stat* ln_st,
+                                    double* partials, const float* ln_g, double* pairs, int accumulate, int nblocks,
+                                    void* stream) {
+  PDG_CHECK_ARG(rows > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_decoder_bwd_coop: bad sizes");
+  PDG_CHECK_ARG(gy && a1d && Wd2 && Wd1T && gz1d && gx, "pdg_decoder_bwd_coop: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(a1d) && PDG_ALIGNED(Wd2) && PDG_ALIGNED(Wd1T) && PDG_ALIGNED(gz1d) && PDG_ALIGNED(gx),
+                "pdg_decoder_bwd_coop: misaligned pointer");
+  const size_t tile = (size_t)EFC_TILE * sizeof(float);
+  const size_t cols = ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
+  if (partials) {
+    PDG_CHECK_ARG(ln_a2 && ln_st && PDG_ALIGNED(ln_a2) && (!pairs || ln_g),
+                  "pdg_decoder_bwd_coop: column partials need an aligned ln_a2, ln_st (and ln_g for pairs)");
+    const size_t shm = EBW_IMG + tile > cols ? EBW_IMG + tile : cols;
+    hipLaunchKernelGGL(decoder_bwd_coop_kernel<true>, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream,
+                       rows, gy, a1d, Wd2, Wd1T, gz1d, gx, ln_a2, ln_st, partials, ln_g, pairs, accumulate);
+  } else {
+    hipLaunchKernelGGL(decoder_bwd_coop_kernel<false>, dim3(nblocks), dim3(EBW_THREADS), EBW_IMG + tile,
+                       (hipStream_t)stream, rows, gy, a1d, Wd2, Wd1T, gz1d, gx, nullptr, nullptr, nullptr, nullptr,
+                       nullptr, 0);
+  }
+  PDG_CHECK_LAUNCH("pdg_decoder_bwd_coop");
   return PDG_OK;
 }

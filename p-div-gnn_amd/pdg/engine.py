@@ -405,8 +405,15 @@ class EPDEngine:
             gy = gy * P["_std_local_stress"]
         # decoder
         gz1d, gx = self._empty(N, L), self._empty(N, L)
-        lib.pdg_decoder_bwd(N, _p(gy), _p(ctx.a1d), _p(P["node_decoder.2.weight"]), _p(T["Wd1T"]), _p(gz1d),
-                            _p(gx), s)
+        dl = ctx.per_step[S - 1]
+        if self.nbwd_coop:   # + the column sums of the last node LayerNorm (upstream gradient: gx)
+            self._t("decoder_bwd", lib.pdg_decoder_bwd_coop, N, _p(gy), _p(ctx.a1d), _p(P["node_decoder.2.weight"]),
+                    _p(T["Wd1T"]), _p(gz1d), _p(gx), _p(dl["a2n"]), st[dl["i_n"]], _p(ACC_N), _p(g_node),
+                    _p(PN(S - 1)), 1, self._nslabs_e, s)
+            self._nparts.value = self._nslabs_e
+        else:
+            lib.pdg_decoder_bwd(N, _p(gy), _p(ctx.a1d), _p(P["node_decoder.2.weight"]), _p(T["Wd1T"]), _p(gz1d),
+                                _p(gx), s)
         lib.pdg_wgrad_narrow(N, _p(ctx.a1d), _p(gy), 3, 1, _p(self._part_narrow), _p(G["node_decoder.2.weight"]),
                              None, _p(G["node_decoder.2.bias"]), s)
         segs["d1"].append((gz1d, ctx.x_S, N))
@@ -419,9 +426,9 @@ class EPDEngine:
         gx_next = gx
         # node LayerNorm of the last step (upstream gradient: the decoder's); for the earlier steps
         # the previous iteration's pdg_gemm_sum2_rw produces these partials
-        dl = ctx.per_step[S - 1]
-        lib.pdg_ln_colsum(N, _p(gx_next), None, _p(dl["a2n"]), st[dl["i_n"]], _p(ACC_N), np_, _p(g_node),
-                          _p(PN(S - 1)), 1, s)
+        if not self.nbwd_coop:
+            lib.pdg_ln_colsum(N, _p(gx_next), None, _p(dl["a2n"]), st[dl["i_n"]], _p(ACC_N), np_, _p(g_node),
+                              _p(PN(S - 1)), 1, s)
         n_node = self._nparts.value
         n_edge = 0
         for t in reversed(range(S)):

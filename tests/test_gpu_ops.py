@@ -892,6 +892,51 @@ def test_mlp2_bwd_coop_vs_mlp2_bwd(env, N, nb):
     assert rel(o1[1], z1) < TOL and rel(o0[1], z1) < TOL
 
 
+@pytest.mark.parametrize("N,nb", [(1, 1), (7, 37), (1031, 37), (40328, 256)])
+def test_decoder_bwd_coop_vs_decoder_bwd(env, N, nb):
+    """pdg_decoder_bwd_coop against pdg_decoder_bwd: gz1d bitwise (the same 3-wide FMA chain), gx to
+    fp32 rounding against fp64; its LayerNorm column partials / pairs against the pdg_ln_colsum
+    formulas on the kernel's own gx."""
+    import struct
+    lib, sh, _ = env
+    s = sh()
+    gy = rnd(N, 3)
+    a1 = torch.relu(rnd(N, L))
+    Wd2 = rnd(3, L)
+    W1T, _ = lin(L, L)
+    a2 = torch.relu(rnd(N, L))
+    g = rnd(L) * 0.3 + 1.0
+    r64 = a2.double()
+    mean, sd = float(r64.mean()), float(r64.std(unbiased=False))
+    den = float(torch.tensor(sd, dtype=torch.float32) + 1e-5)
+    st = torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, N * L)),
+                          dtype=torch.uint8).cuda()
+    z0, x0 = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
+    assert lib.pdg_decoder_bwd(N, gy.data_ptr(), a1.data_ptr(), Wd2.data_ptr(), W1T.data_ptr(), z0.data_ptr(),
+                               x0.data_ptr(), s) == 0
+    ref = z0.double() @ W1T.double().T
+    for cols in (False, True):
+        z1, x1 = (torch.full((N, L), float("nan"), device="cuda") for _ in range(2))
+        part = torch.zeros(nb * 256, dtype=torch.float64, device="cuda")
+        pairs = torch.zeros(nb * 2, dtype=torch.float64, device="cuda")
+        assert lib.pdg_decoder_bwd_coop(N, gy.data_ptr(), a1.data_ptr(), Wd2.data_ptr(), W1T.data_ptr(),
+                                        z1.data_ptr(), x1.data_ptr(), a2.data_ptr() if cols else None,
+                                        st.data_ptr() if cols else None, part.data_ptr() if cols else None,
+                                        g.data_ptr() if cols else None, pairs.data_ptr() if cols else None, 0, nb,
+                                        s) == 0
+        assert torch.equal(z0, z1)
+        assert rel(x1, ref) < TOL and rel(x0, ref) < TOL
+        if cols:
+            got = part.view(nb, 256).sum(0).cpu()
+            gyv = x1.double().cpu()
+            xhat = ((a2.double() - mean) / den).cpu()
+            want = torch.cat([gyv.sum(0), (gyv * xhat).sum(0)])
+            assert rel(got, want) < 1e-6
+            sp = pairs.view(nb, 2).sum(0).cpu()
+            gd = g.double().cpu()
+            assert rel(sp, torch.stack([(gd * got[:L]).sum(), (gd * got[L:]).sum()])) < 1e-9
+
+
 def test_wgrad_segments_batch_matches_single(env):
     """pdg_wgrad_segments_batch (three weights' segment passes in one launch) == one
     pdg_wgrad_segments per weight, slab for slab (the same kernel body per job)."""
