@@ -832,19 +832,24 @@ __global__ __launch_bounds__(512, 1) void wgrad_x6_pair_kernel(WgradSegs3 sg, lo
     }
     seg = lo;
   }
-  // two rounds of rows in flight (register sets v[0], v[1] in turn): round k's MFMAs run while the
-  // loads of rounds k+1 and k+2 are outstanding
-  f32x4 v[2][3][2];
-  auto stage = [&](f32x4 (&u)[3][2]) {
+  f32x4 v[3][2];
+  auto stage = [&]() {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      bs0 += u[0][i];
-      if (SHX) bs1 += u[1][i];
+      bs0 += v[0][i];
+      if (SHX) bs1 += v[1][i];
     }
 #pragma unroll
-    for (int a = 0; a < 3; ++a) x6_store2(img + a * 3 * X6_TERM, cg, rg, u[a]);
+    for (int a = 0; a < 3; ++a) x6_store2(img + a * 3 * X6_TERM, cg, rg, v[a]);
   };
-  auto products = [&]() {
+  if (r0 < r1) {
+    x6_load3(tb, nseg, r0 + 2 * rg, r1, seg, cg, v);
+    stage();
+  }
+  __syncthreads();
+  for (long base = r0; base < r1; base += X6_ROWS) {
+    const bool more = base + X6_ROWS < r1;
+    if (more) x6_load3(tb, nseg, base + X6_ROWS + 2 * rg, r1, seg, cg, v);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 A[2][3], B[2][3];
@@ -871,28 +876,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_x6_pair_kernel(WgradSegs3 sg, lo
           t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][1], t, 0, 0, 0);
           acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][0], t, 0, 0, 0);
         }
-      __builtin_amdgcn_sched_barrier(0);   // one k-slice's operands live at a time
     }
-  };
-  if (r0 < r1) {
-    x6_load3(tb, nseg, r0 + 2 * rg, r1, seg, cg, v[0]);
-    if (r0 + X6_ROWS < r1) x6_load3(tb, nseg, r0 + X6_ROWS + 2 * rg, r1, seg, cg, v[1]);
-    stage(v[0]);
-  }
-  __syncthreads();
-  for (long base = r0; base < r1; base += 2 * X6_ROWS) {
-    // images: rows base; v[1]: rows base + 32 (in flight)
-    if (base + 2 * X6_ROWS < r1) x6_load3(tb, nseg, base + 2 * X6_ROWS + 2 * rg, r1, seg, cg, v[0]);
-    products();
     __syncthreads();
-    if (base + X6_ROWS >= r1) break;
-    stage(v[1]);
-    __syncthreads();
-    // images: rows base + 32; v[0]: rows base + 64 (in flight)
-    if (base + 3 * X6_ROWS < r1) x6_load3(tb, nseg, base + 3 * X6_ROWS + 2 * rg, r1, seg, cg, v[1]);
-    products();
-    __syncthreads();
-    if (base + 2 * X6_ROWS < r1) stage(v[0]);
+    if (more) stage();
     __syncthreads();
   }
   float* slab = (pw ? slabs1 : slabs0) + (size_t)blockIdx.x * SLAB;
