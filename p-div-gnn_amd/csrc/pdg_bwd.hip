@@ -176,29 +176,14 @@ __global__ __launch_bounds__(256) void ln_colsum_nodes_kernel(int N, const float
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const int nhw = blockDim.x >> 5;
   double sg[4] = {0, 0, 0, 0}, sx[4] = {0, 0, 0, 0};
-  // CN rows per half-wave in flight (all loads of a group issued before any use)
-  constexpr int CN = 4;
-  const int stride = gridDim.x * nhw;
-  for (int v0 = blockIdx.x * nhw + hw; v0 < N; v0 += CN * stride) {
-    f32x4 g[CN], x[CN];
-    int p0[CN], p1[CN];
+  for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
+    const float deg = (float)(rowptr[v + 1] - rowptr[v]);
+    const f32x4 g = reinterpret_cast<const f32x4*>(gaggr + (size_t)v * L)[j];
+    const f32x4 x = reinterpret_cast<const f32x4*>(xs + (size_t)v * L)[j];
 #pragma unroll
-    for (int k = 0; k < CN; ++k) {
-      const int v = min(v0 + k * stride, N - 1);
-      p0[k] = rowptr[v];
-      p1[k] = rowptr[v + 1];
-      g[k] = reinterpret_cast<const f32x4*>(gaggr + (size_t)v * L)[j];
-      x[k] = reinterpret_cast<const f32x4*>(xs + (size_t)v * L)[j];
-    }
-#pragma unroll
-    for (int k = 0; k < CN; ++k) {
-      if (v0 + k * stride >= N) break;
-      const float deg = (float)(p1[k] - p0[k]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        sg[c] += (double)deg * (double)g[k][c];
-        sx[c] += (double)g[k][c] * (double)x[k][c];
-      }
+    for (int c = 0; c < 4; ++c) {
+      sg[c] += (double)deg * (double)g[c];
+      sx[c] += (double)g[c] * (double)x[c];
     }
   }
 #pragma unroll
