@@ -336,7 +336,9 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
     fused = eng.fused_edge_wgrad
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
-    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, getattr(eng, "seg_sums", False))
+    # the fused message sums run in inference only unless PDG_SEG_SUMS_TRAIN=1 (engine.py:253)
+    seg = getattr(eng, "seg_sums", False) if infer else getattr(eng, "seg_sums_train", False)
+    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg)
     pmc = load_pmc(fused) if with_pmc else {}
     step_s = el * ev_steps / args.steps
     dominant = max([k for k in ("edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])
