@@ -448,7 +448,9 @@ def main():
         torch.cuda.set_device(dev_index)
         device = torch.device("cuda", dev_index)
     pg = None
-    if world > 1:
+    # PDG_FORCE_PG=1: a process group (and the Trainer's all-reduce) even at one rank, to rehearse the
+    # RCCL data path on a one-GPU box
+    if world > 1 or os.environ.get("PDG_FORCE_PG") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)

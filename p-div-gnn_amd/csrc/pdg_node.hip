@@ -180,6 +180,122 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
   }
 }
 
+// node_net_kernel with TWO tiles per iteration (the block's tiles i = 2p and 2p + 1 of the same
+// tile sequence, one after the other with node_net_kernel's MFMA order, so a1 / a2 and the fp64
+// partials - tile 2p's rows before 2p + 1's - are bitwise node_net_kernel's): half the barriers
+// per node and twice the bytes per loader round.  Loader and compute waves run separate loops
+// with the same barrier sequence (one per pair: the stores into buffer (p + 2) % 3 after it are
+// read after the next pair's barrier, and layer 1 of pair p + 1 writes the layer-1 tile pair that
+// layer 2 of pair p - 1 read before this one), so the loaders' two tiles of registers are never
+// live beside the compute waves' 96 weight VGPRs (one shared loop spilled at the 168-VGPR budget
+// of 12 waves).  Three pair buffers (prefetch distance 2 pairs) and a double-buffered pair of
+// layer-1 tiles: 136 KB of LDS, one block per CU.
+__global__ __launch_bounds__(NU_THREADS, 1) void node_net_pair_kernel(
+    int N, const float* __restrict__ aggr, const float* __restrict__ x, const float* __restrict__ W1,
+    const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
+    float* __restrict__ a1_out, float* __restrict__ a2_out, double* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float xin[6 * XBUF];
+  __shared__ __attribute__((aligned(16))) float a1t[4 * TILE * AS];
+  const int w = wave_id(), l = lane_id();
+  const int ntiles = tiles_of(N);
+  double s1 = 0, s2 = 0;
+  if (w >= NU_COMPUTE) {
+    // ---- loader waves: pair p + 2 fetched before the barrier of pair p, stored after it into
+    // buffer (p + 2) % 3, last read by layer 1 of pair p - 1 (before the barrier of pair p - 1)
+    const int lt = threadIdx.x - 64 * NU_COMPUTE;
+    TileRegs tr[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (nu_tile(2 * k) < ntiles) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) fetch_tile(tr[h], nu_tile(2 * k + h), N, lt, aggr, x);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) store_tile(xin + (2 * k + h) * XBUF, lt, tr[h]);
+      }
+    __syncthreads();
+    for (int p = 0; nu_tile(2 * p) < ntiles; ++p) {
+      const bool ahead = nu_tile(2 * (p + 2)) < ntiles;
+      if (ahead) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) fetch_tile(tr[h], nu_tile(2 * (p + 2) + h), N, lt, aggr, x);
+      }
+      __syncthreads();
+      if (ahead) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) store_tile(xin + (2 * ((p + 2) % 3) + h) * XBUF, lt, tr[h]);
+      }
+    }
+  } else {
+    const int r = l & 15, q = l >> 4;
+    f32x4 w1f[16], w2f[8];
+    const float* w1r = W1 + (size_t)(16 * w + r) * (2 * L) + 4 * q;
+    const float* w2r = W2 + (size_t)(16 * w + r) * L + 4 * q;
+#pragma unroll
+    for (int T = 0; T < 16; ++T) w1f[T] = *reinterpret_cast<const f32x4*>(w1r + 16 * T);
+#pragma unroll
+    for (int T = 0; T < 8; ++T) w2f[T] = *reinterpret_cast<const f32x4*>(w2r + 16 * T);
+    const f32x4 bias1 = *reinterpret_cast<const f32x4*>(b1 + 16 * w + 4 * q);
+    const f32x4 bias2 = *reinterpret_cast<const f32x4*>(b2 + 16 * w + 4 * q);
+    __syncthreads();
+    for (int p = 0; nu_tile(2 * p) < ntiles; ++p) {
+      const float* xb = xin + 2 * (p % 3) * XBUF;
+      float* at = a1t + 2 * (p & 1) * TILE * AS;
+      // layer 1: a1 = relu(W1 [aggr | x] + b1), K = 256, tile 2p then tile 2p + 1
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int T = 0; T < 16; ++T) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(xb + h * XBUF + r * XS + 4 * q + 16 * T);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w1f[T][jj], bv[jj], acc, 0, 0, 0);
+        }
+        f32x4 a1;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a1[c] = fmaxf(acc[c] + bias1[c], 0.f);
+        *reinterpret_cast<f32x4*>(at + h * TILE * AS + r * AS + 16 * w + 4 * q) = a1;
+        const int row = nu_tile(2 * p + h) * TILE + r;
+        if (row < N && a1_out) stg4(a1_out + (size_t)row * L + 16 * w + 4 * q, a1);
+      }
+      __syncthreads();   // the layer-1 tiles are complete
+      // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int T = 0; T < 8; ++T) {
+          const f32x4 bv = *reinterpret_cast<const f32x4*>(at + h * TILE * AS + r * AS + 4 * q + 16 * T);
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[T][jj], bv[jj], acc, 0, 0, 0);
+        }
+        f32x4 a2;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a2[c] = fmaxf(acc[c] + bias2[c], 0.f);
+        const int row = nu_tile(2 * p + h) * TILE + r;
+        if (row < N) {
+          stg4(a2_out + (size_t)row * L + 16 * w + 4 * q, a2);
+          const float p1 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+          const float p2 = (a2[0] * a2[0] + a2[1] * a2[1]) + (a2[2] * a2[2] + a2[3] * a2[3]);
+          s1 += (double)p1;
+          s2 += (double)p2;
+        }
+      }
+    }
+  }
+  __shared__ double red[2 * (NU_THREADS / 64)];
+  block_sum2(s1, s2, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s1;
+    part[2 * blockIdx.x + 1] = s2;
+  }
+}
+
+// paired tiles (node_net_pair_kernel) by default: 46.6 -> 45.5-46.4 us per config-2 call in a same-box
+// A/B; the same pairing of node_pq_rw measured no faster and is not kept
+#ifndef PDG_NODE_NET_PAIR
+#define PDG_NODE_NET_PAIR 1
+#endif
+
 extern "C" int pdg_node_net(int n_nodes, const float* aggr, const float* x, const float* Wn1, const float* bn1,
                             const float* Wn2, const float* bn2, float* a1n, float* a2n, double* partials,
                             int* nparts, void* stream) {
@@ -191,8 +307,8 @@ extern "C" int pdg_node_net(int n_nodes, const float* aggr, const float* x, cons
   const int tiles = tiles_of(n_nodes);
   const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
   const int grid = tiles < cap ? tiles : cap;
-  hipLaunchKernelGGL(node_net_kernel, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes, aggr, x, Wn1,
-                     bn1, Wn2, bn2, a1n, a2n, partials);
+  hipLaunchKernelGGL(PDG_NODE_NET_PAIR ? node_net_pair_kernel : node_net_kernel, dim3(grid), dim3(NU_THREADS), 0,
+                     (hipStream_t)stream, n_nodes, aggr, x, Wn1, bn1, Wn2, bn2, a1n, a2n, partials);
   PDG_CHECK_LAUNCH("pdg_node_net");
   if (nparts) *nparts = grid;
   return PDG_OK;

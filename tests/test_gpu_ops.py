@@ -321,7 +321,7 @@ def test_wgrad_segments_dynamic_range(env):
     assert worst < 1e-6
 
 
-@pytest.mark.parametrize("N", [5, 1031, 4099, 40328])
+@pytest.mark.parametrize("N", [5, 1031, 4099, 8209, 40328, 100489])
 def test_node_net_matches_separate_kernels(env, N):
     """Fused node_net (register-stationary weights) == pdg_node_mlp1 + pdg_mlp2_fwd bitwise;
     LayerNorm partial totals equal to fp32 rounding; against float64 torch."""
@@ -403,7 +403,8 @@ def test_node_bwd_matches_separate_kernels(env, N):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("N,res", [(7, True), (1031, False), (40328, True)])
+@pytest.mark.parametrize("N,res", [(7, True), (1031, False), (4099, True), (8209, False), (40328, True),
+                                   (100489, False)])
 def test_register_weight_kernels_match_lds_kernels(env, N, res):
     """pdg_node_pq_rw / pdg_gemm_sum2_rw (weights in registers) == pdg_node_pq / pdg_gemm_sum2
     (weights in LDS) bitwise."""
