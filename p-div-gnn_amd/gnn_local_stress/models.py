@@ -182,6 +182,29 @@ class EncodeProcessDecode(StressFieldBaseModel):
         return self._engines[key][1]
 
     def stats_tensor(self, device) -> torch.Tensor:
+        """The 8 dataset statistics as one fp32 tensor on `device` (pdg_format_inputs' operand).
+
+        Cached while the statistics are unchanged (the same tensor objects at the same version
+        counter, or equal Python scalars): rebuilding it took 8 host-to-device copies per training
+        step.  Callers only read it."""
+        key = [("d", str(device))]
+        for k in _STAT_ORDER:
+            v = getattr(self, k)
+            key.append(("t", v, v._version) if isinstance(v, torch.Tensor) else ("s", float(v)))
+
+        def same(a, b):
+            if a[0] != b[0]:
+                return False
+            return (a[1] is b[1] and a[2] == b[2]) if a[0] == "t" else a[1] == b[1]
+
+        c = self.__dict__.get("_stats_cache")
+        if c is not None and all(same(a, b) for a, b in zip(c[0], key)):
+            return c[1]
+        out = self._build_stats_tensor(device)
+        self.__dict__["_stats_cache"] = (key, out)
+        return out
+
+    def _build_stats_tensor(self, device) -> torch.Tensor:
         vals = []
         for k in _STAT_ORDER:
             v = torch.as_tensor(getattr(self, k), dtype=torch.float32)

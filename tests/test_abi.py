@@ -93,6 +93,26 @@ def test_vector_statistics_are_refused():
     assert m.stats_tensor("cpu")[0] == 1.5
 
 
+def test_stats_tensor_cache_follows_the_statistics():
+    """stats_tensor is built once per set of statistics (no per-step host-to-device copies) and
+    rebuilt when one is reassigned or modified in place."""
+    import torch
+    from gnn_local_stress.models import EncodeProcessDecode
+    m = EncodeProcessDecode(1, 2, latent_size=128, input_nodes_features_size=6, output_nodes_features_size=3,
+                            mean_pos=torch.tensor(1.0), std_pos=2.0)
+    t0 = m.stats_tensor("cpu")
+    assert m.stats_tensor("cpu") is t0
+    m.mean_pos.add_(1.0)                      # in place: version counter moves
+    t1 = m.stats_tensor("cpu")
+    assert t1 is not t0 and float(t1[0]) == 2.0
+    m.std_pos = 4.0                           # reassigned Python scalar
+    t2 = m.stats_tensor("cpu")
+    assert t2 is not t1 and float(t2[1]) == 4.0 and m.stats_tensor("cpu") is t2
+    m.std_pos = torch.tensor(4.0)             # same value, now a tensor: rebuilt, equal contents
+    t3 = m.stats_tensor("cpu")
+    assert t3 is not t2 and torch.equal(t3, t2)
+
+
 def test_call_sites_match_signatures():
     """Every direct call of a C-ABI entry point in the host code and the tests passes as many
     arguments as the header declares (calls through lib.pdg_x(...) and engine._t(name, lib.pdg_x, ...)
