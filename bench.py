@@ -52,7 +52,7 @@ import torch.distributed as dist  # noqa: E402
 PMC_FILE = ROOT / "profiles" / "r02_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
 PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
              "edge_bwd": "void edge_bwd_kernel<true>",
-             "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": "node_net_kernel",
+             "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_pair_kernel", "node_net_kernel"),
              "pq_scatter_bwd": "pq_scatter_bwd_kernel",
              "wgrad_W2": "wgrad_x6_kernel", "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
              "edge_gout": "void edge_gout_wc_kernel<true>"}
