@@ -215,12 +215,9 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   int r0, r1;
   block_rows(E, r0, r1);
   WSlice ws;
-  load_wslice(ws, W2T, w);
   const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
   const LNStat ste = *reinterpret_cast<const LNStat*>(EU ? ste_p : stm_p);
-  const pdg_ln_bwd lbm = lnb_resolve(lbm_p, pm, npm, stm_p);
-  const pdg_ln_bwd lbe = EU ? lnb_resolve(lbe_p, pe, npe, ste_p) : lbm;
   f32x16 acc[2];
 #pragma unroll
   for (int b = 0; b < 2; ++b)
@@ -253,6 +250,10 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     }
     issue(r0, d0);
   }
+  // the weights and the LayerNorm scalars after the first round's row loads: the round trips overlap
+  load_wslice(ws, W2T, w);
+  const pdg_ln_bwd lbm = lnb_resolve(lbm_p, pm, npm, stm_p);
+  const pdg_ln_bwd lbe = EU ? lnb_resolve(lbe_p, pe, npe, ste_p) : lbm;
   for (int base = r0; base < r1; base += X6_ROWS) {
     // ---- stage: gz2 (LN + relu backward), a1 and its relu mask into the images
 #pragma unroll
@@ -341,7 +342,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
   int r0, r1;
   block_rows(E, r0, r1);
   WSlice ws;
-  load_wslice(ws, WcT, w);
   f32x16 acc[2];
 #pragma unroll
   for (int b = 0; b < 2; ++b)
@@ -363,6 +363,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
     }
   };
   if (r0 < r1) issue(r0);
+  load_wslice(ws, WcT, w);   // after the first round's row loads: both round trips in flight together
   for (int base = r0; base < r1; base += X6_ROWS) {
     f32x4 res[2], a2[2];
 #pragma unroll
@@ -998,8 +999,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void gemm_sum2_coop_kernel(
   int r0, r1;
   block_rows(N, r0, r1);
   WSlice ws0, ws1;
-  load_wslice(ws0, W0T, w);
-  load_wslice(ws1, W1T, w);
   double cs_g[4] = {0, 0, 0, 0}, cs_x[4] = {0, 0, 0, 0};
   f32x4 p0[2], p1[2], pres[2], pa2[2];
   auto issue = [&](int base) {
@@ -1013,6 +1012,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void gemm_sum2_coop_kernel(
     }
   };
   if (r0 < r1) issue(r0);
+  load_wslice(ws0, W0T, w);   // after the first round's row loads: both round trips in flight together
+  load_wslice(ws1, W1T, w);
   for (int base = r0; base < r1; base += X6_ROWS) {
     const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 rv[2], av[2];
