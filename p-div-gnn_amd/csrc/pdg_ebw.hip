@@ -636,13 +636,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   // the weights as A operands, rows = output features 16w .. 16w + 15 (W is out x in, row-major):
   // Wc = W1[:, 256:384] (row stride 384), W2
   f32x4 wcf[8];   // Wc rows 16w + (l & 15), inputs 16T + 4(l >> 4) .. +3 (node_pq_rw's A fragments)
-  {
-    const float* pc = W1 + (size_t)(16 * w + (l & 15)) * (3 * L) + 2 * L + 4 * (l >> 4);
-#pragma unroll
-    for (int T = 0; T < 8; ++T) wcf[T] = *reinterpret_cast<const f32x4*>(pc + 16 * T);
-  }
-  WSlice ws2;
-  load_wslice(ws2, W2, w);
+  WSlice ws2;     // both loaded after the first round's row loads (the round trips overlap)
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg), bb4 = *reinterpret_cast<const f32x4*>(lb + 4 * cg);
   const f32x4 b1o = *reinterpret_cast<const f32x4*>(b1 + oc), b2o = *reinterpret_cast<const f32x4*>(b2 + oc);
@@ -734,10 +728,14 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     }
     prev_last = sdst[nr - 1];
   };
-  if (r0 < r1) {
-    issue(r0);
-    stage(r0);
+  if (r0 < r1) issue(r0);
+  {
+    const float* pc = W1 + (size_t)(16 * w + (l & 15)) * (3 * L) + 2 * L + 4 * (l >> 4);
+#pragma unroll
+    for (int T = 0; T < 8; ++T) wcf[T] = *reinterpret_cast<const f32x4*>(pc + 16 * T);
   }
+  load_wslice(ws2, W2, w);
+  if (r0 < r1) stage(r0);
   for (int base = r0; base < r1; base += X6_ROWS) {
     __syncthreads();   // e tile complete
     int dc[2] = {dq[0], dq[1]}, sc[2] = {sq[0], sq[1]};
