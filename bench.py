@@ -49,7 +49,9 @@ sys.path[:0] = [str(ROOT), str(ROOT / "p-div-gnn_amd")]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PMC_FILE = ROOT / "profiles" / "r02_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
+PMC_FILE = ROOT / "profiles" / "r03_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
+TREE_GLOBS = ("p-div-gnn_amd/csrc/*.hip", "p-div-gnn_amd/csrc/*.hpp", "include/*.h", "p-div-gnn_amd/pdg/*.py",
+              "p-div-gnn_amd/gnn_local_stress/*.py", "bench.py")
 PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
              "edge_bwd": "void edge_bwd_kernel<true>",
              "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_pair_kernel", "node_net_kernel"),
@@ -105,6 +107,19 @@ def dataset_stats(b):
             "std_edge_weight": b.edge_attr.std()}
 
 
+def tree_hash() -> str:
+    """sha256 (16 hex) over the sources of the timed path (kernels, C ABI, engine, bench): the same
+    value in the bench line and in the profiles/ files measured from the same tree, on any box (the
+    GPU box's snapshot has no .git)."""
+    import hashlib
+    h = hashlib.sha256()
+    for pat in TREE_GLOBS:
+        for f in sorted(ROOT.glob(pat)):
+            h.update(f.relative_to(ROOT).as_posix().encode())
+            h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
 # ---------------------------------------------------------------------------------- CPU baseline
 def _cpu_model_name() -> str:
     try:
@@ -114,6 +129,27 @@ def _cpu_model_name() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+def cpu_threads() -> tuple[int, dict]:
+    """Threads for the CPU baseline: the CPUs this process may really use.  The affinity mask of a
+    GPU box lists every core of the host (256), but the container's CPU quota (cgroup cpu.max) and
+    the OMP_NUM_THREADS the box exports (16) grant far fewer; torch at 256 threads on 16 CPUs would
+    time oversubscription.  Returns (threads, the three figures and which one bounds)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    cands = {"sched_getaffinity": aff, "cgroup_cpu_max": quota, "OMP_NUM_THREADS": omp}
+    n = min(v for v in cands.values() if v)
+    bound = [k for k, v in cands.items() if v == n][0]
+    return n, {**cands, "bound_by": bound}
 
 
 def _oracle_step_fn(cfg, samples):
@@ -153,33 +189,41 @@ def _median_rate(step, nodes, reps):
     return nodes / statistics.median(ts), ts
 
 
-def cpu_baseline(cfg, samples, reps: int = 3, one_thread_graphs: int = 1, one_thread_reps: int = 3):
-    """The reference algorithm on this host's CPU cores: all the threads torch uses
-    here (OMP_NUM_THREADS / the CPU share of the box) on the config's own batch, median of `reps`
-    after one warm-up; plus one thread on `one_thread_graphs` graph(s) of it.  (The config-2 batch
-    takes ~16 s per step on 16 threads of the GPU box's EPYC, so the sample stays at 3 + 1 steps
-    to keep the default bench within a few minutes.)"""
-    threads = torch.get_num_threads()
+def cpu_baseline(cfg, samples, full_graphs: int, reps: int = 5, one_thread: bool = True):
+    """The reference algorithm on this host's CPU cores: median of
+    `reps` steps after one warm-up, at the threads this process may use (cpu_threads) and, with
+    `one_thread`, at 1 thread on one graph.  `samples` is a bounded sample of the config's batch
+    (10-30 s of CPU work; the whole config-2 batch takes ~19 s per step on 16 host threads): every
+    op of the path is linear in the number of graphs (per-graph losses, row-wise MLPs, segment
+    sums, graph-global LayerNorm statistics), so nodes/s on the sample stands for the batch of
+    `full_graphs` graphs; the sample is named in the record."""
+    threads, tinfo = cpu_threads()
+    prev = torch.get_num_threads()
     what = "inference forwards" if cfg.get("inference") else \
         f"training steps (fwd+NMSE{'+div' if cfg['divergence'] else ''}+bwd)"
-    step, nodes = _oracle_step_fn(cfg, samples)
-    rate, ts = _median_rate(step, nodes, reps)
-    torch.set_num_threads(1)
+    rec = {"unit": "nodes/s", "cores": threads, "kind": "port", "threads_info": tinfo}
     try:
-        step1, nodes1 = _oracle_step_fn(cfg, samples[:one_thread_graphs])
-        rate1, ts1 = _median_rate(step1, nodes1, one_thread_reps)
-    finally:
         torch.set_num_threads(threads)
-    return {"value": round(rate, 1), "unit": "nodes/s", "cores": threads, "kind": "port",
-            "sample": f"median of {reps} {what} (after 1 warm-up) of the config's batch: {len(samples)} graph(s), "
-                      f"{nodes} nodes, {cfg['steps']} MP steps, fp32, torch CPU ({threads} threads), "
-                      f"oracle/epd_oracle.py",
-            "step_s": [round(t, 3) for t in ts],
-            "value_1thread": round(rate1, 1),
-            "sample_1thread": f"median of {one_thread_reps} (after 1 warm-up), {one_thread_graphs} graph(s), "
-                              f"{nodes1} nodes, 1 thread",
-            "host_cpu_count": os.cpu_count(), "host_affinity": len(os.sched_getaffinity(0)),
-            "cpu_model": _cpu_model_name()}
+        step, nodes = _oracle_step_fn(cfg, samples)
+        rate, ts = _median_rate(step, nodes, reps)
+        rec.update(value=round(rate, 1), step_s=[round(t, 3) for t in ts],
+                   sample=f"median of {reps} {what} (after 1 warm-up) on {len(samples)} of the config's "
+                          f"{full_graphs} graph(s) ({nodes} nodes), {cfg['steps']} MP steps, fp32, torch CPU "
+                          f"at {threads} threads, oracle/epd_oracle.py"
+                          + ("" if len(samples) == full_graphs else
+                             "; nodes/s extrapolates linearly to the full batch (every op is linear in the "
+                             "number of graphs)"),
+                   extrapolated=len(samples) != full_graphs)
+        if one_thread:
+            torch.set_num_threads(1)
+            step1, nodes1 = _oracle_step_fn(cfg, samples[:1])
+            rate1, _ = _median_rate(step1, nodes1, reps)
+            rec.update(value_1thread=round(rate1, 1),
+                       sample_1thread=f"median of {reps} (after 1 warm-up), 1 graph, {nodes1} nodes, 1 thread")
+    finally:
+        torch.set_num_threads(prev)
+    rec.update(host_cpu_count=os.cpu_count(), cpu_model=_cpu_model_name())
+    return rec
 
 
 # ---------------------------------------------------------------------------------- roofline
@@ -217,10 +261,18 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
     }
 
 
+def pmc_tree() -> str | None:
+    """Tree hash the PMC file was measured on (tools/gpu_measure.sh writes it under "_meta")."""
+    if not PMC_FILE.exists():
+        return None
+    return json.loads(PMC_FILE.read_text()).get("_meta", {}).get("tree")
+
+
 def load_pmc(fused: bool) -> dict:
     pmc = {}
     if PMC_FILE.exists():
         data = json.loads(PMC_FILE.read_text())
+        data.pop("_meta", None)
         for k, prefix in PMC_NAMES.items():
             if fused and k == "edge_bwd":
                 prefix = PMC_NAMES["edge_bwd_w2"]
@@ -230,7 +282,8 @@ def load_pmc(fused: bool) -> dict:
     return pmc
 
 
-def roofline(k, work, kt, ktot, step_s, pmc):
+def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None):
+    nlaunch = nlaunch or {}
     terms, nbytes = work[k]
     t = kt[k]
     flops = sum(f for f, _ in terms)
@@ -242,17 +295,21 @@ def roofline(k, work, kt, ktot, step_s, pmc):
         ach, peak, unit = flops / t / 1e12, flops / t_peak / 1e12, "TFLOP/s"
     else:
         ach, peak, unit = nbytes / t / 1e9, PEAK_HBM / 1e9, "GB/s"
+    traffic = pmc.get(k)
     return {"kernel": k, "bound": bound, "achieved": round(ach, 2), "peak": round(peak, 1), "unit": unit,
-            "frac": round(ach / peak, 4), "traffic": pmc.get(k),
+            "frac": round(ach / peak, 4), "traffic": traffic,
+            # real DRAM rate: the PMC bytes of a launch (profiles/, same tree when traffic_tree matches)
+            # over this run's event-timed launch average, against 8 TB/s
+            "frac_pmc": round(traffic / t / PEAK_HBM, 4) if traffic else None,
             "traffic_source": (f"profiles/{PMC_FILE.name}: 2*FETCH_SIZE+WRITE_SIZE per dispatch" if k in pmc else None),
             "flops_per_launch": flops, "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4),
-            "frac_hbm": round(f_hbm, 4), "avg_launch_ms": round(t * 1e3, 4),
+            "frac_hbm": round(f_hbm, 4), "avg_launch_ms": round(t * 1e3, 4), "launches_timed": nlaunch.get(k),
             "share_of_step": round(ktot[k] / step_s, 4)}
 
 
 # ---------------------------------------------------------------------------------- timing
 TIMED_KERNELS = ["edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2", "segment_sum", "node_net", "node_bwd", "edge_enc_fwd",
-                 "node_pq", "gemm_sum2", "pq_scatter_bwd"]
+                 "node_pq", "gemm_sum2", "pq_scatter_bwd", "sync_collective"]
 
 
 def _allgather_ints(vals, world, device):
@@ -264,12 +321,37 @@ def _allgather_ints(vals, world, device):
     return [o.tolist() for o in out]
 
 
+def _allgather_floats(vals, world, device):
+    if world == 1:
+        return [list(vals)]
+    t = torch.tensor(vals, dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
 def _max_over_ranks(x: float, world: int, device) -> float:
     if world == 1:
         return x
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t)
+
+
+def per_rank_fields(world: int, device, pg, counts, step_ms: float, allreduce_ms: float, sync_ms: float) -> dict:
+    """Every rank's share and the split of its step (gathered to all ranks): nodes / edges / graphs,
+    the world size its process group reports, its own ms per step, the RCCL gradient all-reduce and
+    the sync-LN collectives per step (event-timed on the compute stream, so they include waiting for
+    the slowest rank), the rest as compute, and the node balance max/mean over ranks."""
+    ints = _allgather_ints(list(counts) + [dist.get_world_size() if pg is not None else 1], world, device)
+    fl = _allgather_floats([step_ms, allreduce_ms, sync_ms], world, device)
+    nodes = [r[0] for r in ints]
+    return {"nodes": nodes, "edges": [r[1] for r in ints], "graphs": [r[2] for r in ints],
+            "world_size_rccl": [r[3] for r in ints],
+            "step_ms": [round(r[0], 3) for r in fl], "allreduce_ms": [round(r[1], 4) for r in fl],
+            "sync_ln_collectives_ms": [round(r[2], 4) for r in fl],
+            "compute_ms": [round(r[0] - r[1] - r[2], 3) for r in fl],
+            "node_balance": round(max(nodes) / (sum(nodes) / world), 4) if sum(nodes) else None}
 
 
 def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: bool = False) -> tuple[dict, list]:
@@ -321,18 +403,30 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
             # replay); the other timed steps replay the graph captured during warmup
             trainer.capture = False
             eng.timed = {k: [] for k in TIMED_KERNELS}
+            trainer.timed = {}
         out = run_step()
     torch.cuda.synchronize()
+    el_local = time.perf_counter() - t0     # this rank's time (the max below adds the barrier skew)
     if pg is not None:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, world, device)
     ev = {k: v for k, v in eng.timed.items() if v}
+    coll = {k: sum(a.elapsed_time(b) for a, b in v) / ev_steps for k, v in (trainer.timed or {}).items()}
     eng.timed = None
+    trainer.timed = None
+    # per-rank split of a step: collectives (event-timed on the compute stream: the RCCL gradient
+    # all-reduce including its wait for the slowest rank, and the sync-LN collectives) and the rest
+    sync_ms = coll.get("sync_collective", 0.0) + (sum(a.elapsed_time(b) for a, b in ev["sync_collective"]) / ev_steps
+                                                   if "sync_collective" in ev else 0.0)
+    ar_ms = coll.get("allreduce", 0.0)
+    step_ms_local = el_local / args.steps * 1e3
     loss = float(out["total"])
-    per_rank = _allgather_ints([N, E, len(idx)], world, device)
-    total_nodes = sum(r[0] for r in per_rank)
+    per_rank_rec = per_rank_fields(world, device, pg, [N, E, len(idx)], step_ms_local, ar_ms, sync_ms)
+    total_nodes = sum(per_rank_rec["nodes"])
 
+    ev.pop("sync_collective", None)
     kt = {k: sum(a.elapsed_time(b) for a, b in v) / len(v) * 1e-3 for k, v in ev.items()}
+    nlaunch = {k: len(v) for k, v in ev.items()}
     ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
     fused = eng.fused_edge_wgrad
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
@@ -357,12 +451,12 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
                    "message_passing_steps": cfg["steps"], "latent": L, "divergence": cfg["divergence"],
                    "parallelism": f"graph-DP x{world}" + ("" if args.dp_mode == "replica" else " (sync-LN)"),
                    "final_loss": round(loss, 6), "hip_graph_steps": graph_steps,
-                   "per_rank": {"nodes": [r[0] for r in per_rank], "edges": [r[1] for r in per_rank],
-                                "graphs": [r[2] for r in per_rank]}},
-        "roofline": roofline(dominant, work, kt, ktot, step_s, pmc),
-        "roofline_gather_scatter": [roofline(k, work, kt, ktot, step_s, pmc)
+                   "per_rank": per_rank_rec},
+        "kernel_variants": eng.variants(),
+        "roofline": roofline(dominant, work, kt, ktot, step_s, pmc, nlaunch),
+        "roofline_gather_scatter": [roofline(k, work, kt, ktot, step_s, pmc, nlaunch)
                                     for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
-        "roofline_node_net": roofline("node_net", work, kt, ktot, step_s, pmc) if "node_net" in kt else None,
+        "roofline_node_net": roofline("node_net", work, kt, ktot, step_s, pmc, nlaunch) if "node_net" in kt else None,
         "kernel_ms": {k: round(v * 1e3, 4) for k, v in kt.items()},
     }
     del trainer, model, batch, plan
@@ -379,18 +473,24 @@ def time_plumbing(args, rank: int, world: int, pg, device) -> dict:
     if pg is not None:
         dist.barrier()
     t0 = time.perf_counter()
+    ar = 0.0
     for _ in range(args.steps):
         if pg is not None:
+            t1 = time.perf_counter()
             dist.all_reduce(bucket)
+            ar += time.perf_counter() - t1
+    el_local = time.perf_counter() - t0
     if pg is not None:
         dist.barrier()
     el = _max_over_ranks(time.perf_counter() - t0, world, device)
     per_rank = _allgather_ints([rank, dist.get_world_size() if pg is not None else 1], world, device)
+    split = per_rank_fields(world, device, pg, [0, 0, 0], el_local / args.steps * 1e3, ar / args.steps * 1e3, 0.0)
     return {"metric": "plumbing only (no HIP kernels): launch, rendezvous, timing and reporting of bench.py",
             "value": None, "unit": "nodes/s", "n_gpus": world, "ms_per_step": round(el / args.steps * 1e3, 3),
             "scaling": "weak", "plumbing": True,
             "config": {"workload": "gradient-bucket all-reduce only", "parallelism": f"graph-DP x{world}",
-                       "per_rank": {"rank": [r[0] for r in per_rank], "world_seen": [r[1] for r in per_rank]}}}
+                       "per_rank": {"rank": [r[0] for r in per_rank], "world_seen": [r[1] for r in per_rank],
+                                    **split}}}
 
 
 # ---------------------------------------------------------------------------------- launch
@@ -479,16 +579,18 @@ def main():
                 "backend": backend if pg is not None else None}
         line.update({k: v for k, v in res.items() if k not in line})
         cpu_ok = world == 1 and not args.no_cpu_baseline and not args.plumbing
-        line["cpu_baseline"] = cpu_baseline(CONFIGS[args.config], samples) if cpu_ok else None
+        line["tree"] = tree_hash()
+        line["pmc_tree"] = pmc_tree()
+        line["traffic_tree_match"] = line["pmc_tree"] == line["tree"]
+        cfg0 = CONFIGS[args.config]
+        # bounded samples (10-30 s of CPU work each): 2 graphs of a training batch, the config-5 mesh itself
+        line["cpu_baseline"] = (cpu_baseline(cfg0, samples[:2], full_graphs=cfg0["graphs"]) if cpu_ok else None)
         if subs:
             line["sub_results"] = {}
             for name, (r, s) in subs.items():
                 cfg = CONFIGS[int(name[-1])]
-                if cpu_ok:   # bounded samples: 2 graphs (config 3/4) or one 5,041-node mesh (config 5)
-                    if cfg.get("inference"):
-                        from pdg import meshgen
-                        s = meshgen.make_dataset(1, n=71, seed=69)
-                    r["cpu_baseline"] = cpu_baseline(cfg, s[:2], reps=3, one_thread_reps=1)
+                if cpu_ok:
+                    r["cpu_baseline"] = cpu_baseline(cfg, s[:2], full_graphs=cfg["graphs"], one_thread=False)
                 r["steps"], r["warmup"] = args.extra_steps, args.warmup
                 line["sub_results"][name] = r
         print(json.dumps(line), flush=True)

@@ -169,6 +169,11 @@ extern "C" int pdg_ln_colsum(int rows, const float* gy_rows, const int* gidx, co
 #ifndef PDG_COLSUM_NODES_BPC
 #define PDG_COLSUM_NODES_BPC 2   // 2 blocks per CU: config-2 step -0.008..-0.018 ms in 3 of 3 same-box A/B pairs
 #endif
+// every block adds its partial row into the caller's LayerNorm accumulator group, whose capacity is
+// 2 rows per CU (pdg_ln_colsum in include/pdivgnn.h; EPDEngine._acc_rows): a larger grid would write
+// into the next group's rows
+static_assert(PDG_COLSUM_NODES_BPC >= 1 && PDG_COLSUM_NODES_BPC <= 2,
+              "ln_colsum_nodes: the accumulator holds 2 partial rows per CU");
 __global__ __launch_bounds__(256) void ln_colsum_nodes_kernel(int N, const float* __restrict__ gaggr,
                                                               const int* __restrict__ rowptr,
                                                               const float* __restrict__ xs,

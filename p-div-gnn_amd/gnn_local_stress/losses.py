@@ -5,6 +5,8 @@
 * ``batch_loss``: the whole per-graph loop of gnn_train.py:168-197 fused into
   two segmented kernels over the batch's ``ptr`` (no Python loop, no dense
   operator), returning (total, nmse, div) with nmse/div already / batch_size.
+  All three are differentiable: total = nmse + div, and back-propagating nmse
+  and div separately (or their sum) gives the reference's gradients.
 
 All three run through the ``torch.ops.pdivgnn.batch_loss`` custom op (pdg.ops).
 """
@@ -33,7 +35,7 @@ def _loss(pred, gt, plan: GraphPlan, types, with_nmse: bool, divergence: bool, p
         plan.a_rowptr if d else None, plan.a_col if d else None, plan.a_val if d else None,
         plan.at_rowptr if d else None, plan.at_row if d else None, plan.at_comp if d else None,
         plan.at_val if d else None, bool(with_nmse), bool(divergence), float(penalty), bool(reduce_abs))
-    return total, nmse.detach(), div.detach()
+    return total, nmse, div
 
 
 def batch_loss(pred: torch.Tensor, batch, gt_std: torch.Tensor, divergence: bool = False,

@@ -60,7 +60,12 @@ class GraphLayerNorm(torch.nn.Module):
 
 
 def print_model(model: torch.nn.Module, data_loader, device: str) -> str:
-    """models.py:33-41 (PyG ``summary`` is unavailable): a parameter table."""
+    """models.py:33-41 (PyG ``summary`` is unavailable): a parameter table.  Like the reference it
+    takes one minibatch from a fresh iterator of ``data_loader`` (when given), so the global-RNG
+    draws of that iterator (base seed, sampler seed) happen here too and the training epochs that
+    follow see the reference's shuffles."""
+    if data_loader is not None:
+        next(iter(data_loader))
     lines = [f"{type(model).__name__}  (parameters: {sum(p.numel() for p in model.parameters()):,})"]
     for name, p in model.named_parameters():
         lines.append(f"  {name:40s} {tuple(p.shape)}")
@@ -178,7 +183,7 @@ class EncodeProcessDecode(StressFieldBaseModel):
         key = str(device)
         if key not in self._engines:
             eng = EPDEngine(device)
-            self._engines[key] = (ops.register_engine(eng), eng)
+            self._engines[key] = (ops.register_engine(eng, owner=self), eng)
         return self._engines[key][1]
 
     def stats_tensor(self, device) -> torch.Tensor:

@@ -14,9 +14,13 @@ the config in the results folder.  What runs underneath is MI355X-native:
   loss, HIP backward, Adam stepped with GradScaler's skip semantics) with no host sync;
 * the test pass runs the HIP forward under ``no_grad`` and the fused batch loss.
 
-Shuffling uses ``torch.utils.data.RandomSampler`` over the graph indices, the sampler PyG's
-``DataLoader(shuffle=True)`` uses, so the minibatch order follows torch's global RNG as the
-reference's does.  TensorBoard logging, dataset histograms and the tqdm bars are out of scope
+Minibatches come from ``torch.utils.data.DataLoader`` objects over the graph indices
+(``pdg.graph.index_loader``; PyG's ``DataLoader`` is that same torch loader with a graph collate),
+created where the reference creates its loaders (gnn_train.py:387-394) and iterated where it
+iterates them: ``print_model`` takes one batch from a fresh train iterator (models.py:38), every
+epoch iterates the train loader (one base-seed draw plus the RandomSampler's seed) and the test
+loader (one base-seed draw).  After ``torch.manual_seed(69)`` the harness therefore visits the
+graphs in the reference's order (tests/test_train_order.py).  TensorBoard logging, dataset histograms and the tqdm bars are out of scope
 (SURVEY §8); the losses they would log are printed and returned.
 
     python -m gnn_local_stress.train configs_train/config_train_div.yml
@@ -33,6 +37,7 @@ import numpy as np
 import torch
 
 from pdg.collate import DeviceGraphStore
+from pdg.graph import index_loader
 from pdg.trainer import Trainer
 
 from . import data_utils, datasets, losses, models
@@ -40,22 +45,23 @@ from . import data_utils, datasets, losses, models
 SEED = 69   # gnn_train.py:38
 
 
-def _batches(store: DeviceGraphStore, batch_size: int, shuffle: bool):
-    """PyG DataLoader(batch_size, shuffle) order over a device-resident store."""
-    n = store.num_graphs
-    order = list(torch.utils.data.RandomSampler(range(n))) if shuffle else list(range(n))
-    for i in range(0, n, batch_size):
-        yield store.batch(order[i:i + batch_size])
+def make_loaders(train_store: DeviceGraphStore, test_store: DeviceGraphStore, batch_size: int):
+    """The reference's two loaders (gnn_train.py:387-394) over the stores' graph indices."""
+    return (index_loader(train_store.num_graphs, batch_size, shuffle=True),
+            index_loader(test_store.num_graphs, batch_size, shuffle=False))
 
 
-def evaluate(model, store: DeviceGraphStore, batch_size: int, monitor_divergence: bool):
+def evaluate(model, store: DeviceGraphStore, loader, monitor_divergence: bool):
     """The test pass of gnn_train.py:208-252: sum over batches of (NMSE/B [+ div/B]) and of the
-    divergence term (unpenalised, as the reference monitors it), as device scalars."""
+    divergence term (unpenalised, as the reference monitors it), as device scalars.  ``loader``
+    yields graph-index lists (an int batch size builds an unshuffled one)."""
+    if isinstance(loader, int):
+        loader = index_loader(store.num_graphs, loader, shuffle=False)
     total = torch.zeros((), dtype=torch.float32, device=store.device)
     div_sum = torch.zeros((), dtype=torch.float32, device=store.device)
     nb = 0
     with torch.no_grad():
-        for batch in _batches(store, batch_size, shuffle=False):
+        for batch in (store.batch(idx) for idx in loader):
             pred = model.forward(batch, scale_output=False, scale_input=True).local_stress
             gt = data_utils.standardize(batch.local_stress, model.mean_local_stress, model.std_local_stress)
             t, _, d = losses.batch_loss(pred, batch, gt.float().contiguous(), divergence=monitor_divergence,
@@ -71,8 +77,10 @@ def train(model: models.EncodeProcessDecode, train_store: DeviceGraphStore, test
           epochs: int, batch_size: int, learning_rate: float = 0.001, weights_folder: str = "",
           early_stopping_limit: int = 10, optimize_divergence: bool = True, divergence_penalty: float = 1.0,
           train_all_epochs: bool = False, monitor_divergence_in_test: bool = False,
-          log=print) -> tuple[list[float], list[float]]:
-    """gnn_train.py:95-305 (without TensorBoard)."""
+          log=print, loaders=None) -> tuple[list[float], list[float]]:
+    """gnn_train.py:95-305 (without TensorBoard).  ``loaders``: the (train, test) index loaders
+    (make_loaders; built here when omitted)."""
+    train_loader, test_loader = loaders if loaders is not None else make_loaders(train_store, test_store, batch_size)
     trainer = Trainer(model, lr=learning_rate, divergence=optimize_divergence,
                       divergence_penalty=divergence_penalty)
     folder = Path(weights_folder)
@@ -97,15 +105,15 @@ def train(model: models.EncodeProcessDecode, train_store: DeviceGraphStore, test
         div_sum = torch.zeros((), dtype=torch.float32, device=dev)
         total_sum = torch.zeros((), dtype=torch.float32, device=dev)
         n_train = 0
-        for batch in _batches(train_store, batch_size, shuffle=True):
-            out = trainer.step(batch)
+        for idx in train_loader:
+            out = trainer.step(train_store.batch(idx))
             nmse_sum = nmse_sum + out["nmse"]
             total_sum = total_sum + out["total"]
             if optimize_divergence:
                 div_sum = div_sum + out["div"]
             n_train += 1
         model.eval()
-        test_total, test_div, n_test = evaluate(model, test_store, batch_size, monitor_divergence_in_test)
+        test_total, test_div, n_test = evaluate(model, test_store, test_loader, monitor_divergence_in_test)
         # one host sync per epoch (the reference's .item() calls, gnn_train.py:258-275)
         vals = torch.stack([nmse_sum, total_sum, div_sum, test_total, test_div]).tolist()
         train_mse_loss = vals[0] / n_train
@@ -158,7 +166,8 @@ def run_experience(dataset_train_csv: str, dataset_test_csv: str, results_folder
         input_edges_features_size=1, input_nodes_features_size=6, message_passing_steps=message_passing_steps,
         latent_size=latent_size, output_nodes_features_size=3,
         **{k: v.to(device) for k, v in train_dataset.stats().items()})
-    log(models.print_model(model, None, device))
+    loaders = make_loaders(train_store, test_store, batch_size)
+    log(models.print_model(model, loaders[0], device))
     model.to(device)
     results = Path(results_folder)
     results.mkdir(parents=True, exist_ok=True)
@@ -169,7 +178,7 @@ def run_experience(dataset_train_csv: str, dataset_test_csv: str, results_folder
                  weights_folder=(results / "weights").as_posix(), early_stopping_limit=early_stopping_limit,
                  optimize_divergence=divergence, divergence_penalty=divergence_penalty,
                  train_all_epochs=train_all_epochs, monitor_divergence_in_test=monitor_divergence_in_test,
-                 log=log)
+                 log=log, loaders=loaders)
 
 
 def main(config_path: str, **overrides: Any):

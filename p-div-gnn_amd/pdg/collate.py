@@ -186,8 +186,8 @@ class DeviceGraphStore:
         return out
 
     def batches(self, batch_size: int, shuffle: bool = False, generator: torch.Generator | None = None):
-        """Iterate over minibatches like PyG's DataLoader(batch_size, shuffle) (gnn_train.py:387-394)."""
-        order = (torch.randperm(self.num_graphs, generator=generator) if shuffle
-                 else torch.arange(self.num_graphs)).tolist()
-        for i in range(0, self.num_graphs, batch_size):
-            yield self.batch(order[i:i + batch_size])
+        """Iterate over minibatches like PyG's DataLoader(batch_size, shuffle) (gnn_train.py:387-394):
+        the same order and the same global-RNG draws (pdg.graph.index_loader)."""
+        from .graph import index_loader
+        for idx in index_loader(self.num_graphs, batch_size, shuffle, generator):
+            yield self.batch(idx)

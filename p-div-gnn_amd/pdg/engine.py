@@ -57,6 +57,82 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+# Kernel variants of the engine: attribute -> (A/B environment variable, shipped default).  The
+# defaults are the product path, the only one the full-size parity tests (tests/test_gpu_fullsize.py)
+# and the bench time; the alternatives are kept for same-box A/B timing (tools/ab_env.sh) and are
+# checked against the defaults by the GPU op / model tests.  Tests select them through the engine
+# attributes; the environment is read only under PDG_AB=1, and a non-default value set in the
+# environment without it is an error (a stray variable must not swap kernels silently).
+VARIANTS = {
+    # edge backward with the W2 / Wc weight gradients fused (pdg_edge_bwd_w2 / pdg_edge_gout_wc); False:
+    # pdg_edge_bwd + deferred pdg_wgrad_segments passes
+    "fused_edge_wgrad": ("PDG_FUSED_EDGE_WGRAD", True),
+    # P/Q gather backward before the Wc pass (gz1m / gz1e re-read while still in the Infinity Cache:
+    # pq_scatter_bwd 63.6 -> 59.7 us and edge_gout_wc 145 -> 140 us per call, same box)
+    "pq_first": ("PDG_PQ_FIRST", True),
+    # edge forward in the block-cooperative layout (pdg_edge_fwd_coop; 240 -> 230 us per call at config 2)
+    # instead of pdg_edge_fwd
+    "coop_fwd": ("PDG_EDGE_FWD_COOP", True),
+    # inference: the cooperative edge forward also forms the aggregation's message sums in fp64
+    # (pdg_edge_fwd_coop_seg + pdg_segsum_fixup; pdg_segsum_finish applies the message LayerNorm) instead of
+    # pdg_segment_sum re-reading a2m, and a2m is not stored (config 5: 11.8 -> 11.5 ms per step, same box).
+    # Training keeps pdg_segment_sum (seg_sums_train False): a2m is stored for the backward anyway and the
+    # in-kernel sums cost more than the re-read they save (9.91 vs 10.12 ms, config 2).  fp64, because fp32
+    # raw sums (sum a2m - deg mean cancels) flipped a relu mask bit against the fp64 reference.
+    "seg_sums": ("PDG_SEG_SUMS", True),
+    "seg_sums_train": ("PDG_SEG_SUMS_TRAIN", False),
+    # the backward's input gradient of x (gP, gQ -> gx) in bf16x6 (pdg_gemm_sum2_coop) instead of the fp32-MFMA
+    # pdg_gemm_sum2_rw
+    "gsum2_coop": ("PDG_GSUM2_COOP", True),
+    # node_net backward likewise (pdg_node_bwd_coop, three W^T products in bf16x6), and the cooperative
+    # node-encoder / decoder backward
+    "nbwd_coop": ("PDG_NODE_BWD_COOP", True),
+    # pdg_wgrad_pairs blocks per CU (2 per CU ran as two sequential block waves at 166 VGPRs: 9.07-9.12 vs
+    # 9.14-9.23 ms per config-2 step, same box)
+    "pair_blocks_per_cu": ("PDG_PAIR_BLOCKS_PER_CU", 1),
+    # pdg_edge_enc_fwd blocks per CU (104 VGPRs, 41 KB LDS per 8-wave block)
+    "enc_blocks_per_cu": ("PDG_ENC_BLOCKS_PER_CU", 2),
+}
+
+
+def _parse_variant(name: str, raw: str):
+    env, default = VARIANTS[name]
+    if isinstance(default, bool):
+        if raw not in ("0", "1"):
+            raise ValueError(f"{env}={raw!r}: expected 0 or 1")
+        return raw == "1"
+    try:
+        v = int(raw)
+    except ValueError:
+        raise ValueError(f"{env}={raw!r}: expected an integer") from None
+    if v < 1 or v > 4:
+        raise ValueError(f"{env}={raw!r}: expected 1..4")
+    return v
+
+
+def kernel_variants(overrides: dict | None = None) -> dict:
+    """The variant settings an engine starts with: the shipped defaults, the environment's A/B
+    selection under PDG_AB=1 (refused without it unless every value equals the default), then
+    ``overrides``."""
+    out = {k: d for k, (_, d) in VARIANTS.items()}
+    ab = os.environ.get("PDG_AB") == "1"
+    for name, (env, default) in VARIANTS.items():
+        raw = os.environ.get(env)
+        if raw is None:
+            continue
+        val = _parse_variant(name, raw)
+        if val != default and not ab:
+            raise RuntimeError(f"{env}={raw} selects a non-default kernel variant of the HIP path; these are "
+                               "for A/B timing only (set PDG_AB=1 to allow them), unset it to run the shipped "
+                               "kernels")
+        out[name] = val
+    for k, v in (overrides or {}).items():
+        if k not in VARIANTS:
+            raise KeyError(f"unknown kernel variant {k!r} (known: {sorted(VARIANTS)})")
+        out[k] = v
+    return out
+
+
 class _StatBuf:
     """A device array of pdg_ln_stat (or pdg_ln_bwd) structs."""
 
@@ -88,8 +164,9 @@ class FwdCtx:
 class EPDEngine:
     """Stateless executor; parameters are passed per call as a name->tensor dict."""
 
-    def __init__(self, device: torch.device) -> None:
+    def __init__(self, device: torch.device, variants: dict | None = None) -> None:
         self.device = torch.device(device)
+        var = kernel_variants(variants)
         self.max_blocks = lib.pdg_max_blocks()
         f64 = dict(dtype=torch.float64, device=self.device)
         self._part_a = torch.empty(self.max_blocks * 2, **f64)
@@ -106,45 +183,34 @@ class EPDEngine:
         self._nparts = ctypes.c_int(0)
         # one weight-gradient slab per block of pdg_wgrad_segments: three blocks per CU
         self._nslabs = lib.pdg_wgrad_slabs_per_cu() * torch.cuda.get_device_properties(self.device).multi_processor_count
-        # pdg_wgrad_pairs: one block per CU (2 per CU ran as two sequential block waves at 166 VGPRs:
-        # 9.07-9.12 vs 9.14-9.23 ms per config-2 step, same box)
-        self._nslabs_p = min(int(os.environ.get("PDG_PAIR_BLOCKS_PER_CU", "1")) *
+        self._nslabs_p = min(var["pair_blocks_per_cu"] *
                              torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
         self._pair = torch.zeros(2, **f64)
         self.sync = None
-        # edge backward with the W2 / Wc weight gradients fused (pdg_edge_bwd_w2 / pdg_edge_gout_wc);
-        # False selects pdg_edge_bwd + deferred pdg_wgrad_segments passes (kept for A/B and tests)
-        self.fused_edge_wgrad = os.environ.get("PDG_FUSED_EDGE_WGRAD", "1") != "0"
-        # backward order within a step: P/Q gather backward before the Wc pass (both only need the
-        # edge backward's outputs; gz1m / gz1e are re-read while still in the Infinity Cache:
-        # pq_scatter_bwd 63.6 -> 59.7 us and edge_gout_wc 145 -> 140 us per call, same box)
-        self.pq_first = os.environ.get("PDG_PQ_FIRST", "1") == "1"
-        # edge forward in the block-cooperative layout (pdg_edge_fwd_coop; 240 -> 230 us per call at
-        # config 2, same box) instead of pdg_edge_fwd (PDG_EDGE_FWD_COOP=0)
-        self.coop_fwd = os.environ.get("PDG_EDGE_FWD_COOP", "1") == "1"
+        # kernel variants (VARIANTS above; tests and A/B tools flip these attributes)
+        self.fused_edge_wgrad = var["fused_edge_wgrad"]
+        self.pq_first = var["pq_first"]
+        self.coop_fwd = var["coop_fwd"]
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
-        # inference: the cooperative edge forward also forms the aggregation's message sums in fp64
-        # (pdg_edge_fwd_coop_seg + pdg_segsum_fixup; pdg_segsum_finish applies the message LayerNorm)
-        # instead of pdg_segment_sum re-reading a2m, and a2m is not stored (config 5: 11.8 -> 11.5 ms
-        # per step, same box).  Training keeps pdg_segment_sum: a2m is stored for the backward anyway
-        # and the in-kernel sums cost more than the re-read they save (9.91 vs 10.12 ms, config 2).
-        # fp64, because fp32 raw sums (sum a2m - deg mean cancels) flipped a relu mask bit against the
-        # fp64 reference in a golden test.  PDG_SEG_SUMS=0 / PDG_SEG_SUMS_TRAIN=1 for A/B and tests.
-        self.seg_sums = self.coop_fwd and os.environ.get("PDG_SEG_SUMS", "1") == "1"
-        self.seg_sums_train = self.coop_fwd and os.environ.get("PDG_SEG_SUMS_TRAIN", "0") == "1"
-        # the backward's input gradient of x (gP, gQ -> gx) in bf16x6 (pdg_gemm_sum2_coop) instead of the
-        # fp32-MFMA pdg_gemm_sum2_rw (PDG_GSUM2_COOP=0)
-        self.gsum2_coop = os.environ.get("PDG_GSUM2_COOP", "1") == "1"
-        # node_net backward likewise (pdg_node_bwd_coop, three W^T products in bf16x6; PDG_NODE_BWD_COOP=0)
-        self.nbwd_coop = os.environ.get("PDG_NODE_BWD_COOP", "1") == "1"
-        # edge encoder forward blocks (pdg_edge_enc_fwd: 104 VGPRs, 41 KB LDS per 8-wave block)
-        self._enc_blocks = min(int(os.environ.get("PDG_ENC_BLOCKS_PER_CU", "2")) *
+        self.seg_sums = self.coop_fwd and var["seg_sums"]
+        self.seg_sums_train = self.coop_fwd and var["seg_sums_train"]
+        self.gsum2_coop = var["gsum2_coop"]
+        self.nbwd_coop = var["nbwd_coop"]
+        self._enc_blocks = min(var["enc_blocks_per_cu"] *
                                torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
         self._seg_part = torch.empty(2 * self._nslabs_e * L, dtype=torch.float64, device=self.device)
         self._seg_info = torch.empty(4 * self._nslabs_e, dtype=torch.int32, device=self.device)
         # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
         self.timed: dict | None = None
+
+    def variants(self) -> dict:
+        """The kernel variants in effect (recorded in the bench line)."""
+        cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        return {"fused_edge_wgrad": self.fused_edge_wgrad, "pq_first": self.pq_first, "coop_fwd": self.coop_fwd,
+                "seg_sums": self.seg_sums, "seg_sums_train": self.seg_sums_train, "gsum2_coop": self.gsum2_coop,
+                "nbwd_coop": self.nbwd_coop, "pair_blocks_per_cu": self._nslabs_p // cus,
+                "enc_blocks_per_cu": self._enc_blocks // cus}
 
     def _t(self, name: str, fn, *args):
         """Launch fn(*args); when timing is enabled for `name`, bracket it with HIP events
@@ -170,7 +236,7 @@ class EPDEngine:
         # exact DP LayerNorm: statistics of the whole minibatch over all ranks
         group, n_glob, e_glob = self.sync
         lib.pdg_ln_partials_sum(part.data_ptr(), self._nparts.value, self._pair.data_ptr(), s)
-        torch.distributed.all_reduce(self._pair, group=group)
+        self._t("sync_collective", lambda: torch.distributed.all_reduce(self._pair, group=group))
         lib.pdg_ln_finalize(self._pair.data_ptr(), 1, float((e_glob if edges else n_glob) * L), out_ptr, s)
 
     def set_sync(self, group, n_nodes_global: int = 0, n_edges_global: int = 0) -> None:
@@ -389,7 +455,7 @@ class EPDEngine:
             out = self._sync_pairs[sync_slot[0] % 8]
             sync_slot[0] += 1
             lib.pdg_ln_partials_sum(_p(pp), n, _p(out), s)
-            torch.distributed.all_reduce(out, group=self.sync[0])
+            self._t("sync_collective", lambda: torch.distributed.all_reduce(out, group=self.sync[0]))
             return _p(out), 1
 
         def edge_ln_pairs(pp, gy_rows, a2, st_ptr, accb, g):
@@ -566,9 +632,15 @@ class EPDEngine:
             ("ee2", "edge_encoder.2.weight", L, 0, "edge_encoder.2.bias"),
         ]
         ns = self._nslabs
-        if getattr(self, "_slabs", None) is None or self._slabs.device != self.device:
-            # one slab set per deferred weight (the reductions run batched at the end)
-            self._slabs = torch.empty(len(red), ns, L * L + L, dtype=torch.float32, device=self.device)
+        slab_sets = self.__dict__.setdefault("_slab_sets", {})
+
+        def slab_set(key):
+            """The slab set of one deferred weight (the reductions run batched at the end), allocated
+            the first time that weight has a segment pass: with the fused edge backward and the pair
+            passes only node_net.2, the decoder and the node encoder need one."""
+            if key not in slab_sets:
+                slab_sets[key] = torch.empty(ns, L * L + L, dtype=torch.float32, device=self.device)
+            return slab_sets[key]
         # the weight pairs that share an operand, one pass each (pdg_wgrad_pairs): Wa / Wb against x
         # (gP, gQ), node_net.0's halves from gz1n (against aggr, x)
         nsp = self._nslabs_p
@@ -613,15 +685,15 @@ class EPDEngine:
                     (ctypes.c_void_p * n)(*[g.data_ptr() for g, _, _ in flat]),
                     (ctypes.c_void_p * n)(*[x.data_ptr() for _, x, _ in flat]),
                     (ctypes.c_int * n)(*[r for _, _, r in flat]),
-                    (ctypes.c_void_p * len(grp))(*[_p(self._slabs[[r[0] for r in red].index(k[0])]) for k in grp]),
+                    (ctypes.c_void_p * len(grp))(*[_p(slab_set(k[0])) for k in grp]),
                     ns, s)
             for key, wname, ld, col0, bname in grp:
-                reduce_now_or_later(self._slabs[[r[0] for r in red].index(key)], ns, wname, ld, col0, bname, True)
+                reduce_now_or_later(slab_set(key), ns, wname, ld, col0, bname, True)
         for key, wname, ld, col0, bname in red_k:
             sl = segs[key]
             if len(sl) <= 32:
                 continue
-            slabs_k = self._slabs[[r[0] for r in red].index(key)]
+            slabs_k = slab_set(key)
             for c0 in range(0, len(sl), 32):
                 chunk = sl[c0:c0 + 32]
                 n = len(chunk)

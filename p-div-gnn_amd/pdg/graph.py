@@ -181,22 +181,25 @@ class Batch(Data):
         return out
 
 
-class DataLoader:
-    """PyG ``DataLoader`` subset used by the reference scripts (gnn_train.py:387-394,
-    gnn_inference.py:103-107): host collate of ``batch_size`` graphs, optional shuffle."""
+class DataLoader(torch.utils.data.DataLoader):
+    """PyG ``DataLoader`` (gnn_train.py:387-394, gnn_inference.py:103-107): like PyG's, a
+    ``torch.utils.data.DataLoader`` whose collate is ``Batch.from_data_list``.  Being the torch
+    loader itself, it draws from torch's global RNG exactly as the reference's loaders do (one
+    base seed per iterator, plus the RandomSampler's seed when shuffling), so a seeded run visits
+    the graphs in the reference's order."""
 
     def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False,
-                 generator: torch.Generator | None = None) -> None:
-        self.dataset = dataset
-        self.batch_size = int(batch_size)
-        self.shuffle = shuffle
-        self.generator = generator
+                 generator: torch.Generator | None = None, **kwargs: Any) -> None:
+        kwargs.pop("collate_fn", None)
+        super().__init__(dataset, batch_size=batch_size, shuffle=shuffle, generator=generator,
+                         collate_fn=Batch.from_data_list, **kwargs)
 
-    def __len__(self) -> int:
-        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
 
-    def __iter__(self):
-        n = len(self.dataset)
-        order = torch.randperm(n, generator=self.generator).tolist() if self.shuffle else list(range(n))
-        for i in range(0, n, self.batch_size):
-            yield Batch.from_data_list([self.dataset[j] for j in order[i:i + self.batch_size]])
+def index_loader(num_graphs: int, batch_size: int, shuffle: bool,
+                 generator: torch.Generator | None = None) -> torch.utils.data.DataLoader:
+    """The graph-index lists a PyG ``DataLoader(dataset, batch_size, shuffle)`` over ``num_graphs``
+    graphs would collate, in the same order and with the same global-RNG draws (a torch
+    DataLoader over ``range(num_graphs)`` with a list collate).  Device-resident stores
+    (``pdg.collate.DeviceGraphStore``) collate these indices on the GPU."""
+    return torch.utils.data.DataLoader(range(num_graphs), batch_size=batch_size, shuffle=shuffle,
+                                       generator=generator, collate_fn=list)

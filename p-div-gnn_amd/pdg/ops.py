@@ -44,12 +44,20 @@ _engine_keys = itertools.count(1)
 _plans: dict = {}                # id(edge_index) -> (weakref, num_nodes, version, GraphPlan)
 
 
-def register_engine(engine: EPDEngine) -> int:
+def register_engine(engine: EPDEngine, owner=None) -> int:
     """Key under which the ops find ``engine`` (a model's own executor: its scratch buffers and
-    data-parallel settings stay its own).  Engines live as long as the process."""
+    data-parallel settings stay its own).  With ``owner`` (the model) the registration ends when
+    the owner is garbage collected, so the engine's device scratch is freed with the model; a
+    pending backward keeps its engine alive through its saved context."""
     key = next(_engine_keys)
     _engines[key] = engine
+    if owner is not None:
+        weakref.finalize(owner, unregister_engine, key)
     return key
+
+
+def unregister_engine(key: int) -> None:
+    _engines.pop(key, None)
 
 
 def engine_for(device, key: int = 0) -> EPDEngine:
@@ -195,28 +203,33 @@ def _(pred, gt, ptr, types, a_rowptr, a_col, a_val, at_rowptr, at_row, at_comp, 
 
 
 @torch.library.custom_op("pdivgnn::batch_loss_backward", mutates_args=())
-def batch_loss_backward(g_total: Tensor, pred: Tensor, gt: Optional[Tensor], ptr: Tensor, den: Tensor,
-                        divf: Tensor, at_rowptr: Optional[Tensor], at_row: Optional[Tensor],
-                        at_comp: Optional[Tensor], at_val: Optional[Tensor], penalty: float,
-                        reduce_abs: bool) -> Tensor:
+def batch_loss_backward(g_total: Tensor, g_nmse: Tensor, g_div: Tensor, pred: Tensor, gt: Optional[Tensor],
+                        ptr: Tensor, den: Tensor, divf: Tensor, at_rowptr: Optional[Tensor],
+                        at_row: Optional[Tensor], at_comp: Optional[Tensor], at_val: Optional[Tensor],
+                        penalty: float, reduce_abs: bool) -> Tensor:
+    """d(loss)/d(pred) for upstream gradients of all three scalar outputs: total = nmse + div, so
+    the NMSE term's gradient is scaled by g_total + g_nmse and the divergence term's by
+    g_total + g_div (a caller may back-propagate nmse and div separately, as the reference's
+    batch_loss and batch_divergence_loss are separate tensors, gnn_train.py:168-197)."""
     s = stream_handle(pred.device)
     B, N = ptr.numel() - 1, pred.shape[0]
     pred = pred.float().contiguous()
-    scale = (g_total.float() / B).reshape(1).contiguous()
+    gt_all = g_total.float().reshape(1)
     gp = torch.zeros_like(pred)
     if den.numel():
         gt = gt.float().contiguous()
+        scale = ((gt_all + g_nmse.float().reshape(1)) / B).contiguous()
         lib.pdg_nmse_bwd(B, ptr.data_ptr(), N, gt.data_ptr(), pred.data_ptr(), den.data_ptr(), scale.data_ptr(), 0,
                          gp.data_ptr(), s)
     if divf.numel():
-        sd = (scale * penalty).contiguous()
+        sd = ((gt_all + g_div.float().reshape(1)) * (penalty / B)).contiguous()
         lib.pdg_div_bwd(B, ptr.data_ptr(), N, at_rowptr.data_ptr(), at_row.data_ptr(), at_comp.data_ptr(),
                         at_val.data_ptr(), divf.data_ptr(), sd.data_ptr(), int(reduce_abs), 1, gp.data_ptr(), s)
     return gp
 
 
 @batch_loss_backward.register_fake
-def _(g_total, pred, gt, ptr, den, divf, at_rowptr, at_row, at_comp, at_val, penalty, reduce_abs):
+def _(g_total, g_nmse, g_div, pred, gt, ptr, den, divf, at_rowptr, at_row, at_comp, at_val, penalty, reduce_abs):
     return torch.empty_like(pred)
 
 
@@ -229,11 +242,14 @@ def _loss_setup(ctx, inputs, output):
     ctx.save_for_backward(pred, ptr, output[3], output[4], *((gt,) if ctx.has_gt else ()), *at)
 
 
-def _loss_bwd(ctx, g_total, _g_nmse, _g_div, _g_den, _g_divf):
+def _loss_bwd(ctx, g_total, g_nmse, g_div, _g_den, _g_divf):
     pred, ptr, den, divf, *rest = ctx.saved_tensors
     gt = rest.pop(0) if ctx.has_gt else None
     at = rest if ctx.has_at else [None, None, None, None]
-    gp = torch.ops.pdivgnn.batch_loss_backward(g_total, pred, gt, ptr, den, divf, *at, ctx.penalty, ctx.reduce_abs)
+    zero = torch.zeros((), dtype=torch.float32, device=pred.device)
+    g_total, g_nmse, g_div = (zero if g is None else g for g in (g_total, g_nmse, g_div))
+    gp = torch.ops.pdivgnn.batch_loss_backward(g_total, g_nmse, g_div, pred, gt, ptr, den, divf, *at, ctx.penalty,
+                                               ctx.reduce_abs)
     return (gp,) + (None,) * 14
 
 

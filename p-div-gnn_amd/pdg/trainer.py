@@ -59,7 +59,10 @@ class Trainer:
         sizes = [int(torch.Size(s).numel()) for _, s in PARAM_SHAPES]
         total = sum(sizes)
         self.flat_p = torch.empty(total, dtype=torch.float32, device=dev)
-        self.flat_g = torch.zeros(total, dtype=torch.float32, device=dev)
+        # the all-reduced bucket: every parameter gradient, then one slot holding 1.0 when this rank's
+        # batch has a nonzero mean stress (the zero-mean-stress guard of models.py:294-299, below)
+        self._bucket = torch.zeros(total + 1, dtype=torch.float32, device=dev)
+        self.flat_g = self._bucket[:total]
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
         self.P, self.G = {}, {}
@@ -81,9 +84,29 @@ class Trainer:
         self._calls = 0
         self._count_bound = 0
         self._table = None
+        self._table_key = None
+        self._nz_cache: dict = {}
         # captured forward+backward per batch object (dp_mode="sync" reads counts on the host: eager)
         self.capture = capture and not self.sync
         self._graph = None            # (id(batch), torch.cuda.CUDAGraph, static outputs)
+        # optional live timing of the data-parallel collectives: name -> list of (start, end) event
+        # pairs on the current stream ("allreduce": the gradient bucket; "sync_collective": the
+        # global row counts of dp_mode="sync")
+        self.timed: dict | None = None
+
+    def _mark(self, name: str):
+        """Start an event-timed region on the current stream; returns its end() (a no-op when
+        timing is off)."""
+        if self.timed is None:
+            return lambda: None
+        a = torch.cuda.Event(enable_timing=True)
+        a.record()
+
+        def end():
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            self.timed.setdefault(name, []).append((a, b))
+        return end
 
     def _gt(self, batch) -> torch.Tensor:
         key = id(batch)
@@ -91,6 +114,20 @@ class Trainer:
             m = self.model
             self._gt_cache = {key: ((batch.local_stress - m.mean_local_stress) / m.std_local_stress).float().contiguous()}
         return self._gt_cache[key]
+
+    def _nonzero_flag(self, batch) -> torch.Tensor:
+        """1.0 when any mean stress of `batch` is nonzero, else 0.0 (a device scalar): the guard of
+        models.py:294-299 without its host sync.  Cached per batch object while mean_stress is
+        unchanged (bench / training re-use resident batches)."""
+        ms = batch.mean_stress
+        key = (id(batch), id(ms), ms._version)
+        hit = self._nz_cache.get("k")
+        if hit != key:
+            flag = torch.zeros(1, dtype=torch.int32, device=self.device)
+            msf = ms.float().contiguous()
+            lib.pdg_any_nonzero(msf.data_ptr(), msf.numel(), flag.data_ptr(), stream_handle(self.device))
+            self._nz_cache = {"k": key, "v": flag.float(), "batch": batch}
+        return self._nz_cache["v"]
 
     def step(self, batch) -> dict:
         """One optimisation step; returns device scalars (no host sync, except one read of the
@@ -104,7 +141,9 @@ class Trainer:
         Bn = B                                      # loss normaliser (gnn_train.py:193/196)
         if self.sync:
             cnt = torch.tensor([N, plan.n_edges, B], dtype=torch.float64, device=self.device)
+            end = self._mark("sync_collective")
             torch.distributed.all_reduce(cnt, group=self.pg)
+            end()
             n_g, e_g, Bn = (int(v) for v in cnt.tolist())
             self.engine.set_sync(self.pg, n_g, e_g)
         try:
@@ -112,7 +151,7 @@ class Trainer:
                 out = self._replay(batch, plan, stats8, B, N, Bn, f32)
             else:
                 out = self._fwd_bwd(batch, plan, stats8, B, N, Bn, f32, s)
-            return self._update(out, f32, s)
+            return self._update(out, f32, s, self._nonzero_flag(batch))
         finally:
             self.engine.set_sync(None)
 
@@ -170,12 +209,22 @@ class Trainer:
         del ctx
         return out
 
-    def _update(self, out, f32, s) -> dict:
+    def _update(self, out, f32, s, nz) -> dict:
+        # zero-mean-stress guard (models.py:294-299): the reference's forward returns zeros without a
+        # graph there, so its backward() raises and no update happens.  Here the step is skipped like a
+        # non-finite one (parameters, moments and Adam's count unchanged; out["skipped"] = 1), decided
+        # on the device.  Under data parallelism the flag rides in the gradient bucket, so the step is
+        # skipped on every rank exactly when the GLOBAL minibatch is all zero, as one device would.
+        self._bucket[-1:].copy_(nz)
         if self.pg is not None:
-            torch.distributed.all_reduce(self.flat_g, group=self.pg)
+            end = self._mark("allreduce")
+            torch.distributed.all_reduce(self._bucket, group=self.pg)
+            end()
             if self.sync:                           # per-rank shares of the global-batch loss: sum
                 parts = torch.stack([out["nmse"], out.get("div", torch.zeros((), **f32))])
+                end = self._mark("sync_collective")
                 torch.distributed.all_reduce(parts, group=self.pg)
+                end()
                 out["nmse"] = parts[0]
                 if "div" in out:
                     out["div"] = parts[1]
@@ -183,6 +232,7 @@ class Trainer:
                 self.flat_g.mul_(1.0 / torch.distributed.get_world_size(self.pg))
         self._ensure_table(self._count_bound + 1)
         lib.pdg_nonfinite(self.flat_g.data_ptr(), self.flat_g.numel(), self._skip.data_ptr(), s)
+        self._skip.bitwise_or_(self._bucket[-1:].eq(0))
         lib.pdg_adam(self.flat_p.numel(), self.flat_p.data_ptr(), self.flat_g.data_ptr(), self.exp_avg.data_ptr(),
                      self.exp_avg_sq.data_ptr(), self._table.data_ptr(), self._table.shape[0],
                      float(1.0 - self.betas[0]), self.betas[1], float(1.0 - self.betas[1]), self.eps,
@@ -198,9 +248,12 @@ class Trainer:
     def _ensure_table(self, need: int) -> None:
         """Bias-correction table of torch.optim.Adam (_single_tensor_adam, capturable=False): entry
         t-1 = (lr / (1 - beta1**t), (1 - beta2**t) ** 0.5) in Python double, stored as float32 (the
-        precision the elementwise ops apply them in).  Grown by doubling, never per step."""
-        if self._table is not None and self._table.shape[0] >= need:
+        precision the elementwise ops apply them in).  Grown by doubling, never per step; rebuilt when
+        lr or betas are reassigned (e.g. a learning-rate schedule writing trainer.lr)."""
+        key = (float(self.lr), tuple(float(b) for b in self.betas))
+        if self._table is not None and self._table.shape[0] >= need and self._table_key == key:
             return
+        self._table_key = key
         n = max(64, 2 * need)
         b1, b2 = self.betas
         rows = []

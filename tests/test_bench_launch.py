@@ -32,6 +32,13 @@ def _check(d):
     assert d["n_gpus"] == 2 and d["world_size_rccl"] == 2 and d["plumbing"] is True
     assert d["config"]["per_rank"]["rank"] == [0, 1]
     assert d["config"]["per_rank"]["world_seen"] == [2, 2]
+    pr = d["config"]["per_rank"]
+    # the per-rank split of a step the driver's 8-GPU run reports
+    for k in ("step_ms", "allreduce_ms", "sync_ln_collectives_ms", "compute_ms", "world_size_rccl", "nodes"):
+        assert len(pr[k]) == 2, k
+    assert pr["world_size_rccl"] == [2, 2]
+    assert all(a > 0 for a in pr["allreduce_ms"])
+    assert all(abs(s - a - c) < 1e-2 for s, a, c in zip(pr["step_ms"], pr["allreduce_ms"], pr["compute_ms"]))
     assert d["value"] is None and d["ms_per_step"] > 0
 
 

@@ -11,6 +11,11 @@ the HIP backward produced.
 * An injected NaN gradient: GradScaler skips optimizer.step(), so parameters, moments and
   Adam's step count stay put and the next step's bias correction is that of the step after
   the last real one (the advisor's round-1 finding).
+* A batch whose mean stress is all zero (the guard of gnn_local_stress/models.py:294-299, where
+  the reference's forward returns zeros without a graph and no update can follow) skips the
+  step the same way: nothing moves, ``skipped`` is 1.
+* Assigning ``trainer.lr`` between steps takes effect at the next step, as assigning the
+  param group's lr does for torch.optim.Adam.
 * state_dict() speaks torch.optim.Adam's format: a Trainer resumed from it, and a torch Adam
   resumed from it, continue identically.
 """
@@ -95,7 +100,7 @@ def _step(tr, batch, poison=False):
     out = tr._fwd_bwd(batch, plan, tr.model.stats_tensor(tr.device), plan.n_graphs, plan.n_nodes, plan.n_graphs,
                       f32, stream_handle(tr.device))
     tr.flat_g[1234] = float("nan")
-    return tr._update(out, f32, stream_handle(tr.device))
+    return tr._update(out, f32, stream_handle(tr.device), tr._nonzero_flag(batch))
 
 
 def test_adam_matches_torch_over_steps():
@@ -147,3 +152,42 @@ def test_state_dict_round_trip_with_torch_adam():
         ref.step(tr2)
         ref.check(tr2)
     assert tr2.step_count == 5
+
+
+def test_zero_mean_stress_batch_skips_update():
+    tr, batch = _setup(divergence=True)
+    tr.step(batch)
+    torch.cuda.synchronize()
+    zero = batch.clone() if hasattr(batch, "clone") else None
+    if zero is None:
+        import copy
+        zero = copy.copy(batch)
+    zero.mean_stress = torch.zeros_like(batch.mean_stress)
+    before = (tr.flat_p.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(), tr.step_count)
+    out = tr.step(zero)
+    torch.cuda.synchronize()
+    assert int(out["skipped"]) == 1
+    assert torch.equal(before[0], tr.flat_p) and torch.equal(before[1], tr.exp_avg)
+    assert torch.equal(before[2], tr.exp_avg_sq) and tr.step_count == before[3]
+    # the guard is per batch content: the original batch steps again, and an in-place zeroing of a
+    # batch already seen is noticed (the flag cache keys on the tensor's version counter)
+    out = tr.step(batch)
+    torch.cuda.synchronize()
+    assert int(out["skipped"]) == 0 and tr.step_count == before[3] + 1
+    batch.mean_stress.zero_()
+    out = tr.step(batch)
+    torch.cuda.synchronize()
+    assert int(out["skipped"]) == 1 and tr.step_count == before[3] + 1
+
+
+def test_lr_assignment_takes_effect():
+    tr, batch = _setup(divergence=False)
+    ref = _RefAdam(tr)
+    for lr in (1e-3, 1e-3, 3e-4, 3e-4, 2e-3):
+        tr.lr = lr
+        for g in ref.opt.param_groups:
+            g["lr"] = lr
+        _step(tr, batch)
+        torch.cuda.synchronize()
+        ref.step(tr)
+        ref.check(tr)

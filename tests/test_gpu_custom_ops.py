@@ -106,3 +106,43 @@ def test_ops_refuse_cpu_tensors():
     args[2] = args[2].cpu()
     with pytest.raises(RuntimeError, match="HIP device"):
         torch.ops.pdivgnn.epd_forward(*args)
+
+
+def test_batch_loss_separate_outputs_carry_gradients():
+    """nmse and div are differentiable outputs (total = nmse + div): d(a*nmse + b*div)/d(pred)
+    = a*d(nmse) + b*d(div), each part checked against the fp64 oracle's gradient."""
+    from gnn_local_stress import losses
+    from oracle import epd_oracle as O
+    m, b = _setup(steps=2)
+    with torch.no_grad():
+        pred0 = m(b, scale_output=False).local_stress
+    gt = ((b.local_stress - m.mean_local_stress) / m.std_local_stress).float().contiguous()
+    ops64 = [d.op_div_matrix.double() for d in b._data_list]
+
+    def oracle_grad(wn, wd):
+        p = pred0.detach().cpu().double().requires_grad_(True)
+        _, n, d = O.batch_loss(p, gt.cpu().double(), b.ptr, ops64, b.nodes_types.cpu(), True, 10.0)
+        (wn * n + wd * d).backward()
+        return p.grad
+
+    for wn, wd in ((1.0, 0.0), (0.0, 1.0), (2.0, -0.5)):
+        pred = pred0.clone().requires_grad_(True)
+        _, nmse, div = losses.batch_loss(pred, b, gt, divergence=True, divergence_penalty=10.0)
+        (wn * nmse + wd * div).backward()
+        ref = oracle_grad(wn, wd)
+        err = float((pred.grad.double().cpu() - ref).norm() / ref.norm())
+        assert err < 1e-5, (wn, wd, err)
+
+
+def test_model_engines_are_freed_with_the_model():
+    """A model's executor (and its device scratch) is unregistered when the model is collected."""
+    from pdg import ops
+    n0 = len(ops._engines)
+    for _ in range(3):
+        m, b = _setup(steps=1, n=9, graphs=1)
+        out = m(b).local_stress
+        out.sum().backward()
+        assert len(ops._engines) == n0 + 1
+        del m, out
+        gc.collect()
+        assert len(ops._engines) == n0

@@ -1,4 +1,4 @@
-"""Parity at the BASELINE workloads themselves (BASELINE.json configs[1], [2], [4]): the exact
+"""Parity at the BASELINE workloads themselves (BASELINE.json configs[1] to [4]): the exact
 batches bench.py times, run through the exact benchmarked path (pdg.trainer.Trainer for
 training, EncodeProcessDecode.forward under no_grad for inference), checked against the CPU
 oracle (oracle/epd_oracle.py) in float32 AND float64 on this host.
@@ -7,6 +7,11 @@ oracle (oracle/epd_oracle.py) in float32 AND float64 on this host.
   forward + backward;
 * config 3 — 32 x 5,041 nodes (N = 161,312, E = 958,976), NMSE + 10 x divergence, forward +
   backward (the divergence stencil at full size);
+* config 4 — 64 hyperelastic-style hole plates (N = 312,688, E = 1,853,216 at seed 69: internal-
+  boundary nodes labelled -1, strain +-0.15), NMSE + 10 x divergence, forward + backward: the
+  largest graph-LayerNorm reductions of any config (2.4e8 elements per edge LayerNorm, 3.7e7
+  rows per W2 weight gradient) and the only one with the -1 divergence mask at scale
+  (scripts/gnn_train.py:79-86);
 * config 5 — one 317 x 317 periodic mesh (N = 100,489, E = 601,672), 15 MP steps, inference.
 
 Tolerances (north_star "within 1e-5 rel fp32"; the same rules as tests/test_gpu_model.py):
@@ -16,12 +21,13 @@ sizes at which the bf16x6 products (W2 in the edge kernels, every weight gradien
 graph-LayerNorm reductions accumulate the most terms (up to 9.6e5 rows per LayerNorm and 2e7
 rows per weight gradient), so they are where a precision shortfall would show.
 
-At config 3 the oracle keeps activations of one message-passing step at a time
+At configs 3 and 4 the oracle keeps activations of one message-passing step at a time
 (checkpoint_steps: ~35 GB of host memory in float64 instead of ~170 GB) and the float32 oracle
 runs only when a gradient is outside the fixed 1e-4 bound (it can only loosen the bound): the
 float64 run alone takes a few minutes of host CPU.  A heartbeat line is appended to
 gpurun_out/fullsize_heartbeat.log every 20 s while a test runs (long silent runs look hung).
-Set PDG_PARITY_LOG=<file> to append the measured errors as JSON lines.
+Every test appends its measured errors as one JSON line to gpurun_out/parity.jsonl (and to
+$PDG_PARITY_LOG when set), so the margins to the tolerances are on record, not only "passed".
 """
 import json
 import os
@@ -68,10 +74,17 @@ def _heartbeat(request):
 
 
 def _log(rec):
-    path = os.environ.get("PDG_PARITY_LOG")
-    if path:
-        with open(path, "a") as f:
-            f.write(json.dumps(rec) + "\n")
+    rec = {**rec, "out_tol": OUT_TOL, "grad_tol_rule": f"max({GRAD_TOL}, 2 x fp32-oracle vs fp64)"}
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", Path(__file__).resolve().parents[1])) / "gpurun_out"
+    paths = [out / "parity.jsonl"] + ([Path(os.environ["PDG_PARITY_LOG"])] if os.environ.get("PDG_PARITY_LOG") else [])
+    for path in paths:
+        try:
+            path.parent.mkdir(parents=True, exist_ok=True)
+            with open(path, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+        except OSError:
+            pass
+    print("parity:", json.dumps(rec))
 
 
 def _workload(config):
@@ -104,8 +117,9 @@ def _oracle(params, stats, batch, steps, dtype, divergence, train, checkpoint=Fa
     return pred.detach(), float(total), float(nmse), {k: v.grad for k, v in P.items()}
 
 
-@pytest.mark.timeout(900)
-@pytest.mark.parametrize("config", [2, 3])
+@pytest.mark.parametrize("config", [pytest.param(2, marks=pytest.mark.timeout(900)),
+                                    pytest.param(3, marks=pytest.mark.timeout(900)),
+                                    pytest.param(4, marks=pytest.mark.timeout(1100))])
 def test_training_step_at_baseline_size(config):
     from pdg.trainer import Trainer
     torch.set_num_threads(min(16, os.cpu_count() or 1))
@@ -121,7 +135,9 @@ def test_training_step_at_baseline_size(config):
     del tr, out
     big = batch.num_edges > 500_000
     p64, t64, n64, g64 = _oracle(params, stats, batch, cfg["steps"], torch.float64, cfg["divergence"], True, big)
-    rec = {"config": config, "nodes": batch.num_nodes, "edges": batch.num_edges,
+    t0 = time.time()
+    rec = {"config": config, "nodes": batch.num_nodes, "edges": batch.num_edges, "graphs": batch.num_graphs,
+           "internal_boundary_nodes": int((batch.nodes_types == -1).sum()),
            "pred_vs_f64": rel(pred, p64), "loss_vs_f64": abs(total - t64) / abs(t64),
            "nmse_vs_f64": abs(nmse - n64) / abs(n64), "grads": {}}
     need32 = not big or any(rel(grads[n], g64[n]) > GRAD_TOL for n in g64)
@@ -131,6 +147,9 @@ def test_training_step_at_baseline_size(config):
         rec.update(pred_vs_f32=rel(pred, p32), f32_vs_f64=rel(p32, p64), loss_f32_vs_f64=abs(t32 - t64) / abs(t64))
     for name in g64:
         rec["grads"][name] = (rel(grads[name], g64[name]), rel(g32[name], g64[name]) if g32 else None)
+    worst = max(rec["grads"], key=lambda n: rec["grads"][n][0])
+    rec["worst_grad"] = [worst, *rec["grads"][worst]]
+    rec["oracle_s"] = round(time.time() - t0, 1)
     _log(rec)
     assert rec["pred_vs_f64"] < OUT_TOL and rec.get("pred_vs_f32", 0.0) < OUT_TOL, rec
     assert rec["loss_vs_f64"] < OUT_TOL and rec["nmse_vs_f64"] < OUT_TOL, rec

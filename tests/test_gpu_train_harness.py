@@ -4,7 +4,7 @@ end to end over device-resident datasets and writes what the reference writes.
 
 Checked: the best / last checkpoints exist in the reference's format and reload; the config is
 copied; early stopping follows the reference's rule; and the epoch losses equal an independent
-replay of the same loop (same seed, the same RandomSampler order as PyG's DataLoader, one
+replay of the same loop (same seed, torch DataLoaders drawing from the RNG as PyG's do, one
 Trainer step per minibatch, losses averaged over batches) — the bookkeeping of
 gnn_train.py:154-207 / :258-275."""
 import pandas as pd
@@ -68,14 +68,17 @@ def test_harness_end_to_end(tmp_path):
                                        message_passing_steps=3, latent_size=128, output_nodes_features_size=3,
                                        **{k: v.to(dev()) for k, v in tr_ds.stats().items()}).to(dev())
     t = Trainer(model, lr=1e-3, divergence=True, divergence_penalty=10.0)
+    # the reference's loaders (gnn_train.py:387-394) and print_model's extra iterator (models.py:38)
+    tl = torch.utils.data.DataLoader(range(5), batch_size=2, shuffle=True, collate_fn=list)
+    vl = torch.utils.data.DataLoader(range(3), batch_size=2, shuffle=False, collate_fn=list)
+    next(iter(tl))
     for epoch in range(3):
-        order = list(torch.utils.data.RandomSampler(range(5)))
-        tot = [float(t.step(store.batch(order[i:i + 2]))["total"]) for i in range(0, 5, 2)]
+        tot = [float(t.step(store.batch(idx))["total"]) for idx in tl]
         assert abs(sum(tot) / len(tot) - tr_losses[epoch]) <= 1e-6 * abs(tr_losses[epoch])
         with torch.no_grad():
             te = []
-            for i in range(0, 3, 2):
-                b = tstore.batch(list(range(i, min(i + 2, 3))))
+            for idx in vl:
+                b = tstore.batch(idx)
                 pred = model(b, scale_output=False).local_stress
                 gt = ((b.local_stress - model.mean_local_stress) / model.std_local_stress).float().contiguous()
                 te.append(float(losses.batch_loss(pred, b, gt, divergence=True, divergence_penalty=1.0)[0]))

@@ -78,3 +78,30 @@ def test_shard_graphs_balanced_and_deterministic():
     assert sh == shard_graphs(counts, 3)
     with pytest.raises(ValueError):
         shard_graphs(counts, 0)
+
+
+def test_kernel_variants_need_explicit_ab_opt_in(monkeypatch):
+    """Kernel selection is not taken from a stray environment variable: the
+    shipped defaults unless PDG_AB=1; a non-default value without it is refused, malformed values
+    always are, explicit overrides (tests, tools) are validated by name."""
+    import pytest
+    from pdg.engine import VARIANTS, kernel_variants
+    for _, (env, _) in VARIANTS.items():
+        monkeypatch.delenv(env, raising=False)
+    monkeypatch.delenv("PDG_AB", raising=False)
+    base = kernel_variants()
+    assert base == {k: d for k, (_, d) in VARIANTS.items()}
+    monkeypatch.setenv("PDG_FUSED_EDGE_WGRAD", "1")          # equal to the default: allowed
+    assert kernel_variants() == base
+    monkeypatch.setenv("PDG_FUSED_EDGE_WGRAD", "0")
+    with pytest.raises(RuntimeError, match="PDG_AB=1"):
+        kernel_variants()
+    monkeypatch.setenv("PDG_AB", "1")
+    assert kernel_variants()["fused_edge_wgrad"] is False
+    monkeypatch.setenv("PDG_PAIR_BLOCKS_PER_CU", "x")
+    with pytest.raises(ValueError):
+        kernel_variants()
+    monkeypatch.delenv("PDG_PAIR_BLOCKS_PER_CU")
+    assert kernel_variants({"nbwd_coop": False})["nbwd_coop"] is False
+    with pytest.raises(KeyError):
+        kernel_variants({"no_such_variant": 1})

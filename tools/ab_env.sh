@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out/$TAG"
 for rep in 1 2; do
 for e in "$@"; do
-  env $e timeout -k 10 300 python "$R/bench.py" --no-cpu-baseline --no-extras --steps 30 > "$R/gpurun_out/$TAG/x.log" 2>&1 || { echo "$e failed"; tail -5 "$R/gpurun_out/$TAG/x.log"; exit 1; }
+  env PDG_AB=1 $e timeout -k 10 300 python "$R/bench.py" --no-cpu-baseline --no-extras --steps 30 > "$R/gpurun_out/$TAG/x.log" 2>&1 || { echo "$e failed"; tail -5 "$R/gpurun_out/$TAG/x.log"; exit 1; }
   python -c "
 import json,sys
 d=json.loads([l for l in open('$R/gpurun_out/$TAG/x.log') if l.startswith('{')][-1])

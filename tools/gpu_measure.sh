@@ -38,9 +38,10 @@ if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
   cd "$R"
-  python tools/prof_summary.py "$O/prof/bench_kernel_stats.csv" 7 > "$O/prof_summary.txt"
+  TREE=$(python -c "import bench; print(bench.tree_hash())")
+  { echo "tree $TREE"; python tools/prof_summary.py "$O/prof/bench_kernel_stats.csv" 7; } > "$O/prof_summary.txt"
   python tools/pmc_summary.py "$O/pmc_fetch/bench_counter_collection.csv" \
-    "$O/pmc_write/bench_counter_collection.csv" --json "$O/pmc_traffic.json" > "$O/pmc_traffic.txt"
+    "$O/pmc_write/bench_counter_collection.csv" --json "$O/pmc_traffic.json" --tree "$TREE" > "$O/pmc_traffic.txt"
   rm -f "$O"/prof/*kernel_trace.csv "$O"/*/*.db
   cat "$O/prof_summary.txt" "$O/pmc_traffic.txt"
 fi

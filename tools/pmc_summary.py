@@ -24,6 +24,11 @@ def load(path, counter):
 
 def main(argv):
     out_json = None
+    meta = {}
+    if "--tree" in argv:        # tree hash of the measured sources (bench.tree_hash), stored under "_meta"
+        i = argv.index("--tree")
+        meta["tree"] = argv[i + 1]
+        argv = argv[:i] + argv[i + 2:]
     if "--json" in argv:
         i = argv.index("--json")
         out_json = argv[i + 1]
@@ -37,8 +42,10 @@ def main(argv):
         n = max(fetch.get(k, (0, 0))[1], write.get(k, (0, 0))[1])
         res[k] = {"read": f, "write": w, "total": f + w, "dispatches": n}
         print(f"{k[:70]:70s} read {f/1e6:10.1f} MB  write {w/1e6:10.1f} MB  total {(f+w)/1e6:10.1f} MB")
+    if meta:
+        print(f"tree {meta['tree']}")
     if out_json:
-        json.dump(res, open(out_json, "w"), indent=1)
+        json.dump({**({"_meta": meta} if meta else {}), **res}, open(out_json, "w"), indent=1)
 
 
 if __name__ == "__main__":

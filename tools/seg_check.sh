@@ -13,7 +13,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 tail -2 "$O/model.log"
 for c in 2 5; do
 for e in PDG_SEG_SUMS_TRAIN=0 PDG_SEG_SUMS_TRAIN=1 PDG_SEG_SUMS=0 PDG_SEG_SUMS=1; do
-  env $e timeout -k 10 300 python "$R/bench.py" --no-cpu-baseline --no-extras --steps 30 --config $c > "$O/x.log" 2>&1 || { echo "$e failed"; tail -5 "$O/x.log"; exit 1; }
+  env PDG_AB=1 $e timeout -k 10 300 python "$R/bench.py" --no-cpu-baseline --no-extras --steps 30 --config $c > "$O/x.log" 2>&1 || { echo "$e failed"; tail -5 "$O/x.log"; exit 1; }
   python -c "
 import json
 d=json.loads([l for l in open('$O/x.log') if l.startswith('{')][-1])
