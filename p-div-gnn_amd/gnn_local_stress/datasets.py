@@ -38,12 +38,18 @@ class NodeType(IntEnum):
 
 
 def mesh_to_graph(points: np.ndarray, faces: np.ndarray) -> Data:
-    """convert_utils.py:47-60 for triangle meshes: pos = points, undirected coalesced edges."""
-    if faces.shape[1] != 3:
-        raise ValueError("only triangle meshes are supported (quad meshes: convert_utils.py:63-80)")
+    """convert_utils.py:47-60: pos = points, undirected coalesced edges of the cells -- PyG
+    ``FaceToEdge`` for triangles, ``_quad_face_to_edge`` (:63-81) for quads (the reference decides by
+    the first cell's type; the VTK reader refuses mixed cell sizes)."""
     n = len(points)
+    if faces.shape[1] == 3:
+        ei = meshgen.faces_to_edges(faces, n)
+    elif faces.shape[1] == 4:
+        ei = meshgen.quad_faces_to_edges(faces, n)
+    else:
+        raise ValueError(f"cells with {faces.shape[1]} vertices: only triangle and quad meshes are supported")
     return Data(pos=torch.from_numpy(np.ascontiguousarray(points)),
-                edge_index=torch.from_numpy(meshgen.faces_to_edges(faces, n)),
+                edge_index=torch.from_numpy(ei),
                 face=torch.from_numpy(np.ascontiguousarray(faces.T)))
 
 
@@ -87,10 +93,10 @@ def load_sample(mesh_filename: str | Path, data_filename: str | Path, periodic_g
     the reference takes the lengths in fp64 and rounds them: within 1 ulp) and the sample's
     tensors stay on the host until the caller moves them."""
     points, faces = read_legacy_vtk(mesh_filename)
-    if device is not None and torch.device(device).type == "cuda":
+    # the device graph builder (pdg_mesh_graph) takes triangles; quad meshes (convert_utils.py:63-81,
+    # not used by the reference's datasets) are built by the host restatement below on any device
+    if device is not None and torch.device(device).type == "cuda" and faces.shape[1] == 3:
         from pdg.devgraph import mesh_graph
-        if faces.shape[1] != 3:
-            raise ValueError("only triangle meshes are supported (quad meshes: convert_utils.py:63-80)")
         ei, ea = mesh_graph(torch.from_numpy(np.ascontiguousarray(points, np.float32)).to(device),
                             torch.from_numpy(np.ascontiguousarray(faces, np.int64)).to(device), periodic_graph)
         graph = Data(pos=torch.from_numpy(np.ascontiguousarray(points)), edge_index=ei.cpu(), edge_attr=ea.cpu(),

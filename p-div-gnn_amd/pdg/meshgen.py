@@ -93,6 +93,15 @@ def faces_to_edges(faces: np.ndarray, num_nodes: int) -> np.ndarray:
     return ei
 
 
+def quad_faces_to_edges(faces: np.ndarray, num_nodes: int) -> np.ndarray:
+    """convert_utils.py:63-81 (``_quad_face_to_edge``): the four sides (f0,f1), (f1,f2), (f2,f3),
+    (f0,f3) of every quad, made undirected and coalesced (PyG ``to_undirected``)."""
+    e = np.concatenate([faces[:, [0, 1]], faces[:, [1, 2]], faces[:, [2, 3]], faces[:, [0, 3]]], 0).T
+    e = np.concatenate([e, e[::-1]], 1)
+    ei, _ = coalesce(e, None, num_nodes)
+    return ei
+
+
 def edge_lengths(pos: np.ndarray, edge_index: np.ndarray) -> np.ndarray:
     """Euclidean edge length in float32, computed as datasets.py:182-188 does."""
     import torch

@@ -116,3 +116,41 @@ def test_inference_output_files(tmp_path):
             exp = ds.graphs[i].pos.sum(1, keepdim=True).repeat(1, 3).numpy()
             assert np.array_equal(f["stress_field"], exp)
             assert np.array_equal(f["op_div_matrix_data"], org["op_div_matrix_data"])
+
+
+def test_quad_mesh_graph(tmp_path):
+    """convert_utils.py:63-81: a quad mesh's graph has the four sides of every cell, undirected and
+    coalesced -- checked on a hand-built 3 x 2-cell grid against the grid's own neighbour pairs, then
+    through a VTK file and the dataset's periodic construction."""
+    nx, ny = 4, 3                                  # nodes per row / column
+    pts = np.array([[x * 10.0, y * 7.0, 0.0] for y in range(ny) for x in range(nx)], np.float32)
+    quads = np.array([[y * nx + x, y * nx + x + 1, (y + 1) * nx + x + 1, (y + 1) * nx + x]
+                      for y in range(ny - 1) for x in range(nx - 1)], np.int64)
+    g = datasets.mesh_to_graph(pts, quads)
+    want = set()
+    for y in range(ny):
+        for x in range(nx):
+            v = y * nx + x
+            if x + 1 < nx:
+                want |= {(v, v + 1), (v + 1, v)}
+            if y + 1 < ny:
+                want |= {(v, v + nx), (v + nx, v)}
+    ei = g.edge_index.numpy()
+    assert set(map(tuple, ei.T.tolist())) == want and ei.shape[1] == len(want)   # no diagonals, no duplicates
+    key = ei[0] * len(pts) + ei[1]
+    assert np.all(np.diff(key) > 0)                 # coalesced: sorted by (row, col)
+    # through the VTK reader (cell type 9) and the periodic dataset construction
+    p = tmp_path / "q.vtk"
+    vtk_io.write_legacy_vtk(p, pts, quads)
+    pts2, faces2 = vtk_io.read_legacy_vtk(p)
+    assert faces2.shape == (6, 4)
+    g2 = datasets.mesh_to_graph(pts2, faces2)
+    assert np.array_equal(g2.edge_index.numpy(), ei)
+    g2.edge_attr = datasets.compute_node_distances_as_edge_weights(g2).float()
+    lengths = dict(zip(map(tuple, ei.T.tolist()), g2.edge_attr.numpy().tolist()))
+    assert lengths[(0, 1)] == 10.0 and lengths[(0, nx)] == 7.0
+    gp = datasets.compute_periodic_graph(g2)
+    assert gp.edge_index.shape[1] > ei.shape[1]     # periodic pairs added with zero length
+    assert float(gp.edge_attr[gp.edge_attr == 0].sum()) == 0.0 and int((gp.edge_attr == 0).sum()) > 0
+    with pytest.raises(ValueError):
+        datasets.mesh_to_graph(pts, quads[:, :2])

@@ -158,10 +158,8 @@ def test_zero_mean_stress_batch_skips_update():
     tr, batch = _setup(divergence=True)
     tr.step(batch)
     torch.cuda.synchronize()
-    zero = batch.clone() if hasattr(batch, "clone") else None
-    if zero is None:
-        import copy
-        zero = copy.copy(batch)
+    import copy
+    zero = copy.copy(batch)                   # same graph, its own attribute dict
     zero.mean_stress = torch.zeros_like(batch.mean_stress)
     before = (tr.flat_p.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(), tr.step_count)
     out = tr.step(zero)
