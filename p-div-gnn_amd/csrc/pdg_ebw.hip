@@ -20,10 +20,9 @@
 // read-modified-written once at the end, so slabs accumulate over the steps of a
 // backward pass and are reduced once by pdg_wgrad_reduce (deterministic).
 //
-// Per 32-row round: stage (loads -> LN backward / split -> images) | barrier | next
-// round's loads issued | weight-gradient MFMAs | activation MFMAs | stores | barrier.
-// Every load of a round is issued before the previous round's stores (vmcnt counts
-// loads and stores together, in issue order).
+// Per round: stage (loads -> LN backward / split -> images) | loads of a later round issued |
+// barrier | weight-gradient MFMAs | activation MFMAs | stores.  Every load of a round is issued
+// before the previous round's stores (vmcnt counts loads and stores together, in issue order).
 #include "pdg_common.hpp"
 #include "pdg_runtime.hpp"
 #include "pdg_x6.hpp"
@@ -52,15 +51,22 @@ constexpr int WSLAB = L * L + L;            // floats per slab (weight + bias su
 // pdg_edge_bwd_w2 the three extra tiles measured +2 % and are not used.
 constexpr int OT_STRIDE = L + 4;
 
-// Columns 4cg .. 4cg+3 of image row r, split into the three terms.
+// 16-row images (pdg_edge_bwd_w2's two-round register pipeline): term planes of 16 rows
+constexpr int R16 = 16;
+constexpr int T16 = R16 * X6_ROWB;          // bytes per term plane (4 KB)
+constexpr int IMG16 = 3 * T16;              // one bf16x6 image of 16 rows (12 KB)
+constexpr int MSK16 = R16 * MSK_STRIDE;
+
+// Columns 4cg .. 4cg+3 of image row r, split into the three terms (term planes TERM bytes apart).
+template <int TERM = X6_TERM>
 __device__ __forceinline__ void img_store4(unsigned char* img, int r, int cg, const f32x4& v) {
   unsigned h0, m0, l0, h1, m1, l1;
   split3_pair(v[0], v[1], h0, m0, l0);
   split3_pair(v[2], v[3], h1, m1, l1);
   const int off = x6_addr(r, 8 * cg);
   *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
-  *reinterpret_cast<u32x2*>(img + X6_TERM + off) = u32x2{m0, m1};
-  *reinterpret_cast<u32x2*>(img + 2 * X6_TERM + off) = u32x2{l0, l1};
+  *reinterpret_cast<u32x2*>(img + TERM + off) = u32x2{m0, m1};
+  *reinterpret_cast<u32x2*>(img + 2 * TERM + off) = u32x2{l0, l1};
 }
 
 __device__ __forceinline__ unsigned relu_mask4(const f32x4& a) {
@@ -83,23 +89,25 @@ __device__ __forceinline__ f32x4 ln_relu_bwd4(const f32x4& gy, const f32x4& a2, 
 
 // slab += G^T X over the 32 staged rows (K = rows): wave w owns o in 32 (w & 3) + [0, 32),
 // i in 64 (w >> 2) + [0, 64) as two 32x32 accumulators (wgrad_x6_kernel's operand reads).
+// KS 16-row K steps per call (2: a 32-row image, 1: a 16-row one, term planes TERM bytes apart).
+template <int KS = 2, int TERM = X6_TERM>
 __device__ __forceinline__ void wgrad_round(f32x16 (&acc)[2], const unsigned char* gimg, const unsigned char* ximg) {
   const int l = lane_id(), w = wave_id(), h = l >> 5;
   const int ob = 32 * (w & 3), ib = 64 * (w >> 2);
   const int lrow = 8 * h + ((l & 15) >> 2);
   const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
+  for (int ks = 0; ks < KS; ++ks) {
     const int row = 16 * ks + lrow;
     bf16x8 A[3], B[2][3];
     const int g0 = x6_addr(row, lcolb + 2 * ob), g1 = x6_addr(row + 4, lcolb + 2 * ob);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) A[p] = x6_operand(gimg + p * X6_TERM, g0, g1);
+    for (int p = 0; p < 3; ++p) A[p] = x6_operand(gimg + p * TERM, g0, g1);
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int x0 = x6_addr(row, lcolb + 2 * (ib + 32 * b)), x1 = x6_addr(row + 4, lcolb + 2 * (ib + 32 * b));
 #pragma unroll
-      for (int p = 0; p < 3; ++p) B[b][p] = x6_operand(ximg + p * X6_TERM, x0, x1);
+      for (int p = 0; p < 3; ++p) B[b][p] = x6_operand(ximg + p * TERM, x0, x1);
     }
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
@@ -116,23 +124,23 @@ __device__ __forceinline__ void wgrad_round(f32x16 (&acc)[2], const unsigned cha
 
 // d[nb] = (W^T-slice x image rows 16 nb .. 16 nb + 15): D row = output feature 16w + 4(l >> 4) + j,
 // column = staged row 16 nb + (l & 15).  NI images share the weight operands.
-template <int NI>
-__device__ __forceinline__ void gemm_round(f32x4 (&d)[NI][2], const WSlice& ws, const unsigned char* const (&img)[NI]) {
+template <int NI, int NB = 2, int TERM = X6_TERM>
+__device__ __forceinline__ void gemm_round(f32x4 (&d)[NI][NB], const WSlice& ws, const unsigned char* const (&img)[NI]) {
   const int l = lane_id(), n = l & 15, kg = l >> 4;
 #pragma unroll
   for (int u = 0; u < NI; ++u)
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) d[u][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nb = 0; nb < NB; ++nb) d[u][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
     for (int u = 0; u < NI; ++u)
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
+      for (int nb = 0; nb < NB; ++nb) {
         const int off = x6_addr(16 * nb + n, 64 * ks + 16 * kg);
         bf16x8 B[3];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(img[u] + p * X6_TERM + off);
+        for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(img[u] + p * TERM + off);
         f32x4 t = d[u][nb];
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][2], B[0], t, 0, 0, 0);
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][1], B[1], t, 0, 0, 0);
@@ -191,9 +199,31 @@ __device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const 
 
 __device__ __forceinline__ int clamp_row(int r, int r1) { return r < r1 ? r : r1 - 1; }
 
+// Buffer resource over rows [r0, r1) of a (rows, 128) fp32 array: stores past row r1 fall outside
+// num_records and are dropped by the hardware range check (no branch around them).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int r0, int r1) {
+  return __builtin_amdgcn_make_buffer_rsrc(base + (size_t)r0 * L, (short)0, (r1 - r0) * L * 4, 0x00020000);
+}
+// 16-byte store of columns c .. c+3 of block-relative row r (dropped when r is past the range).
+__device__ __forceinline__ void rows_store4(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, 0);
+}
+
+
 }  // namespace
 
 // ============================================================================ W2 path
+// 16-row rounds with TWO rounds of row loads in flight, in the registers one 32-row round used to
+// take (two sets of one row per thread): set s is consumed by the stage of round n and re-issued for
+// round n + 2 at once, so a CU always has rows landing while it computes.  (The round-2 kernel staged
+// 32-row rounds and issued the next round's loads after the stage's barrier, with no loads in flight
+// between their arrival and the next issue: 219-221 -> 190-196 us per config-2 call, 1,039 MB of DRAM
+// traffic at 5.4 instead of 4.7 TB/s, same box.)  The images and masks are double-buffered by round
+// parity, which leaves one barrier per round.  No memory operation is conditional (rows past the
+// block's end are clamped on load and range-dropped on store): a load or store skipped on some path
+// made the compiler's loop-carried count collapse to vmcnt(0) in the stage, a wait for both sets.
+// gz1m / gz1e / gC are bitwise those of the 32-row kernel; dW2 sums the same products in another
+// order (message and edge-update rows of a round interleave per 16 rows instead of per 32).
 template <bool EU>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
@@ -204,14 +234,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     float* __restrict__ slabs, int E, const double* __restrict__ pm, int npm, const double* __restrict__ pe,
     int npe) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  unsigned char* img_gm = sm;                                  // gz2m
-  unsigned char* img_am = sm + EBW_IMG;                        // a1m
-  unsigned char* img_ge = sm + 2 * EBW_IMG;                    // gz2e (EU)
-  unsigned char* img_ae = sm + 3 * EBW_IMG;                    // a1e (EU)
-  unsigned char* msk_m = sm + (EU ? 4 : 2) * EBW_IMG;          // [a1m > 0]
-  unsigned char* msk_e = msk_m + EBW_MASK;                     // [a1e > 0] (EU)
+  constexpr int NIMG = EU ? 4 : 2, NMSK = EU ? 2 : 1;
+  constexpr int BUF = NIMG * IMG16 + NMSK * MSK16;           // one round's images + masks
   const int l = lane_id(), w = wave_id();
-  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;    // the thread's staged row: rg (0..15)
+  const int oc = 16 * w + 4 * (l >> 4);
   int r0, r1;
   block_rows(E, r0, r1);
   WSlice ws;
@@ -224,101 +251,104 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
   f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  // prefetched rows of the next round: thread rows rg and rg + 16, columns 4cg .. 4cg+3
+  // two register sets of prefetched rows (round parity), and the dst id each set gathers next
   f32x4 pg[2], pa2[2], pa1[2], pge[2], pa2e[2], pa1e[2];
-  int dnext[2] = {0, 0};
-  auto issue = [&](int base, const int (&dn)[2]) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
-      pg[u] = *reinterpret_cast<const f32x4*>(gaggr + (size_t)dn[u] * L + 4 * cg);
-      pa2[u] = *reinterpret_cast<const f32x4*>(a2m + rc);
-      pa1[u] = *reinterpret_cast<const f32x4*>(a1m + rc);
-      if (EU) {
-        pge[u] = *reinterpret_cast<const f32x4*>(ge_next + rc);
-        pa2e[u] = *reinterpret_cast<const f32x4*>(a2e + rc);
-        pa1e[u] = *reinterpret_cast<const f32x4*>(a1e + rc);
-      }
+  int dn[2];
+  auto issue = [&](int s, int base) {
+    const size_t rc = (size_t)clamp_row(base + rg, r1) * L + 4 * cg;
+    pg[s] = *reinterpret_cast<const f32x4*>(gaggr + (size_t)dn[s] * L + 4 * cg);
+    pa2[s] = *reinterpret_cast<const f32x4*>(a2m + rc);
+    pa1[s] = *reinterpret_cast<const f32x4*>(a1m + rc);
+    if (EU) {
+      pge[s] = *reinterpret_cast<const f32x4*>(ge_next + rc);
+      pa2e[s] = *reinterpret_cast<const f32x4*>(a2e + rc);
+      pa1e[s] = *reinterpret_cast<const f32x4*>(a1e + rc);
     }
   };
-  if (r0 < r1) {
-    int d0[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      d0[u] = dst[clamp_row(r0 + rg + 16 * u, r1)];
-      dnext[u] = dst[clamp_row(r0 + X6_ROWS + rg + 16 * u, r1)];
-    }
-    issue(r0, d0);
-  }
-  // the weights and the LayerNorm scalars after the first round's row loads: the round trips overlap
+  // no memory operation below is conditional (rows past the block's end are clamped on load and
+  // dropped by the buffer range check on store), so the compiler can count the loads in flight: a
+  // skipped store or load on some path made it wait for all of them (vmcnt(0)) in the stage
+  const __amdgpu_buffer_rsrc_t out_m = rows_rsrc(gz1m, r0, r1), out_c = rows_rsrc(gC, r0, r1);
+  const __amdgpu_buffer_rsrc_t out_e = rows_rsrc(EU ? gz1e : gz1m, r0, r1);
+  dn[0] = dst[clamp_row(r0 + rg, r1)];   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
+  dn[1] = dst[clamp_row(r0 + R16 + rg, r1)];
+  // each set's loads strictly before the next set's (sched_barrier), in the order the loop re-issues
+  // them: the loop waits for one set by count, and an interleaved prologue lowers that count
+  issue(0, r0);
+  dn[0] = dst[clamp_row(r0 + 2 * R16 + rg, r1)];
+  __builtin_amdgcn_sched_barrier(0);
+  issue(1, r0 + R16);
+  dn[1] = dst[clamp_row(r0 + 3 * R16 + rg, r1)];
+  __builtin_amdgcn_sched_barrier(0);
+  // the weights and the LayerNorm scalars after the first rounds' row loads: the round trips overlap
   load_wslice(ws, W2T, w);
   const pdg_ln_bwd lbm = lnb_resolve(lbm_p, pm, npm, stm_p);
   const pdg_ln_bwd lbe = EU ? lnb_resolve(lbe_p, pe, npe, ste_p) : lbm;
-  for (int base = r0; base < r1; base += X6_ROWS) {
-    // ---- stage: gz2 (LN + relu backward), a1 and its relu mask into the images
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int r = rg + 16 * u;
-      const bool ok = base + r < r1;
+  auto round = [&](const int s, const int base) {
+    unsigned char* img_gm = sm + s * BUF;                      // gz2m
+    unsigned char* img_am = img_gm + IMG16;                    // a1m
+    unsigned char* img_ge = img_gm + 2 * IMG16;                // gz2e (EU)
+    unsigned char* img_ae = img_gm + 3 * IMG16;                // a1e (EU)
+    unsigned char* msk_m = img_gm + NIMG * IMG16;              // [a1m > 0]
+    unsigned char* msk_e = msk_m + MSK16;                      // [a1e > 0] (EU)
+    // ---- stage: gz2 (LN + relu backward), a1 and its relu mask into this round's images
+    {
+      const bool ok = base + rg < r1;
       const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 zm = ok ? ln_relu_bwd4(pg[u], pa2[u], stm, lbm, g4) : zero;
-      const f32x4 am = ok ? pa1[u] : zero;
+      const f32x4 zm = ok ? ln_relu_bwd4(pg[s], pa2[s], stm, lbm, g4) : zero;
+      const f32x4 am = ok ? pa1[s] : zero;
       bsum += zm;
-      img_store4(img_gm, r, cg, zm);
-      img_store4(img_am, r, cg, am);
-      *reinterpret_cast<unsigned*>(msk_m + r * MSK_STRIDE + 4 * cg) = relu_mask4(am);
+      img_store4<T16>(img_gm, rg, cg, zm);
+      img_store4<T16>(img_am, rg, cg, am);
+      *reinterpret_cast<unsigned*>(msk_m + rg * MSK_STRIDE + 4 * cg) = relu_mask4(am);
       if (EU) {
-        const f32x4 ze = ok ? ln_relu_bwd4(pge[u], pa2e[u], ste, lbe, g4) : zero;
-        const f32x4 ae = ok ? pa1e[u] : zero;
+        const f32x4 ze = ok ? ln_relu_bwd4(pge[s], pa2e[s], ste, lbe, g4) : zero;
+        const f32x4 ae = ok ? pa1e[s] : zero;
         bsum += ze;
-        img_store4(img_ge, r, cg, ze);
-        img_store4(img_ae, r, cg, ae);
-        *reinterpret_cast<unsigned*>(msk_e + r * MSK_STRIDE + 4 * cg) = relu_mask4(ae);
+        img_store4<T16>(img_ge, rg, cg, ze);
+        img_store4<T16>(img_ae, rg, cg, ae);
+        *reinterpret_cast<unsigned*>(msk_e + rg * MSK_STRIDE + 4 * cg) = relu_mask4(ae);
       }
     }
-    __syncthreads();
-    // ---- next round's loads, ahead of this round's stores
-    if (base + X6_ROWS < r1) {
-      const int dcur[2] = {dnext[0], dnext[1]};
-#pragma unroll
-      for (int u = 0; u < 2; ++u) dnext[u] = dst[clamp_row(base + 2 * X6_ROWS + rg + 16 * u, r1)];
-      issue(base + X6_ROWS, dcur);
-    }
+    // ---- the set is free: its rows of the round after next, then the dst ids of the one after that
+    issue(s, base + 2 * R16);
+    dn[s] = dst[clamp_row(base + 4 * R16 + rg, r1)];
+    __syncthreads();   // this round's images complete (the other buffer is the previous round's)
     // ---- dW2 += gz2m^T a1m (+ gz2e^T a1e)
-    wgrad_round(acc, img_gm, img_am);
-    if (EU) wgrad_round(acc, img_ge, img_ae);
+    wgrad_round<1, T16>(acc, img_gm, img_am);
+    if (EU) wgrad_round<1, T16>(acc, img_ge, img_ae);
     // ---- gz1 = (W2^T gz2) [a1 > 0], gC = gz1m + gz1e
     constexpr int NI = EU ? 2 : 1;
-    f32x4 d[NI][2];
+    f32x4 d[NI][1];
     const unsigned char* imgs[NI];
     imgs[0] = img_gm;
     if (EU) imgs[NI - 1] = img_ge;
-    gemm_round<NI>(d, ws, imgs);
-    const int oc = 16 * w + 4 * (l >> 4);
+    gemm_round<NI, 1, T16>(d, ws, imgs);
+    const int r = l & 15;
+    const int row = base + r;
+    const unsigned mm = *reinterpret_cast<const unsigned*>(msk_m + r * MSK_STRIDE + oc);
+    f32x4 zm;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int r = 16 * nb + (l & 15);
-      const int row = base + r;
-      const unsigned mm = *reinterpret_cast<const unsigned*>(msk_m + r * MSK_STRIDE + oc);
-      f32x4 zm;
+    for (int j = 0; j < 4; ++j) zm[j] = (mm >> (8 * j)) & 1u ? d[0][0][j] : 0.f;
+    f32x4 c = zm;
+    if (EU) {
+      const unsigned me = *reinterpret_cast<const unsigned*>(msk_e + r * MSK_STRIDE + oc);
+      f32x4 ze;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) zm[j] = (mm >> (8 * j)) & 1u ? d[0][nb][j] : 0.f;
-      f32x4 c = zm;
-      if (EU) {
-        const unsigned me = *reinterpret_cast<const unsigned*>(msk_e + r * MSK_STRIDE + oc);
-        f32x4 ze;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ze[j] = (me >> (8 * j)) & 1u ? d[NI - 1][nb][j] : 0.f;
-        c = zm + ze;
-        if (row < r1) stg4(gz1e + (size_t)row * L + oc, ze);
-      }
-      if (row < r1) {
-        stg4(gz1m + (size_t)row * L + oc, zm);
-        stg4(gC + (size_t)row * L + oc, c);
-      }
+      for (int j = 0; j < 4; ++j) ze[j] = (me >> (8 * j)) & 1u ? d[NI - 1][0][j] : 0.f;
+      c = zm + ze;
+      rows_store4(out_e, row - r0, oc, ze);
     }
-    __syncthreads();   // the images are rewritten by the next round
+    rows_store4(out_m, row - r0, oc, zm);
+    rows_store4(out_c, row - r0, oc, c);
+  };
+  // both rounds of a 32-row step always run: a round past r1 stages zero rows (adding exact zeros to
+  // the weight gradient) and stores nothing
+  for (int base = r0; base < r1; base += 2 * R16) {
+    round(0, base);
+    round(1, base + R16);
   }
+  __syncthreads();   // the last rounds' image reads precede the LDS reuse below
   slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
 }
 
@@ -1405,7 +1435,8 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
   PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && gz1e && st_e && (lb_e || pairs_e) && PDG_ALIGNED(a2e) &&
                         PDG_ALIGNED(a1e) && PDG_ALIGNED(gz1e)),
                 "pdg_edge_bwd_w2: edge-update arguments missing or misaligned");
-  const size_t shm = eu ? 4 * EBW_IMG + 2 * EBW_MASK : 2 * EBW_IMG + EBW_MASK;
+  // 16-row rounds, two rounds of loads in flight (edge_bwd_w2_kernel): two buffers of images + masks
+  const size_t shm = eu ? 2 * (4 * IMG16 + 2 * MSK16) : 2 * (2 * IMG16 + MSK16);
   if (eu)
     hipLaunchKernelGGL(edge_bwd_w2_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, dst,
                        gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, gz1m, gz1e, gC, slabs,
