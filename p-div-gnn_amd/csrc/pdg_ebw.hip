@@ -199,14 +199,26 @@ __device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const 
 
 __device__ __forceinline__ int clamp_row(int r, int r1) { return r < r1 ? r : r1 - 1; }
 
+// An empty asm that reads x: its load has completed here, and cannot be sunk past this point.
+template <class T>
+__device__ __forceinline__ void pin_vgpr(const T& x) {
+  asm volatile("" ::"v"(x));
+}
+
 // Buffer resource over rows [r0, r1) of a (rows, 128) fp32 array: stores past row r1 fall outside
-// num_records and are dropped by the hardware range check (no branch around them).
+// num_records and are dropped by the hardware range check (no branch around them).  A null array
+// gets an empty range (every store dropped).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int r0, int r1) {
-  return __builtin_amdgcn_make_buffer_rsrc(base + (size_t)r0 * L, (short)0, (r1 - r0) * L * 4, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(base ? base + (size_t)r0 * L : nullptr, (short)0,
+                                           base ? (r1 - r0) * L * 4 : 0, 0x00020000);
 }
 // 16-byte store of columns c .. c+3 of block-relative row r (dropped when r is past the range).
 __device__ __forceinline__ void rows_store4(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, 0);
+}
+// The same, nontemporal (aux nt: the policy of stnt4 / PDG_NT_ST).
+__device__ __forceinline__ void rows_store4_nt(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, PDG_NT_ST ? 2 : 0);
 }
 
 
@@ -673,6 +685,15 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
   f32x4 xa[2], xr[2];
   int dq[2], sq[2];
+  // the row outputs through range-checked buffer stores: no memory operation of the loop is
+  // conditional, so the compiler's vmcnt counts stay exact (a store skipped on some path made them
+  // collapse).  An omitted output (a1m / a1e in inference, a2m beside the inference sums) gets an
+  // empty range: its stores are issued and dropped.
+  const __amdgpu_buffer_rsrc_t rs_e = rows_rsrc(eout, r0, r1);
+  const __amdgpu_buffer_rsrc_t rs_a1m = rows_rsrc(a1m, r0, r1);
+  const __amdgpu_buffer_rsrc_t rs_a1e = rows_rsrc(EU ? a1e : nullptr, r0, r1);
+  const __amdgpu_buffer_rsrc_t rs_a2m = rows_rsrc(a2m, r0, r1);
+  const __amdgpu_buffer_rsrc_t rs_a2e = rows_rsrc(EU ? a2e : nullptr, r0, r1);
   auto issue = [&](int base) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -696,7 +717,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         if (RES) y += xr[u][j];
         e[j] = y;
       }
-      if (ok) stnt4(eout + (size_t)(base + r) * L + 4 * cg, e);
+      rows_store4_nt(rs_e, base + r - r0, 4 * cg, e);
       *reinterpret_cast<f32x4*>(t_e + r * EFC_ES + 4 * cg) = ok ? e : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
@@ -758,22 +779,41 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     }
     prev_last = sdst[nr - 1];
   };
-  if (r0 < r1) issue(r0);
+  issue(r0);   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
   {
     const float* pc = W1 + (size_t)(16 * w + (l & 15)) * (3 * L) + 2 * L + 4 * (l >> 4);
 #pragma unroll
     for (int T = 0; T < 8; ++T) wcf[T] = *reinterpret_cast<const f32x4*>(pc + 16 * T);
   }
   load_wslice(ws2, W2, w);
-  if (r0 < r1) stage(r0);
+  // the loop-invariant weights and biases are in registers before the loop (an empty asm using them
+  // here): left to the compiler, their loads were sunk to the loop's preheader, still in flight at
+  // the loop head, and the count merged there made every round's C product wait for the previous
+  // round's stores (vmcnt 23 .. 16)
+#pragma unroll
+  for (int T = 0; T < 8; ++T) pin_vgpr(wcf[T]);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) pin_vgpr(ws2.a[ks][p]);
+  pin_vgpr(b1o);
+  pin_vgpr(b2o);
+  // and the first round's gather indices (pending at the loop head, they made every round wait for
+  // the previous round's a1 / a2 stores, vmcnt(2))
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    pin_vgpr(dq[u]);
+    pin_vgpr(sq[u]);
+  }
+  stage(r0);
   for (int base = r0; base < r1; base += X6_ROWS) {
     __syncthreads();   // e tile complete
     int dc[2] = {dq[0], dq[1]}, sc[2] = {sq[0], sq[1]};
     const int par = ((base - r0) / X6_ROWS) & 1;
     if (SEG && w == 0 && l < X6_ROWS) sdst0[par * X6_ROWS + l] = dc[l >> 4];   // lane l: row l
-    const bool more = base + X6_ROWS < r1;
-    if (more) issue(base + X6_ROWS);
-    // ---- C = Wc e + b1 and the two first layers at this wave's 16 features
+    // ---- this round's P / Q rows first, then the next round's rows (pinned by sched_barrier): the
+    // gathers are waited for in the C product below, and with the next round's HBM loads issued
+    // ahead of them (vmcnt counts in issue order) every round waited for those too
     f32x4 gpd[2], gqs[2], gps[2], gqd[2];
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
@@ -784,6 +824,10 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         gqd[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)dc[nb] * L + oc);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
+    issue(base + X6_ROWS);   // clamped past r1: unconditional
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- C = Wc e + b1 and the two first layers at this wave's 16 features
     f32x4 d[2];
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {   // the MFMA order of gemm128: step (T, jj) sums inputs 16T + 4k + jj
@@ -815,15 +859,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       }
     }
     __syncthreads();   // a1 images and tiles complete
-    if (a1m) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int r = rg + 16 * u;
-        if (base + r < r1) {
-          stnt4(a1m + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_m + r * OT_STRIDE + 4 * cg));
-          if (EU) stnt4(a1e + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
-        }
-      }
+    for (int u = 0; u < 2; ++u) {   // (dropped without a1m / a1e: the tiles are then not written)
+      const int r = rg + 16 * u;
+      rows_store4_nt(rs_a1m, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_m + r * OT_STRIDE + 4 * cg));
+      if (EU) rows_store4_nt(rs_a1e, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
     }
     // the previous round's sums (the row after its last is this round's row 0)
     if (SEG && base > r0) walk(base - X6_ROWS, par ^ 1, sdst0[par * X6_ROWS], true);
@@ -857,12 +897,10 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
-      if (base + r < r1) {
-        if (a2m) stnt4(a2m + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_a2 + r * OT_STRIDE + 4 * cg));
-        if (EU) stnt4(a2e + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
-      }
+      rows_store4_nt(rs_a2m, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_a2 + r * OT_STRIDE + 4 * cg));
+      if (EU) rows_store4_nt(rs_a2e, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
     }
-    if (more) stage(base + X6_ROWS);   // the e tile was last read before the second barrier
+    stage(base + X6_ROWS);   // past r1: stores dropped, the tile unused; the e tile was last read before the second barrier
   }
   if (SEG && r0 < r1) walk(r0 + (r1 - 1 - r0) / X6_ROWS * X6_ROWS, ((r1 - 1 - r0) / X6_ROWS) & 1, after, false);
   if (SEG && threadIdx.x == 0) {   // the block's partials: head (+ whether it also runs past r1), tail

@@ -134,8 +134,8 @@ def test_training_step_at_baseline_size(config):
     grads = {n: tr.G[n].detach().cpu().clone() for n in tr.G}
     del tr, out
     big = batch.num_edges > 500_000
-    p64, t64, n64, g64 = _oracle(params, stats, batch, cfg["steps"], torch.float64, cfg["divergence"], True, big)
     t0 = time.time()
+    p64, t64, n64, g64 = _oracle(params, stats, batch, cfg["steps"], torch.float64, cfg["divergence"], True, big)
     rec = {"config": config, "nodes": batch.num_nodes, "edges": batch.num_edges, "graphs": batch.num_graphs,
            "internal_boundary_nodes": int((batch.nodes_types == -1).sum()),
            "pred_vs_f64": rel(pred, p64), "loss_vs_f64": abs(total - t64) / abs(t64),
