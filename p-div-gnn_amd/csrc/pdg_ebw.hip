@@ -531,8 +531,18 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd_kernel(
       pe[u] = e_in[rc];
     }
   };
-  if (r0 < r1) issue(r0);
-  for (int base = r0; base < r1; base += X6_ROWS) {
+  // loads unconditional (clamped) and issued before the barrier; the first round's complete before
+  // the loop (pending at the loop head they set every stage's wait to vmcnt(0))
+  issue(r0);   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    pin_vgpr(pg[u]);
+    pin_vgpr(pa2[u]);
+    pin_vgpr(pe[u]);
+  }
+  // the first round peeled off (unconditional: an empty block stages zero rows), so the loop is
+  // entered in its steady state
+  auto round = [&](const int base) {
     const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -549,8 +559,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd_kernel(
       *reinterpret_cast<unsigned*>(msk + r * MSK_STRIDE + 4 * cg) = relu_mask4(a);
       if (cg == 0) ev[r] = ok ? pe[u] : 0.f;
     }
+    issue(base + X6_ROWS);
     __syncthreads();
-    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
     wgrad_round(acc, img_g, img_a);                        // dW2 += gz2^T a1
     f32x4 d[1][2];
     const unsigned char* imgs[1] = {img_g};
@@ -568,7 +578,9 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd_kernel(
       }
     }
     __syncthreads();   // the images are rewritten by the next round
-  }
+  };
+  round(r0);
+  for (int base = r0 + X6_ROWS; base < r1; base += X6_ROWS) round(base);
   slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
   // the 16 lanes holding the same features (different rows): fixed xor butterfly
 #pragma unroll
@@ -963,8 +975,21 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_fwd_kernel(
 #pragma unroll
     for (int u = 0; u < 2; ++u) pe[u] = e_in[clamp_row(base + rg + 16 * u, r1)];
   };
-  if (r0 < r1) issue(r0);
-  for (int base = r0; base < r1; base += X6_ROWS) {
+  // every memory operation of the loop unconditional (clamped loads, range-checked stores: a store
+  // skipped on some path made the stage wait for the previous round's stores), the next round's
+  // inputs issued before the barrier, the first round's and the weights complete before the loop
+  const __amdgpu_buffer_rsrc_t rs_a2 = rows_rsrc(a2, r0, r1);
+  issue(r0);   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
+#pragma unroll
+  for (int u = 0; u < 2; ++u) pin_vgpr(pe[u]);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pin_vgpr(ws2.a[ks][q]);
+  pin_vgpr(b2o);
+  // the first round peeled off (unconditional: an empty block runs it with every store dropped), so
+  // the loop is entered in its steady state: next round's loads, then this round's stores
+  auto round = [&](const int base) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
@@ -973,8 +998,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_fwd_kernel(
       for (int j = 0; j < 4; ++j) a[j] = fmaxf(fmaf(w04[j], pe[u], 0.f) + b04[j], 0.f);
       img_store4(img, r, cg, base + r < r1 ? a : f32x4{0.f, 0.f, 0.f, 0.f});
     }
+    issue(base + X6_ROWS);
     __syncthreads();   // the a1 image is complete
-    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
     f32x4 d[1][2];
     const unsigned char* imgs[1] = {img};
     gemm_round<1>(d, ws2, imgs);
@@ -994,10 +1019,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_fwd_kernel(
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
-      if (base + r < r1)
-        stnt4(a2 + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_a + r * OT_STRIDE + 4 * cg));
+      rows_store4_nt(rs_a2, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_a + r * OT_STRIDE + 4 * cg));
     }
-  }
+  };
+  round(r0);
+  for (int base = r0 + X6_ROWS; base < r1; base += X6_ROWS) round(base);
   double* red = reinterpret_cast<double*>(sm);
   __syncthreads();
   block_sum2(s1, s2, red);
