@@ -22,7 +22,7 @@ step() {  # step NAME SECONDS CMD...
 }
 cd "$R" || exit 1
 if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q || exit 1
+  step pytest_gpu 1150 python -u -m pytest tests -m gpu -x -v --timeout 1100 --timeout-method thread || exit 1
 fi
 if [ "$WHAT" = all ] || [ "$WHAT" = bench ]; then
   step bench2 600 python bench.py || exit 1
