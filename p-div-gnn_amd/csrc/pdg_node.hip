@@ -203,37 +203,27 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_pair_kernel(
     // ---- loader waves: pair p + 2 fetched before the barrier of pair p, stored after it into
     // buffer (p + 2) % 3, last read by layer 1 of pair p - 1 (before the barrier of pair p - 1)
     const int lt = threadIdx.x - 64 * NU_COMPUTE;
-    // two register sets (pair parity): pair p + 3 is fetched before the barrier of pair p and stored
-    // after the barrier of pair p + 1, so its loads have two compute phases to land
-    TileRegs ta[2], tb[2];
+    TileRegs tr[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (nu_tile(2 * k) < ntiles) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) fetch_tile(ta[h], nu_tile(2 * k + h), N, lt, aggr, x);
+        for (int h = 0; h < 2; ++h) fetch_tile(tr[h], nu_tile(2 * k + h), N, lt, aggr, x);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) store_tile(xin + (2 * k + h) * XBUF, lt, ta[h]);
+        for (int h = 0; h < 2; ++h) store_tile(xin + (2 * k + h) * XBUF, lt, tr[h]);
       }
-    if (nu_tile(4) < ntiles) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) fetch_tile(ta[h], nu_tile(4 + h), N, lt, aggr, x);   // pair 2: even set
-    }
     __syncthreads();
-    auto pair = [&](int p, TileRegs (&fset)[2], TileRegs (&sset)[2]) {
-      if (nu_tile(2 * (p + 3)) < ntiles) {
+    for (int p = 0; nu_tile(2 * p) < ntiles; ++p) {
+      const bool ahead = nu_tile(2 * (p + 2)) < ntiles;
+      if (ahead) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) fetch_tile(fset[h], nu_tile(2 * (p + 3) + h), N, lt, aggr, x);
+        for (int h = 0; h < 2; ++h) fetch_tile(tr[h], nu_tile(2 * (p + 2) + h), N, lt, aggr, x);
       }
       __syncthreads();
-      if (nu_tile(2 * (p + 2)) < ntiles) {
+      if (ahead) {
 #pragma unroll
-        for (int h = 0; h < 2; ++h) store_tile(xin + (2 * ((p + 2) % 3) + h) * XBUF, lt, sset[h]);
+        for (int h = 0; h < 2; ++h) store_tile(xin + (2 * ((p + 2) % 3) + h) * XBUF, lt, tr[h]);
       }
-    };
-    for (int p = 0; nu_tile(2 * p) < ntiles; p += 2) {
-      pair(p, tb, ta);                                   // fetch pair p + 3 (odd), store pair p + 2 (even)
-      if (nu_tile(2 * (p + 1)) >= ntiles) break;
-      pair(p + 1, ta, tb);
     }
   } else {
     const int r = l & 15, q = l >> 4;
@@ -575,25 +565,22 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
       wbf[T] = *reinterpret_cast<const f32x4*>(pa + L + 16 * T);
     }
   }
-  // loader register sets by tile parity: tile i + 3 is fetched before the barrier of tile i and
-  // stored after the barrier of tile i + 1 (two compute phases for its loads to land)
-  XtRegs ra, rb;
+  XtRegs rg;
   if (loader) {
 #pragma unroll
     for (int k = 0; k < 2; ++k)
       if (nu_tile(k) < ntiles) {
-        fetch_xt<RES>(ra, nu_tile(k), N, lt, a2p, xres);
-        store_xt<RES>(xt + k * TILE * GS, nu_tile(k), N, lt, ra, st, lg, lb, xout);
+        fetch_xt<RES>(rg, nu_tile(k), N, lt, a2p, xres);
+        store_xt<RES>(xt + k * TILE * GS, nu_tile(k), N, lt, rg, st, lg, lb, xout);
       }
-    if (nu_tile(2) < ntiles) fetch_xt<RES>(ra, nu_tile(2), N, lt, a2p, xres);   // tile 2: even set
   }
   __syncthreads();
-  auto iter = [&](int i, XtRegs& fset, XtRegs& sset) -> bool {
+  for (int i = 0;; ++i) {
     const int tile = nu_tile(i);
-    if (tile >= ntiles) return false;   // uniform across the block
+    if (tile >= ntiles) break;   // uniform across the block
     const bool ahead = nu_tile(i + 2) < ntiles;
     if (loader) {
-      if (nu_tile(i + 3) < ntiles) fetch_xt<RES>(fset, nu_tile(i + 3), N, lt, a2p, xres);
+      if (ahead) fetch_xt<RES>(rg, nu_tile(i + 2), N, lt, a2p, xres);
     } else {
       const int row = tile * TILE + r;
       f32x4 acc_p = {0.f, 0.f, 0.f, 0.f}, acc_q = {0.f, 0.f, 0.f, 0.f};
@@ -614,12 +601,7 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
     }
     __syncthreads();
     if (loader && ahead)   // buffer (i + 2) % 3 was last read in iteration i - 1
-      store_xt<RES>(xt + ((i + 2) % 3) * TILE * GS, nu_tile(i + 2), N, lt, sset, st, lg, lb, xout);
-    return true;
-  };
-  for (int i = 0;; i += 2) {
-    if (!iter(i, rb, ra)) break;       // fetch tile i + 3 (odd), store tile i + 2 (even)
-    if (!iter(i + 1, ra, rb)) break;
+      store_xt<RES>(xt + ((i + 2) % 3) * TILE * GS, nu_tile(i + 2), N, lt, rg, st, lg, lb, xout);
   }
 }
 
