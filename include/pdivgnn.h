@@ -274,6 +274,15 @@ int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, 
                       const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                       const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                       double* part_e, int with_edge_update, int nblocks, void* stream);
+/* pdg_edge_fwd_coop for training with a backward that recomputes the first layers
+ * (pdg_edge_bwd_w2_rc): instead of a1m and a1e it stores c_out = Wc e + b1 (E x 128, b1 added), from
+ * which a1m = relu((c_out + P[dst]) + Q[src]) and a1e = relu((c_out + P[src]) + Q[dst]) follow bit for
+ * bit (models.py:219-222, :233-238 with W1 = [Wa | Wb | Wc]); one E-row array written instead of two. */
+int pdg_edge_fwd_coop_c(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                        const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
+                        const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
+                        const float* b2, float* c_out, float* a2m, float* a2e, double* part_m, double* part_e,
+                        int with_edge_update, int nblocks, void* stream);
 /* pdg_edge_fwd_coop that also forms the aggregation's message sums (models.py:215-217) from its
  * a2m tiles, replacing pdg_segment_sum's re-read of a2m: sums[v] (fp64, N x 128) = sum of a2m over
  * v's incoming edges, raw (the message LayerNorm's statistics come out of this launch); rows of
@@ -317,6 +326,16 @@ int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float
                     const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
                     float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
                     const double* pairs_e, int npairs_e, void* stream);
+/* pdg_edge_bwd_w2 reading, instead of a1m / a1e, the C rows of pdg_edge_fwd_coop_c and the step's P / Q
+ * (N x 128, the pdg_node_pq_rw outputs the forward gathered), recomputing a1m / a1e bit for bit: the
+ * same outputs as pdg_edge_bwd_w2 on the stored a1 arrays, with one E-row array read instead of two
+ * (the four P / Q rows per edge are gathered, mostly from the caches). */
+int pdg_edge_bwd_w2_rc(int n_edges, const int* dst, const int* src, const float* gaggr, const float* ge_next,
+                       const float* a2m, const float* C, const float* P, const float* Q, const float* a2e,
+                       const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
+                       const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m, float* gz1e,
+                       float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
+                       const double* pairs_e, int npairs_e, void* stream);
 /* Edge encoder backward (models.py:268-274), fused: gz2 = LN_bwd(gy) [a2 > 0], slabs (zeroed
  * before, pdg_wgrad_reduce layout) += gz2^T a1 and the b2 sums, gz1 = (W2T gz2) [a1 > 0], and per
  * block narrow_sums[b] = (sum gz1 e_in, sum gz1) as 2 x 128 doubles; a1 = relu(w0 e_in + b0) is

@@ -92,6 +92,12 @@ VARIANTS = {
     "pair_blocks_per_cu": ("PDG_PAIR_BLOCKS_PER_CU", 1),
     # pdg_edge_enc_fwd blocks per CU (104 VGPRs, 41 KB LDS per 8-wave block)
     "enc_blocks_per_cu": ("PDG_ENC_BLOCKS_PER_CU", 2),
+    # training with the fused cooperative kernels: the edge forward stores C = Wc e + b1 instead of a1m
+    # and a1e (pdg_edge_fwd_coop_c) and the edge backward recomputes both bit for bit from C and the
+    # step's P / Q (pdg_edge_bwd_w2_rc): one E-row array written and one read instead of two each.
+    # Bitwise the same; off: 8.85-8.91 vs 8.78 ms per config-2 step (same box; edge_bwd 214 vs 201 us,
+    # the four P / Q row gathers cost more than the a1 row they replace, edge_fwd unchanged)
+    "recompute_a1": ("PDG_RECOMPUTE_A1", False),
 }
 
 
@@ -197,6 +203,7 @@ class EPDEngine:
         self.seg_sums_train = self.coop_fwd and var["seg_sums_train"]
         self.gsum2_coop = var["gsum2_coop"]
         self.nbwd_coop = var["nbwd_coop"]
+        self.recompute_a1 = var["recompute_a1"]
         self._enc_blocks = min(var["enc_blocks_per_cu"] *
                                torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
         self._seg_part = torch.empty(2 * self._nslabs_e * L, dtype=torch.float64, device=self.device)
@@ -209,7 +216,8 @@ class EPDEngine:
         cus = torch.cuda.get_device_properties(self.device).multi_processor_count
         return {"fused_edge_wgrad": self.fused_edge_wgrad, "pq_first": self.pq_first, "coop_fwd": self.coop_fwd,
                 "seg_sums": self.seg_sums, "seg_sums_train": self.seg_sums_train, "gsum2_coop": self.gsum2_coop,
-                "nbwd_coop": self.nbwd_coop, "pair_blocks_per_cu": self._nslabs_p // cus,
+                "nbwd_coop": self.nbwd_coop, "recompute_a1": self.recompute_a1,
+                "pair_blocks_per_cu": self._nslabs_p // cus,
                 "enc_blocks_per_cu": self._enc_blocks // cus}
 
     def _t(self, name: str, fn, *args):
@@ -300,11 +308,17 @@ class EPDEngine:
         a2n_prev, stn_prev, gn_prev, bn_prev = a2_ne, st[0], P["node_encoder.4.weight"], P["node_encoder.4.bias"]
         a2e_prev, ste_prev, ge_prev, be_prev = a2_ee, st[1], P["edge_encoder.4.weight"], P["edge_encoder.4.bias"]
         x_prev = e_prev = None
+        # the backward recomputes a1m / a1e from C and this step's P / Q (pdg_edge_bwd_w2_rc): P and Q
+        # are then kept per step
+        rc = (need_grad and bool(E) and self.recompute_a1 and self.fused_edge_wgrad and self.coop_fwd
+              and not self.seg_sums_train)
         Pm, Qm = self._empty(N, L), self._empty(N, L)
         pend_n = None                        # deferred node LayerNorm statistics (nparts)
         for t in range(steps):
             i_m, i_e, i_n = 2 + 3 * t, 3 + 3 * t, 4 + 3 * t
             x_t = self._empty(N, L)
+            if rc and t > 0:
+                Pm, Qm = self._empty(N, L), self._empty(N, L)
             if pend_n is not None:    # the previous step's node statistics, reduced inside node_pq
                 self._t("node_pq", lib.pdg_node_pq_rw_fin, N, _p(a2n_prev), self._part_a.data_ptr(), pend_n,
                         float(N * L), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_t), _p(W1), _p(Pm),
@@ -319,10 +333,17 @@ class EPDEngine:
             seg = bool(E) and (self.seg_sums_train if need_grad else self.seg_sums)
             a2m = self._empty(E, L) if (need_grad or not seg) else None   # seg: a backward-only output
             sums = torch.empty(N, L, dtype=torch.float64, device=self.device) if seg else None
-            a1m = self._empty(E, L) if need_grad else None          # layer-1 outputs: backward only
+            a1m = self._empty(E, L) if (need_grad and not rc) else None   # layer-1 outputs: backward only
             a2e = self._empty(E, L) if eu else None
-            a1e = self._empty(E, L) if (eu and need_grad) else None
-            if seg:
+            a1e = self._empty(E, L) if (eu and need_grad and not rc) else None
+            cst = self._empty(E, L) if rc else None                         # rc: C = Wc e + b1 instead
+            if rc:
+                self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop_c, E, _p(a2e_prev), ste_prev,
+                        _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm),
+                        _p(W1), _p(b1), _p(W2), _p(b2), _p(cst), _p(a2m), _p(a2e), _p(self._part_a),
+                        _p(self._part_b), int(eu), self._nslabs_e, s)
+                self._nparts.value = self._nslabs_e
+            elif seg:
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop_seg, E, _p(a2e_prev),
                         ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm),
                         _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e),
@@ -372,7 +393,8 @@ class EPDEngine:
                 self._finalize(self._part_a, N * L, st[i_n], s)
             if need_grad:
                 ctx.per_step.append(dict(x=x_t, e=e_t, a1m=a1m, a2m=a2m, a1e=a1e, a2e=a2e, aggr=aggr, xs=xs,
-                                         a1n=a1n, a2n=a2n, i_m=i_m, i_e=i_e, i_n=i_n, eu=eu))
+                                         a1n=a1n, a2n=a2n, i_m=i_m, i_e=i_e, i_n=i_n, eu=eu, C=cst,
+                                         P=Pm if rc else None, Q=Qm if rc else None))
             a2n_prev, stn_prev, gn_prev, bn_prev = a2n, st[i_n], gn, bnn
             a2e_prev, ste_prev, ge_prev, be_prev = a2e, st[i_e], ge, be
             x_prev, e_prev = x_t, e_t
@@ -528,11 +550,18 @@ class EPDEngine:
                 if eu:   # edge-update LayerNorm: gy = ge_next (per edge)
                     pp, n_e = edge_ln_pairs(PE(t), ge_next, d["a2e"], st[d["i_e"]], ACC_E, g_edge)
                     pe, ne = src(pp, n_e if not fused else n_edge)
-                if fused:
+                if fused and d["C"] is not None:   # a1m / a1e recomputed from C and the step's P / Q
+                    self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2_rc, E, _p(plan.dst),
+                            _p(plan.src), _p(gaggr), _p(ge_next), _p(d["a2m"]), _p(d["C"]), _p(d["P"]), _p(d["Q"]),
+                            _p(d["a2e"]), st[d["i_m"]], st[d["i_e"]] if eu else None, None, None, _p(g_edge),
+                            _p(T["W2T"]), _p(gz1m), _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe,
+                            ne, s)
+                elif fused:
                     self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
                             _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, s)
+                if fused:
                     # + the column sums / pairs of the LayerNorm that produced e_t (LN_e of step t-1, or the
                     # edge encoder's)
                     if t > 0:

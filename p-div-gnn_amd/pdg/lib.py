@@ -59,6 +59,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_edge_fwd_coop_seg": [I] + [P] * 20 + [I, P, P, P, I, P],
+    "pdg_edge_fwd_coop_c": [I] + [P] * 19 + [I, I, P],
     "pdg_segsum_fixup": [I, P, P, P, P],
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
@@ -71,6 +72,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_edge_enc_bwd": [I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P],
     "pdg_enc_narrow_reduce": [P, I, P, P, P],
     "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P, I, P],
+    "pdg_edge_bwd_w2_rc": [I] + [P] * 19 + [I, P, I, P, I, P],
     "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P, P, I, P],
     "pdg_mesh_graph": [I, P, I, I, P, I, P, P, P, ctypes.c_long, P, P, ctypes.c_long, P],
     "pdg_mesh_graph_scratch_bytes": [I, I],

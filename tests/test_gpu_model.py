@@ -252,6 +252,30 @@ def test_forward_variants_agree(nmesh, ngraph, steps):
             assert rel(g, g0[name]) < GRAD_TOL, (key, name, rel(g, g0[name]))
 
 
+@pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
+def test_recompute_a1_variant_is_bitwise(nmesh, ngraph, steps):
+    """recompute_a1 (the edge forward stores C = Wc e + b1, pdg_edge_fwd_coop_c; the edge backward
+    recomputes a1m / a1e from C and the step's P / Q, pdg_edge_bwd_w2_rc) gives the same training
+    output and every parameter gradient bit for bit as the stored-a1 default."""
+    from gnn_local_stress import losses
+    from pdg import meshgen
+    samples = meshgen.make_dataset(ngraph, n=nmesh, hole_radius=(0.15, 0.3), seed=7)
+    batch = make_batch(samples)
+    stats = {k: float(v) for k, v in dataset_stats(batch).items()}
+    res = {}
+    for rc in (False, True):
+        model = _model(steps, stats)
+        model._engine_for(batch.pos.device).recompute_a1 = rc
+        pred = model(batch, scale_output=False).local_stress
+        gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
+        total, _, _ = losses.batch_loss(pred, batch, gt, divergence=True, divergence_penalty=10.0)
+        total.backward()
+        res[rc] = (pred.detach().clone(), {n: p.grad.detach().clone() for n, p in model.named_parameters()})
+    assert torch.equal(res[True][0], res[False][0])
+    for name, g in res[True][1].items():
+        assert torch.equal(g, res[False][1][name]), name
+
+
 def test_edgeless_batch_matches_oracle():
     """A batch whose graphs have no edge at all (SURVEY §4 T1 'E=0 graphs'): as in the reference,
     every message aggregate is zero and the edge parameters get zero gradients; output and every
