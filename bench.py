@@ -50,7 +50,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PMC_FILE = ROOT / "profiles" / "r03_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
-TREE_GLOBS = ("p-div-gnn_amd/csrc/*.hip", "p-div-gnn_amd/csrc/*.hpp", "include/*.h", "p-div-gnn_amd/pdg/*.py",
+TREE_GLOBS = ("p-div-gnn_amd/pdg/libpdivgnn_hip.so", "p-div-gnn_amd/csrc/*.hip", "p-div-gnn_amd/csrc/*.hpp", "include/*.h", "p-div-gnn_amd/pdg/*.py",
               "p-div-gnn_amd/gnn_local_stress/*.py", "bench.py")
 PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
              "edge_bwd": "void edge_bwd_kernel<true>",

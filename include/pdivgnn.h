@@ -53,6 +53,8 @@ typedef struct pdg_ln_bwd {
 /* ---------------------------------------------------------------- library */
 const char* pdg_last_error(void);
 int pdg_version(void);
+/* Hash of the sources the library was built from (16 hex digits; build.py). */
+const char* pdg_source_hash(void);
 /* Upper bound on the number of per-block partials any launcher writes. */
 int pdg_max_blocks(void);
 

@@ -8,6 +8,7 @@ from __future__ import annotations
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -27,6 +28,19 @@ EXTRA = os.environ.get("PDG_EXTRA_FLAGS", "").split()
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", *EXTRA]
 
 
+def source_hash(csrc: Path = CSRC) -> str:
+    """sha256 (16 hex) of the library's sources; embedded as pdg_source_hash() and checked by pdg.lib
+    (same function there)."""
+    h = hashlib.sha256()
+    for f in sorted(csrc.glob("*.hip")) + sorted(csrc.glob("*.hpp")) + [csrc.parent.parent / "include" / "pdivgnn.h"]:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
+
+
+INFO = "pdg_build_info"   # compiled on every build, with the source hash
+
+
 def hipcc() -> str:
     for c in (os.environ.get("HIPCC"), shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if c and Path(c).exists():
@@ -37,9 +51,12 @@ def hipcc() -> str:
 def _compile(src: Path, report: bool) -> Path:
     obj = BUILD / (src.stem + ".o")
     deps = [src] + list(CSRC.glob("*.hpp")) + [CSRC.parent.parent / "include" / "pdivgnn.h"]
-    if obj.exists() and all(obj.stat().st_mtime >= d.stat().st_mtime for d in deps) and not report:
+    info = src.stem == INFO
+    if obj.exists() and all(obj.stat().st_mtime >= d.stat().st_mtime for d in deps) and not report and not info:
         return obj
     cmd = [hipcc(), *FLAGS, "-c", str(src), "-o", str(obj)]
+    if info:
+        cmd.append(f'-DPDG_SRC_HASH="{source_hash()}"')
     if report:
         cmd.append("-Rpass-analysis=kernel-resource-usage")
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -63,11 +80,11 @@ def build(force: bool = False, report: bool = False) -> Path:
             o.unlink()
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, report), srcs))
-    if force or not OUT.exists() or any(o.stat().st_mtime > OUT.stat().st_mtime for o in objs):
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs)]
-        r = subprocess.run(cmd, capture_output=True, text=True)
-        if r.returncode != 0:
-            raise RuntimeError(f"link failed:\n{r.stderr}")
+    # always linked: the build-info object is compiled on every build
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(OUT), *map(str, objs)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr}")
     return OUT
 
 

@@ -8,13 +8,28 @@ hot-path call raises.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 from ctypes import c_double, c_float, c_int, c_int64, c_void_p
 from pathlib import Path
 
 import torch  # noqa: F401  (must be loaded before the HIP library)
 
-LIB_PATH = Path(os.environ.get("PDG_LIB", Path(__file__).resolve().parent / "libpdivgnn_hip.so"))
+SHIPPED = Path(__file__).resolve().parent / "libpdivgnn_hip.so"
+LIB_PATH = Path(os.environ.get("PDG_LIB", SHIPPED))
+CSRC = Path(__file__).resolve().parents[1] / "csrc"
+
+
+def source_hash(csrc: Path = CSRC) -> str | None:
+    """build.py's hash of the library sources beside this package (None when they are absent)."""
+    files = sorted(csrc.glob("*.hip")) + sorted(csrc.glob("*.hpp")) + [csrc.parent.parent / "include" / "pdivgnn.h"]
+    if not csrc.is_dir() or not files[-1].exists():
+        return None
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:16]
 
 P = c_void_p
 I = c_int
@@ -23,6 +38,7 @@ I = c_int
 SIGNATURES: dict[str, list] = {
     "pdg_last_error": [],
     "pdg_version": [],
+    "pdg_source_hash": [],
     "pdg_max_blocks": [],
     "pdg_format_inputs": [I, I, P, P, P, P, P, P, I, P, P, P],
     "pdg_encoder_fwd": [I, I, P, P, P, P, P, P, P, P, P, P],
@@ -87,7 +103,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_collate": [P, I, ctypes.c_long, P],
     "pdg_adam": [c_int64, P, P, P, P, P, I, c_float, c_float, c_float, c_float, P, P, I, P],
 }
-_RESTYPES = {"pdg_last_error": ctypes.c_char_p, "pdg_mesh_graph_scratch_bytes": ctypes.c_long}
+_RESTYPES = {"pdg_last_error": ctypes.c_char_p, "pdg_source_hash": ctypes.c_char_p, "pdg_mesh_graph_scratch_bytes": ctypes.c_long}
 
 LN_STAT_BYTES = 40   # sizeof(pdg_ln_stat)
 LN_BWD_BYTES = 24    # sizeof(pdg_ln_bwd)
@@ -111,6 +127,13 @@ class _Lib:
                 fn = getattr(dll, name)
                 fn.argtypes = args
                 fn.restype = _RESTYPES.get(name, c_int)
+            # the shipped library must be the build of the sources beside it (A/B variants loaded
+            # through PDG_LIB may come from other revisions)
+            if LIB_PATH.resolve() == SHIPPED:
+                want, got = source_hash(), dll.pdg_source_hash().decode()
+                if want is not None and got != want:
+                    raise PdgError(f"{LIB_PATH} was built from other sources (hash {got}, sources {want}): "
+                                   "rebuild it with `python p-div-gnn_amd/build.py`")
             self._dll = dll
         return self._dll
 

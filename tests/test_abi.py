@@ -32,6 +32,12 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(dll, name), name
 
 
+def test_library_is_built_from_these_sources():
+    """The shipped library embeds build.py's hash of csrc/ + the header; pdg.lib refuses a stale one."""
+    from pdg.lib import lib, source_hash
+    assert lib.pdg_source_hash().decode() == source_hash()
+
+
 def test_ctypes_signatures_match_header():
     from pdg.lib import SIGNATURES
     d = _decls()

@@ -30,7 +30,7 @@ fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
   step prof 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o bench -- \
-    python "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-extras || exit 1
+    python "$R/bench.py" --steps 20 --warmup 2 --no-cpu-baseline --no-extras || exit 1
   step pmc_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch" -o bench -- \
     python "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-extras || exit 1
   step pmc_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmc_write" -o bench -- \
@@ -39,7 +39,7 @@ fi
 if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
   cd "$R"
   TREE=$(python -c "import bench; print(bench.tree_hash())")
-  { echo "tree $TREE"; python tools/prof_summary.py "$O/prof/bench_kernel_stats.csv" 7; } > "$O/prof_summary.txt"
+  { echo "tree $TREE"; python tools/prof_summary.py "$O/prof/bench_kernel_stats.csv" 22; } > "$O/prof_summary.txt"
   python tools/pmc_summary.py "$O/pmc_fetch/bench_counter_collection.csv" \
     "$O/pmc_write/bench_counter_collection.csv" --json "$O/pmc_traffic.json" --tree "$TREE" > "$O/pmc_traffic.txt"
   rm -f "$O"/prof/*kernel_trace.csv "$O"/*/*.db
