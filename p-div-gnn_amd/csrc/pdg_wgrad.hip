@@ -906,6 +906,160 @@ __global__ __launch_bounds__(512, 1) void wgrad_x6_pair_kernel(WgradSegs3 sg, lo
   }
 }
 
+// Two-deep form (default): 16-row rounds with TWO rounds of row loads in flight, in the registers one
+// 32-row round used to take (two sets of one row x three arrays per thread, by round parity): set s
+// is staged for round n and re-issued for round n + 2 at once, so rows are landing while the CU
+// multiplies (the form above issues the next round's rows at the top of a round and waits for them
+// after its MFMAs).  The images are double-buffered by round parity, one barrier per round.  No
+// load is conditional (rows past the block are clamped on load and zeroed when staged).  The weight
+// products accumulate the same K steps in the same order (bitwise the same dW); the column sums
+// are formed per thread over other rows (fp32, another order).  Per config-2 call 174-179 -> 164-168 us
+// (rocprofv3, same box); three sets in flight (PDG_WGP_DEPTH=3, triple-buffered images) measured the
+// same as two: what is left is the round's MFMA phase (two waves per SIMD) in series with its stage.
+#ifndef PDG_WGP_2DEEP
+#define PDG_WGP_2DEEP 1
+#endif
+#ifndef PDG_WGP_DEPTH
+#define PDG_WGP_DEPTH 2
+#endif
+constexpr int WGP_DEPTH = PDG_WGP_DEPTH;   // row sets (and image buffers) in flight
+constexpr int WG16 = 16 * X6_ROWB;   // bytes per term plane of a 16-row image (4 KB)
+constexpr int WIMG16 = 3 * WG16;     // one 16-row bf16x6 image (12 KB)
+
+// Split one row's 4 columns 4cg .. 4cg + 3 into image row r of a 16-row image.
+__device__ __forceinline__ void x6_store1(unsigned char* img, int cg, int r, const f32x4& v) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split3_pair(v[0], v[1], h0, m0, l0);
+  split3_pair(v[2], v[3], h1, m1, l1);
+  const int off = x6_addr(r, 8 * cg);
+  *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
+  *reinterpret_cast<u32x2*>(img + WG16 + off) = u32x2{m0, m1};
+  *reinterpret_cast<u32x2*>(img + 2 * WG16 + off) = u32x2{l0, l1};
+}
+
+template <bool SHX>
+__global__ __launch_bounds__(512, 1) void wgrad_x6_pair2_kernel(WgradSegs3 sg, long total, float* __restrict__ slabs0,
+                                                               float* __restrict__ slabs1) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem3[];   // [table | parity x A0 | A1 | A2]
+  WgTable3* tb = reinterpret_cast<WgTable3*>(smem3);
+  unsigned char* img = smem3 + WG3_TABLE_BYTES;
+  const int nseg = sg.nseg;
+  for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
+  for (int i = threadIdx.x; i < 3 * PDG_MAX_SEGS; i += blockDim.x) tb->A[i / PDG_MAX_SEGS][i % PDG_MAX_SEGS] =
+      sg.A[i / PDG_MAX_SEGS][i % PDG_MAX_SEGS];
+  __syncthreads();
+  const int nb = gridDim.x;
+  long per = (total + nb - 1) / nb;
+  per = (per + X6_ROWS - 1) / X6_ROWS * X6_ROWS;
+  const long r0 = min(total, per * blockIdx.x), r1 = min(total, per * (blockIdx.x + 1));
+  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
+  const int pw = w >> 2, w4 = w & 3;                      // product, quadrant
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;  // staged row rg, columns 4 cg ..
+  const int ob = 64 * (w4 >> 1), ib = 64 * (w4 & 1);
+  const int lrow = 8 * h + ((l & 15) >> 2);
+  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  f32x4 bs0 = f32x4{0.f, 0.f, 0.f, 0.f}, bs1 = f32x4{0.f, 0.f, 0.f, 0.f};   // column sums of A0 (and A1)
+  if (r0 < r1) {
+    int seg;
+    {
+      int lo = 0, hi = nseg;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tb->start[mid] <= r0) lo = mid; else hi = mid;
+      }
+      seg = lo;
+    }
+    f32x4 v[WGP_DEPTH][3];
+    auto issue = [&](const int s, long base) {   // rows past r1 read row r1 - 1 (zeroed when staged)
+      const long vr = min(base + rg, r1 - 1);
+      while (seg + 1 < nseg && vr >= tb->start[seg + 1]) ++seg;
+      const long r = vr - tb->start[seg];
+#pragma unroll
+      for (int a = 0; a < 3; ++a) v[s][a] = ldg4(tb->A[a][seg] + r * L + 4 * cg);
+    };
+    auto round = [&](const int s, long base) {
+      unsigned char* im = img + s * 3 * WIMG16;
+      {
+        const bool ok = base + rg < r1;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          const f32x4 x = ok ? v[s][a] : f32x4{0.f, 0.f, 0.f, 0.f};
+          if (a == 0) bs0 += x;
+          if (SHX && a == 1) bs1 += x;
+          x6_store1(im + a * WIMG16, cg, rg, x);
+        }
+      }
+      issue(s, base + 16 * WGP_DEPTH);   // the set is free: the round WGP_DEPTH ahead
+      __syncthreads();       // this round's images complete (the other parity's are the previous round's)
+      const unsigned char* gimg = im + (SHX ? pw : 0) * WIMG16;
+      const unsigned char* ximg = im + (SHX ? 2 : 1 + pw) * WIMG16;
+      bf16x8 A[2][3], B[2][3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int g0 = x6_addr(lrow, lcolb + 2 * (ob + 32 * a)), g1 = x6_addr(lrow + 4, lcolb + 2 * (ob + 32 * a));
+        const int x0 = x6_addr(lrow, lcolb + 2 * (ib + 32 * a)), x1 = x6_addr(lrow + 4, lcolb + 2 * (ib + 32 * a));
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          A[a][p] = x6_operand(gimg + p * WG16, g0, g1);
+          B[a][p] = x6_operand(ximg + p * WG16, x0, x1);
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          f32x16 t = acc[a][b];
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2], B[b][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][1], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][2], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][0], t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][1], t, 0, 0, 0);
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][0], t, 0, 0, 0);
+        }
+    };
+    // each set's loads strictly before the next set's, in the order the loop re-issues them
+#pragma unroll
+    for (int d = 0; d < WGP_DEPTH; ++d) {
+      issue(d, r0 + 16 * d);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    for (long base = r0; base < r1; base += 16 * WGP_DEPTH) {   // every round of a step runs (past r1: zeros)
+#pragma unroll
+      for (int d = 0; d < WGP_DEPTH; ++d) round(d, base + 16 * d);
+    }
+    __syncthreads();   // the last round's image reads precede the LDS reuse below
+  }
+  float* slab = (pw ? slabs1 : slabs0) + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int i = ib + 32 * b + c;
+        slab[o * L + i] = acc[a][b][r];
+      }
+  float* red = reinterpret_cast<float*>(img);
+  *reinterpret_cast<f32x4*>(red + 4 * threadIdx.x) = bs0;
+  *reinterpret_cast<f32x4*>(red + 2048 + 4 * threadIdx.x) = SHX ? bs1 : bs0;
+  __syncthreads();
+  if (threadIdx.x < 2 * L) {
+    const int p = threadIdx.x >> 7, col = threadIdx.x & 127, g = col >> 2, j = col & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += red[2048 * p + 4 * (32 * q + g) + j];
+    (p ? slabs1 : slabs0)[(size_t)blockIdx.x * SLAB + L * L + col] = s;
+  }
+}
+
 extern "C" int pdg_wgrad_pairs(int nseg, const float* const* a0_ptrs, const float* const* a1_ptrs,
                                const float* const* a2_ptrs, const int* rows, int shared_x, float* slabs0,
                                float* slabs1, int nslabs, void* stream) {
@@ -930,13 +1084,23 @@ extern "C" int pdg_wgrad_pairs(int nseg, const float* const* a0_ptrs, const floa
   for (int i = nseg + 1; i <= PDG_MAX_SEGS; ++i) sg.start[i] = tot;
   sg.nseg = nseg;
   PDG_CHECK_ARG(tot > 0, "pdg_wgrad_pairs: no rows");
-  const size_t shm = WG3_TABLE_BYTES + 9 * X6_TERM;
-  if (shared_x)
-    hipLaunchKernelGGL(wgrad_x6_pair_kernel<true>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot, slabs0,
-                       slabs1);
-  else
-    hipLaunchKernelGGL(wgrad_x6_pair_kernel<false>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
-                       slabs0, slabs1);
+  if (PDG_WGP_2DEEP) {
+    const size_t shm = WG3_TABLE_BYTES + WGP_DEPTH * 3 * WIMG16;
+    if (shared_x)
+      hipLaunchKernelGGL(wgrad_x6_pair2_kernel<true>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
+                         slabs0, slabs1);
+    else
+      hipLaunchKernelGGL(wgrad_x6_pair2_kernel<false>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
+                         slabs0, slabs1);
+  } else {
+    const size_t shm = WG3_TABLE_BYTES + 9 * X6_TERM;
+    if (shared_x)
+      hipLaunchKernelGGL(wgrad_x6_pair_kernel<true>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
+                         slabs0, slabs1);
+    else
+      hipLaunchKernelGGL(wgrad_x6_pair_kernel<false>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
+                         slabs0, slabs1);
+  }
   PDG_CHECK_LAUNCH("pdg_wgrad_pairs");
   return PDG_OK;
 }
