@@ -17,6 +17,7 @@
 // separate pdg_node_mlp1 / pdg_mlp2_fwd kernels.
 #include "pdg_common.hpp"
 #include "pdg_runtime.hpp"
+#include "pdg_x6.hpp"
 
 using namespace pdg;
 
@@ -605,6 +606,97 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
   }
 }
 
+// The same pass with P and Q as bf16x6 products (gemm_x6f: unbiased accumulation, 2.7x less matrix
+// time than the fp32 MFMAs; the kernel above is MFMA-bound).  x_t goes through a 16-row bf16x6 image
+// instead of an fp32 tile; Wa / Wb are held as bf16 terms (96 VGPRs).  x_t is bitwise the
+// kernel above's; P / Q agree with it to fp32 rounding and are closer to fp64.
+constexpr int PQ_T16 = TILE * X6_ROWB;       // bytes per term plane of a 16-row image (4 KB)
+constexpr int PQ_IMG = 3 * PQ_T16;           // one 16-row bf16x6 image (12 KB)
+
+// One block of 8 waves per CU, no loader waves (the weight terms need the 256-VGPR budget of 8
+// waves): every thread fetches one row chunk of tile i + 2 (a2_prev, x_prev) before the products of
+// tile i and stores it, LayerNorm applied and split, into buffer (i + 2) % 3 after the barrier.
+template <bool RES>
+__device__ __forceinline__ void fetch_xt1(f32x4& av, f32x4& rv, int t, int N, const float* __restrict__ a2p,
+                                          const float* __restrict__ xres) {
+  const int j = threadIdx.x & 31, node = t * TILE + (threadIdx.x >> 5);
+  const bool ok = node < N;
+  av = ok ? reinterpret_cast<const f32x4*>(a2p + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+  if (RES) rv = ok ? reinterpret_cast<const f32x4*>(xres + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+}
+
+template <bool RES>
+__device__ __forceinline__ void store_xt1(unsigned char* __restrict__ img, int t, int N, const f32x4& av,
+                                          const f32x4& rv, const LNStat& st, const f32x4& gg, const f32x4& bb,
+                                          float* __restrict__ xout) {
+  const int j = threadIdx.x & 31, rr = threadIdx.x >> 5, node = t * TILE + rr;
+  f32x4 y;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {   // ln_res_frag (pdg_fwd.hip), element by element
+    float v = div_den(av[e] - st.mean, st.den, st.rstd) * gg[e] + bb[e];
+    if (RES) v += rv[e];
+    y[e] = v;
+  }
+  x6_store4<PQ_T16>(img, rr, j, y);
+  if (node < N) stg4(xout + (size_t)node * L + 4 * j, y);
+}
+
+template <bool RES>
+__global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_pq_x6_kernel(
+    int N, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
+    const float* __restrict__ lb, const float* __restrict__ xres, float* __restrict__ xout,
+    const float* __restrict__ W1, float* __restrict__ P, float* __restrict__ Q, const double* __restrict__ part,
+    int nparts, double count, pdg_ln_stat* __restrict__ st_out) {
+  __shared__ __attribute__((aligned(16))) unsigned char xt[3 * PQ_IMG];
+  __shared__ LNStat st_sh;
+  __shared__ double red_fin[2 * NU_COMPUTE];
+  const int w = wave_id(), l = lane_id();
+  const int ntiles = tiles_of(N);
+  if (part) {   // the node LayerNorm statistics of the previous step, folded in (pdg_node_pq_rw_fin)
+    ln_stat_from_partials(part, nparts, count, &st_sh, red_fin);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_sh;
+  }
+  const LNStat st = part ? st_sh : *reinterpret_cast<const LNStat*>(stp);
+  const f32x4 gg = reinterpret_cast<const f32x4*>(lg)[threadIdx.x & 31];
+  const f32x4 bb = reinterpret_cast<const f32x4*>(lb)[threadIdx.x & 31];
+  const int r = l & 15, q = l >> 4;
+  const int oc = 16 * w + 4 * q;
+  f32x4 av, rv;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (nu_tile(k) < ntiles) {
+      fetch_xt1<RES>(av, rv, nu_tile(k), N, a2p, xres);
+      store_xt1<RES>(xt + k * PQ_IMG, nu_tile(k), N, av, rv, st, gg, bb, xout);
+    }
+  WSlice wa, wb;
+  load_wslice(wa, W1, w, 3 * L);
+  load_wslice(wb, W1 + L, w, 3 * L);
+  __syncthreads();
+  for (int i = 0;; ++i) {
+    const int tile = nu_tile(i);
+    if (tile >= ntiles) break;   // uniform across the block
+    const bool ahead = nu_tile(i + 2) < ntiles;
+    if (ahead) fetch_xt1<RES>(av, rv, nu_tile(i + 2), N, a2p, xres);
+    const int row = tile * TILE + r;
+    f32x4 dp[1] = {{0.f, 0.f, 0.f, 0.f}}, dq[1] = {{0.f, 0.f, 0.f, 0.f}};
+    const unsigned char* im = xt + (i % 3) * PQ_IMG;
+    gemm_x6f<1, PQ_T16>(dp, wa, im);
+    gemm_x6f<1, PQ_T16>(dq, wb, im);
+    if (row < N) {
+      stg4(P + (size_t)row * L + oc, dp[0]);
+      stg4(Q + (size_t)row * L + oc, dq[0]);
+    }
+    __syncthreads();
+    if (ahead)   // buffer (i + 2) % 3 was last read in iteration i - 1
+      store_xt1<RES>(xt + ((i + 2) % 3) * PQ_IMG, nu_tile(i + 2), N, av, rv, st, gg, bb, xout);
+  }
+}
+
+#ifndef PDG_NODE_PQ_X6
+#define PDG_NODE_PQ_X6 1
+#endif
+
 static int node_pq_rw_launch(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                              const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
                              float* Q, const double* part, int nparts, double count, pdg_ln_stat* st_out,
@@ -616,12 +708,15 @@ static int node_pq_rw_launch(int n_nodes, const float* a2_prev, const pdg_ln_sta
   const int tiles = tiles_of(n_nodes);
   const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
   const int grid = tiles < cap ? tiles : cap;
+  const int nt = PDG_NODE_PQ_X6 ? 64 * NU_COMPUTE : NU_THREADS;
   if (x_res)
-    hipLaunchKernelGGL(node_pq_rw_kernel<true>, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes,
-                       a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, part, nparts, count, st_out);
+    hipLaunchKernelGGL(PDG_NODE_PQ_X6 ? node_pq_x6_kernel<true> : node_pq_rw_kernel<true>, dim3(grid), dim3(nt), 0,
+                       (hipStream_t)stream, n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, part, nparts,
+                       count, st_out);
   else
-    hipLaunchKernelGGL(node_pq_rw_kernel<false>, dim3(grid), dim3(NU_THREADS), 0, (hipStream_t)stream, n_nodes,
-                       a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, part, nparts, count, st_out);
+    hipLaunchKernelGGL(PDG_NODE_PQ_X6 ? node_pq_x6_kernel<false> : node_pq_rw_kernel<false>, dim3(grid), dim3(nt), 0,
+                       (hipStream_t)stream, n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, part, nparts,
+                       count, st_out);
   PDG_CHECK_LAUNCH("pdg_node_pq_rw");
   return PDG_OK;
 }

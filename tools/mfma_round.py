@@ -18,11 +18,14 @@ SO = os.path.join(HERE, "_mfma_round.so")
 def lib():
     if not os.path.exists(SO):
         subprocess.check_call(["hipcc", "-O3", "--offload-arch=gfx950", "-shared", "-fPIC",
+                               "-I", os.path.join(HERE, "..", "p-div-gnn_amd", "csrc"),
                                os.path.join(HERE, "mfma_round.hip"), "-o", SO])
     d = ctypes.CDLL(SO)
     for f in (d.mfma_round_bf16, d.mfma_round_f32):
         f.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4
         f.restype = ctypes.c_int
+    d.x6_chain.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int]
+    d.x6_chain.restype = ctypes.c_int
     return d
 
 
@@ -85,6 +88,20 @@ def main():
         report(f"f32 16x16x4 positive {label}", *run_f32(A32.abs(), B32.abs(), C.abs()))
         report(f"f32 16x16x4 negative {label}", *run_f32(-A32.abs(), B32.abs(), -C.abs()))
         keep.clear()
+    # fp32-accurate K = 128 products: the accumulation schemes (x6_chain modes)
+    names = {0: "bf16x6 one chain", 1: "bf16x6 fresh per chunk + VALU", 2: "bf16x9 one chain", 3: "fp32 MFMA chain"}
+    for label, pos in (("signed", False), ("positive", True)):
+        A = torch.randn(T, 16, 128, generator=g)
+        B = torch.randn(T, 128, 16, generator=g)
+        if pos:
+            A, B = A.abs(), B.abs()
+        exact = torch.bmm(A.double(), B.double())
+        scale = torch.bmm(A.double().abs(), B.double().abs())
+        Ag, Bg = A.to(dev), B.to(dev)
+        for mode in (0, 1, 2, 3):
+            D = torch.empty(T, 16, 16, device=dev)
+            assert d.x6_chain(T, Ag.data_ptr(), Bg.data_ptr(), D.data_ptr(), mode) == 0
+            report(f"K=128 {names[mode]} {label}", D, exact, scale)
 
 
 if __name__ == "__main__":
