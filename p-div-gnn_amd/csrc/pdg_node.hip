@@ -291,6 +291,94 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_pair_kernel(
   }
 }
 
+// node_net with both layers as unbiased bf16x6 products (gemm_x6f; the fp32 kernels above are
+// MFMA-bound): 8 waves, no loader waves, the three weight slices W1a (aggr half), W1b (x half) and W2
+// as bf16 terms in registers (144 VGPRs).  Per 16-row tile: every thread fetches one row chunk of aggr
+// and x of tile i + 2, layer 1 of tile i from its [aggr | x] images, a barrier, the split of tile
+// i + 2 into the images layer 1 of tile i - 1 read, layer 2 of tile i from its a1 image (double-
+// buffered).  One barrier per tile; 96 KB of LDS.
+constexpr int NN_T16 = TILE * X6_ROWB;        // bytes per term plane of a 16-row image (4 KB)
+constexpr int NN_IMG = 3 * NN_T16;            // one 16-row bf16x6 image (12 KB)
+
+__global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
+    int N, const float* __restrict__ aggr, const float* __restrict__ x, const float* __restrict__ W1,
+    const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
+    float* __restrict__ a1_out, float* __restrict__ a2_out, double* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) unsigned char xin[3 * 2 * NN_IMG];   // [buffer][aggr | x]
+  __shared__ __attribute__((aligned(16))) unsigned char a1i[2 * NN_IMG];
+  const int w = wave_id(), l = lane_id();
+  const int ntiles = tiles_of(N);
+  const int r = l & 15, q = l >> 4;
+  const int oc = 16 * w + 4 * q;
+  const int j = threadIdx.x & 31, rr = threadIdx.x >> 5;   // the thread's staged row chunk
+  f32x4 va, vx;
+  auto fetch = [&](int t) {
+    const int node = t * TILE + rr;
+    const bool ok = node < N;
+    va = ok ? reinterpret_cast<const f32x4*>(aggr + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    vx = ok ? reinterpret_cast<const f32x4*>(x + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto stage = [&](int buf) {
+    x6_store4<NN_T16>(xin + (2 * buf) * NN_IMG, rr, j, va);
+    x6_store4<NN_T16>(xin + (2 * buf + 1) * NN_IMG, rr, j, vx);
+  };
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    if (nu_tile(k) < ntiles) {
+      fetch(nu_tile(k));
+      stage(k);
+    }
+  WSlice w1a, w1b, w2;
+  load_wslice(w1a, W1, w, 2 * L);
+  load_wslice(w1b, W1 + L, w, 2 * L);
+  load_wslice(w2, W2, w, L);
+  const f32x4 bias1 = *reinterpret_cast<const f32x4*>(b1 + oc);
+  const f32x4 bias2 = *reinterpret_cast<const f32x4*>(b2 + oc);
+  double s1 = 0, s2 = 0;
+  __syncthreads();
+  for (int i = 0;; ++i) {
+    const int tile = nu_tile(i);
+    if (tile >= ntiles) break;   // uniform across the block
+    const bool ahead = nu_tile(i + 2) < ntiles;
+    if (ahead) fetch(nu_tile(i + 2));
+    const int row = tile * TILE + r;
+    // layer 1: a1 = relu(W1a aggr + W1b x + b1), the aggr chunks first
+    f32x4 d1[1] = {{0.f, 0.f, 0.f, 0.f}};
+    gemm_x6f<1, NN_T16>(d1, w1a, xin + (2 * (i % 3)) * NN_IMG);
+    gemm_x6f<1, NN_T16>(d1, w1b, xin + (2 * (i % 3) + 1) * NN_IMG);
+    f32x4 a1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a1[c] = fmaxf(d1[0][c] + bias1[c], 0.f);
+    x6_store4<NN_T16>(a1i + (i & 1) * NN_IMG, r, 4 * w + q, a1);
+    if (row < N && a1_out) stg4(a1_out + (size_t)row * L + oc, a1);
+    __syncthreads();   // the a1 image is complete; the input buffer of tile i - 1 is free
+    if (ahead) stage((i + 2) % 3);
+    // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
+    f32x4 d2[1] = {{0.f, 0.f, 0.f, 0.f}};
+    gemm_x6f<1, NN_T16>(d2, w2, a1i + (i & 1) * NN_IMG);
+    f32x4 a2;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) a2[c] = fmaxf(d2[0][c] + bias2[c], 0.f);
+    if (row < N) {
+      stg4(a2_out + (size_t)row * L + oc, a2);
+      const float p1 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+      const float p2 = (a2[0] * a2[0] + a2[1] * a2[1]) + (a2[2] * a2[2] + a2[3] * a2[3]);
+      s1 += (double)p1;
+      s2 += (double)p2;
+    }
+  }
+  __shared__ double red[2 * NU_COMPUTE];
+  block_sum2(s1, s2, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s1;
+    part[2 * blockIdx.x + 1] = s2;
+  }
+}
+
+#ifndef PDG_NODE_NET_X6
+#define PDG_NODE_NET_X6 1
+#endif
+
 // paired tiles (node_net_pair_kernel) by default: 46.6 -> 45.5-46.4 us per config-2 call in a same-box
 // A/B; the same pairing of node_pq_rw measured no faster and is not kept
 #ifndef PDG_NODE_NET_PAIR
@@ -308,8 +396,12 @@ extern "C" int pdg_node_net(int n_nodes, const float* aggr, const float* x, cons
   const int tiles = tiles_of(n_nodes);
   const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
   const int grid = tiles < cap ? tiles : cap;
-  hipLaunchKernelGGL(PDG_NODE_NET_PAIR ? node_net_pair_kernel : node_net_kernel, dim3(grid), dim3(NU_THREADS), 0,
-                     (hipStream_t)stream, n_nodes, aggr, x, Wn1, bn1, Wn2, bn2, a1n, a2n, partials);
+  if (PDG_NODE_NET_X6)
+    hipLaunchKernelGGL(node_net_x6_kernel, dim3(grid), dim3(64 * NU_COMPUTE), 0, (hipStream_t)stream, n_nodes, aggr, x,
+                       Wn1, bn1, Wn2, bn2, a1n, a2n, partials);
+  else
+    hipLaunchKernelGGL(PDG_NODE_NET_PAIR ? node_net_pair_kernel : node_net_kernel, dim3(grid), dim3(NU_THREADS), 0,
+                       (hipStream_t)stream, n_nodes, aggr, x, Wn1, bn1, Wn2, bn2, a1n, a2n, partials);
   PDG_CHECK_LAUNCH("pdg_node_net");
   if (nparts) *nparts = grid;
   return PDG_OK;

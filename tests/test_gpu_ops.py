@@ -323,8 +323,11 @@ def test_wgrad_segments_dynamic_range(env):
 
 @pytest.mark.parametrize("N", [5, 1031, 4099, 8209, 40328, 100489])
 def test_node_net_matches_separate_kernels(env, N):
-    """Fused node_net (register-stationary weights) == pdg_node_mlp1 + pdg_mlp2_fwd bitwise;
-    LayerNorm partial totals equal to fp32 rounding; against float64 torch."""
+    """Fused node_net (register-stationary weights, unbiased bf16x6 products) against pdg_node_mlp1 +
+    pdg_mlp2_fwd (fp32 MFMA) and float64 torch: each layer's product (fed the fused kernel's own a1 for
+    layer 2) within 1e-6 of fp64, no less accurate than the fp32 kernels and without a mean bias; the
+    LayerNorm partial totals equal to the fused a2's to fp32 rounding; the inference form (a1n not
+    stored) bitwise the training form."""
     lib, sh, _ = env
     s = sh()
     aggr = rnd(N, L) * 3.0
@@ -337,23 +340,32 @@ def test_node_net_matches_separate_kernels(env, N):
     lib.pdg_node_mlp1(N, aggr.data_ptr(), x.data_ptr(), W1.data_ptr(), b1.data_ptr(), a10.data_ptr(), s)
     lib.pdg_mlp2_fwd(N, a10.data_ptr(), W2.data_ptr(), b2.data_ptr(), a20.data_ptr(), part0.data_ptr(),
                      ctypes.byref(n), s)
-    n0 = n.value
     a11, a21 = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
     part1 = torch.zeros(4096, dtype=torch.float64, device="cuda")
     assert lib.pdg_node_net(N, aggr.data_ptr(), x.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(),
                             b2.data_ptr(), a11.data_ptr(), a21.data_ptr(), part1.data_ptr(), ctypes.byref(n), s) == 0
     n1 = n.value
-    assert torch.equal(a10, a11) and torch.equal(a20, a21)
-    t0 = part0[: 2 * n0].view(n0, 2).sum(0)
+    # layer 1 (pre-activation compared where both relu outputs are positive) and layer 2 on the fused a1
+    z1 = torch.cat([aggr, x], 1).double() @ W1.double().T + b1.double()
+    h1 = torch.relu(z1)
+    assert rel(a11, h1) < 1e-6 and rel(a11, h1) <= rel(a10, h1) * 1.05 + 1e-9, (rel(a11, h1), rel(a10, h1))
+    h2 = torch.relu(a11.double() @ W2.double().T + b2.double())
+    h2_0 = torch.relu(a10.double() @ W2.double().T + b2.double())
+    assert rel(a21, h2) < 1e-6 and rel(a21, h2) <= rel(a20, h2_0) * 1.05 + 1e-9, (rel(a21, h2), rel(a20, h2_0))
+    if N >= 1000:   # mean signed error of layer 1 relative to the product scale (one bf16x6 chain: ~ -1e-9)
+        scale = torch.cat([aggr, x], 1).double().abs() @ W1.double().abs().T
+        pos = (a11 > 0) & (z1 > 0)
+        bias = float(((a11.double() - z1) / scale.clamp_min(1e-30))[pos].mean())
+        assert abs(bias) < 3e-10, bias
     t1 = part1[: 2 * n1].view(n1, 2).sum(0)
-    assert float(((t0 - t1).abs() / t0.abs()).max()) < 1e-6
+    a2d = a21.double()
+    assert rel(t1, torch.stack([a2d.sum(), a2d.square().sum()])) < 1e-7
     a2i = torch.empty(N, L, device="cuda")   # inference form: a1n not stored
     lib.pdg_node_net(N, aggr.data_ptr(), x.data_ptr(), W1.data_ptr(), b1.data_ptr(), W2.data_ptr(), b2.data_ptr(),
                      None, a2i.data_ptr(), part1.data_ptr(), ctypes.byref(n), s)
-    assert torch.equal(a2i, a20)
-    h1 = torch.relu(torch.cat([aggr, x], 1).double() @ W1.double().T + b1.double())
-    h2 = torch.relu(h1 @ W2.double().T + b2.double())
-    assert rel(a21, h2) < TOL
+    assert torch.equal(a2i, a21)
+    h2f = torch.relu(h1 @ W2.double().T + b2.double())
+    assert rel(a21, h2f) < TOL
 
 
 @pytest.mark.parametrize("N", [7, 1031, 40328])
