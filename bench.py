@@ -54,7 +54,7 @@ TREE_GLOBS = ("p-div-gnn_amd/pdg/libpdivgnn_hip.so", "p-div-gnn_amd/csrc/*.hip",
               "p-div-gnn_amd/gnn_local_stress/*.py", "bench.py")
 PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
              "edge_bwd": "void edge_bwd_kernel<true>",
-             "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_pair_kernel", "node_net_kernel"),
+             "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_x6_kernel", "node_net_pair_kernel", "node_net_kernel"),
              "pq_scatter_bwd": "pq_scatter_bwd_kernel",
              "wgrad_W2": "wgrad_x6_kernel", "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
              "edge_gout": "void edge_gout_wc_kernel<true>"}
@@ -259,8 +259,10 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
         # (pdg_segsum_finish): reads the fp64 message sums and rowptr, writes aggr
         "segment_sum": ([], (8 * L * N + 4 * (N + 1) + 4 * L * N) if seg
                         else 4 * L * E + 4 * (N + 1) + (1 if infer else 2) * 4 * L * N),
-        # node_net, 2 fp32 GEMMs (K = 256, 128) per node: reads aggr, x; writes a2n (+ a1n)
-        "node_net": ([(N * 2 * L * (2 * L + L), PEAK_FP32_MFMA)], 2 * 4 * L * N + (1 if infer else 2) * 4 * L * N),
+        # node_net, 2 fp32-accurate GEMMs (K = 256, 128) per node as bf16x6 products (node_net_x6_kernel;
+        # the fp32-MFMA kernels are A/B build variants): reads aggr, x; writes a2n (+ a1n)
+        "node_net": ([(N * 2 * L * (2 * L + L) * X6, PEAK_BF16_MFMA)],
+                     2 * 4 * L * N + (1 if infer else 2) * 4 * L * N),
         "pq_scatter_bwd": ([], 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
     }
 
