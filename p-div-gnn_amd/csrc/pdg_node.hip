@@ -297,6 +297,9 @@ __global__ __launch_bounds__(NU_THREADS, 1) void node_net_pair_kernel(
 // and x of tile i + 2, layer 1 of tile i from its [aggr | x] images, a barrier, the split of tile
 // i + 2 into the images layer 1 of tile i - 1 read, layer 2 of tile i from its a1 image (double-
 // buffered).  One barrier per tile; 96 KB of LDS.
+#ifndef PDG_NN_LATE_STAGE
+#define PDG_NN_LATE_STAGE 1
+#endif
 constexpr int NN_T16 = TILE * X6_ROWB;        // bytes per term plane of a 16-row image (4 KB)
 constexpr int NN_IMG = 3 * NN_T16;            // one 16-row bf16x6 image (12 KB)
 
@@ -352,7 +355,9 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
     x6_store4<NN_T16>(a1i + (i & 1) * NN_IMG, r, 4 * w + q, a1);
     if (row < N && a1_out) stg4(a1_out + (size_t)row * L + oc, a1);
     __syncthreads();   // the a1 image is complete; the input buffer of tile i - 1 is free
+#if !PDG_NN_LATE_STAGE
     if (ahead) stage((i + 2) % 3);
+#endif
     // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
     f32x4 d2[1] = {{0.f, 0.f, 0.f, 0.f}};
     gemm_x6f<1, NN_T16>(d2, w2, a1i + (i & 1) * NN_IMG);
@@ -366,6 +371,11 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
       s1 += (double)p1;
       s2 += (double)p2;
     }
+#if PDG_NN_LATE_STAGE
+    // tile i + 2 into the buffer layer 1 of tile i - 1 read (before the previous barrier); read after
+    // the next one.  After layer 2 its loads have the whole tile to land.
+    if (ahead) stage((i + 2) % 3);
+#endif
   }
   __shared__ double red[2 * NU_COMPUTE];
   block_sum2(s1, s2, red);
