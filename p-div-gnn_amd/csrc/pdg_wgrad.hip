@@ -665,6 +665,149 @@ __global__ __launch_bounds__(256 * NG, 3 / NG) void wgrad_x6_jobs_kernel(WgradJo
   wgrad_x6_body<NG>(jobs.s[j], jobs.total[j], jobs.slabs[j]);
 }
 
+constexpr int WG16 = 16 * X6_ROWB;   // bytes per term plane of a 16-row image (4 KB)
+constexpr int WIMG16 = 3 * WG16;     // one 16-row bf16x6 image (12 KB)
+
+// Split one row's 4 columns 4cg .. 4cg + 3 into image row r of a 16-row image.
+__device__ __forceinline__ void x6_store1(unsigned char* img, int cg, int r, const f32x4& v) {
+  unsigned h0, m0, l0, h1, m1, l1;
+  split3_pair(v[0], v[1], h0, m0, l0);
+  split3_pair(v[2], v[3], h1, m1, l1);
+  const int off = x6_addr(r, 8 * cg);
+  *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
+  *reinterpret_cast<u32x2*>(img + WG16 + off) = u32x2{m0, m1};
+  *reinterpret_cast<u32x2*>(img + 2 * WG16 + off) = u32x2{l0, l1};
+}
+
+// Two-deep form (default; the structure of wgrad_x6_pair2_kernel for one product): one block of 8 waves
+// per slab, 16-row rounds with two rounds of (G, X) row loads in flight by round parity, double-
+// buffered 16-row images, one barrier per round.  Wave w owns o in 32 (w & 3) + [0, 32), i in
+// 64 (w >> 2) + [0, 64) as two 32x32 accumulators.  The block's K steps run in row order (the grouped
+// form above summed three row thirds and added them at the end: the same products in another order).
+#ifndef PDG_WGJ_2DEEP
+#define PDG_WGJ_2DEEP 1
+#endif
+__device__ __forceinline__ void wgrad_x6_body2(const WgradSegs& sg, long total, float* __restrict__ slabs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem7[];   // [table | parity x (G | X)]
+  WgTable* tb = reinterpret_cast<WgTable*>(smem7);
+  unsigned char* img = smem7 + WG_TABLE_FLOATS * 4;
+  const int nseg = sg.nseg;
+  for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
+  for (int i = threadIdx.x; i < PDG_MAX_SEGS; i += blockDim.x) {
+    tb->G[i] = sg.G[i];
+    tb->X[i] = sg.X[i];
+  }
+  __syncthreads();
+  const int nb = gridDim.x;
+  long per = (total + nb - 1) / nb;
+  per = (per + X6_ROWS - 1) / X6_ROWS * X6_ROWS;
+  const long r0 = min(total, per * blockIdx.x), r1 = min(total, per * (blockIdx.x + 1));
+  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;   // staged row rg, columns 4 cg ..
+  const int ob = 32 * (w & 3), ib = 64 * (w >> 2);
+  const int lrow = 8 * h + ((l & 15) >> 2);
+  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
+  f32x16 acc[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  f32x4 bs = f32x4{0.f, 0.f, 0.f, 0.f};   // column sums of G
+  if (r0 < r1) {
+    int seg;
+    {
+      int lo = 0, hi = nseg;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tb->start[mid] <= r0) lo = mid; else hi = mid;
+      }
+      seg = lo;
+    }
+    f32x4 vg[2], vx[2];
+    auto issue = [&](const int s, long base) {   // rows past r1 read row r1 - 1 (zeroed when staged)
+      const long vr = min(base + rg, r1 - 1);
+      while (seg + 1 < nseg && vr >= tb->start[seg + 1]) ++seg;
+      const long r = vr - tb->start[seg];
+      vg[s] = ldg4(tb->G[seg] + r * L + 4 * cg);
+      vx[s] = ldg4(tb->X[seg] + r * L + 4 * cg);
+    };
+    auto round = [&](const int s, long base) {
+      unsigned char* gimg = img + s * 2 * WIMG16;
+      unsigned char* ximg = gimg + WIMG16;
+      {
+        const bool ok = base + rg < r1;
+        const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4 g = ok ? vg[s] : zero, x = ok ? vx[s] : zero;
+        bs += g;
+        x6_store1(gimg, cg, rg, g);
+        x6_store1(ximg, cg, rg, x);
+      }
+      issue(s, base + 32);   // the set is free: the round after next
+      __syncthreads();       // this round's images complete (the other parity's are the previous round's)
+      bf16x8 A[3], B[2][3];
+      const int g0 = x6_addr(lrow, lcolb + 2 * ob), g1 = x6_addr(lrow + 4, lcolb + 2 * ob);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) A[p] = x6_operand(gimg + p * WG16, g0, g1);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int x0 = x6_addr(lrow, lcolb + 2 * (ib + 32 * b)), x1 = x6_addr(lrow + 4, lcolb + 2 * (ib + 32 * b));
+#pragma unroll
+        for (int p = 0; p < 3; ++p) B[b][p] = x6_operand(ximg + p * WG16, x0, x1);
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        f32x16 t = acc[b];
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[b][0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[b][1], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[b][2], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[b][0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[b][1], t, 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[b][0], t, 0, 0, 0);
+      }
+    };
+    issue(0, r0);
+    __builtin_amdgcn_sched_barrier(0);
+    issue(1, r0 + 16);
+    __builtin_amdgcn_sched_barrier(0);
+    for (long base = r0; base < r1; base += 32) {   // both rounds always run (a round past r1 adds zeros)
+      round(0, base);
+      round(1, base + 16);
+    }
+    __syncthreads();   // the last round's image reads precede the LDS reuse below
+  }
+  float* slab = slabs + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int i = ib + 32 * b + c;
+      slab[o * L + i] = acc[b][r];
+    }
+  // bias sums: the 16 row groups of each column group, in row-group order (the images are dead)
+  float* red = reinterpret_cast<float*>(img);
+  *reinterpret_cast<f32x4*>(red + 4 * threadIdx.x) = bs;
+  __syncthreads();
+  if (threadIdx.x < L) {
+    const int col = threadIdx.x, g = col >> 2, j = col & 3;
+    float sum = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sum += red[4 * (32 * q + g) + j];
+    slab[L * L + col] = sum;
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void wgrad_x6_kernel2(WgradSegs sg, long total, float* __restrict__ slabs) {
+  wgrad_x6_body2(sg, total, slabs);
+}
+
+__global__ __launch_bounds__(512, 1) void wgrad_x6_jobs_kernel2(WgradJobs jobs) {
+  const int j = blockIdx.y;
+  wgrad_x6_body2(jobs.s[j], jobs.total[j], jobs.slabs[j]);
+}
+
+constexpr size_t WGJ2_SHM = WG_TABLE_FLOATS * 4 + 2 * 2 * WIMG16;
+
 extern "C" int pdg_wgrad_slabs_per_cu(void) { return 3 / PDG_WGRAD_GROUPS; }
 
 extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
@@ -689,7 +832,9 @@ extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const fl
   hipLaunchKernelGGL(wgrad_segments_kernel, dim3(nslabs), dim3(256), (WG_TABLE_FLOATS + 4 * WG_TILE) * sizeof(float),
                      (hipStream_t)stream, sg, tot, slabs);
 #else
-#if PDG_WGRAD_GROUPS == 3
+#if PDG_WGJ_2DEEP
+  hipLaunchKernelGGL(wgrad_x6_kernel2, dim3(nslabs), dim3(512), WGJ2_SHM, (hipStream_t)stream, sg, tot, slabs);
+#elif PDG_WGRAD_GROUPS == 3
   hipLaunchKernelGGL(wgrad_x6_kernel<3>, dim3(nslabs), dim3(768), WG_TABLE_FLOATS * 4 + 18 * X6_TERM,
                      (hipStream_t)stream, sg, tot, slabs);
 #else
@@ -735,8 +880,11 @@ extern "C" int pdg_wgrad_segments_batch(int njobs, const int* nseg, const float*
     jobs.total[j] = tot;
     jobs.slabs[j] = slabs[j];
   }
-  hipLaunchKernelGGL(wgrad_x6_jobs_kernel<3>, dim3(nslabs, njobs), dim3(768), WG_TABLE_FLOATS * 4 + 18 * X6_TERM,
-                     (hipStream_t)stream, jobs);
+  if (PDG_WGJ_2DEEP)
+    hipLaunchKernelGGL(wgrad_x6_jobs_kernel2, dim3(nslabs, njobs), dim3(512), WGJ2_SHM, (hipStream_t)stream, jobs);
+  else
+    hipLaunchKernelGGL(wgrad_x6_jobs_kernel<3>, dim3(nslabs, njobs), dim3(768), WG_TABLE_FLOATS * 4 + 18 * X6_TERM,
+                       (hipStream_t)stream, jobs);
   PDG_CHECK_LAUNCH("pdg_wgrad_segments_batch");
   return PDG_OK;
 #endif
@@ -923,20 +1071,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_x6_pair_kernel(WgradSegs3 sg, lo
 #define PDG_WGP_DEPTH 2
 #endif
 constexpr int WGP_DEPTH = PDG_WGP_DEPTH;   // row sets (and image buffers) in flight
-constexpr int WG16 = 16 * X6_ROWB;   // bytes per term plane of a 16-row image (4 KB)
-constexpr int WIMG16 = 3 * WG16;     // one 16-row bf16x6 image (12 KB)
-
-// Split one row's 4 columns 4cg .. 4cg + 3 into image row r of a 16-row image.
-__device__ __forceinline__ void x6_store1(unsigned char* img, int cg, int r, const f32x4& v) {
-  unsigned h0, m0, l0, h1, m1, l1;
-  split3_pair(v[0], v[1], h0, m0, l0);
-  split3_pair(v[2], v[3], h1, m1, l1);
-  const int off = x6_addr(r, 8 * cg);
-  *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
-  *reinterpret_cast<u32x2*>(img + WG16 + off) = u32x2{m0, m1};
-  *reinterpret_cast<u32x2*>(img + 2 * WG16 + off) = u32x2{l0, l1};
-}
-
 template <bool SHX>
 __global__ __launch_bounds__(512, 1) void wgrad_x6_pair2_kernel(WgradSegs3 sg, long total, float* __restrict__ slabs0,
                                                                float* __restrict__ slabs1) {
