@@ -1349,6 +1349,117 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void node_bwd_coop_kernel(
   }
 }
 
+// Edge encoder backward, two-deep (default; edge_bwd_w2_kernel's form): 16-row rounds with two rounds
+// of row loads in flight in two register sets (round parity), double-buffered images / masks / inputs,
+// one barrier per round.  Every output is bitwise edge_enc_bwd_kernel's: the weight-gradient K steps,
+// the per-lane narrow sums and the per-thread bias sums visit the same rows in the same order.
+#ifndef PDG_EEB_2DEEP
+#define PDG_EEB_2DEEP 1
+#endif
+constexpr int EEB2_BUF = 2 * IMG16 + MSK16 + R16 * 4;   // one round's images, mask and inputs
+
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd2_kernel(
+    const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ e_in,
+    const float* __restrict__ w0, const float* __restrict__ b0, const pdg_ln_stat* __restrict__ st_p,
+    const pdg_ln_bwd* __restrict__ lb_p, const double* __restrict__ pairs, int npairs,
+    const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ slabs,
+    double* __restrict__ nsums, int E) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;    // the thread's staged row: rg (0..15)
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(E, r0, r1);
+  f32x16 acc[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
+  double sw[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};   // narrow sums of features oc .. oc+3
+  f32x4 pg[2], pa2[2];
+  float pe[2];
+  auto issue = [&](const int s, int base) {   // clamped: E > 0 (an empty block reads row E - 1)
+    const int rc = clamp_row(base + rg, r1);
+    pg[s] = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + 4 * cg);
+    pa2[s] = *reinterpret_cast<const f32x4*>(a2 + (size_t)rc * L + 4 * cg);
+    pe[s] = e_in[rc];
+  };
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+  const f32x4 w04 = *reinterpret_cast<const f32x4*>(w0 + 4 * cg);
+  const f32x4 b04 = *reinterpret_cast<const f32x4*>(b0 + 4 * cg);
+  const LNStat st = *reinterpret_cast<const LNStat*>(st_p);
+  issue(0, r0);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(1, r0 + R16);
+  __builtin_amdgcn_sched_barrier(0);
+  // the weights and the LayerNorm scalars after the first rounds' row loads: the round trips overlap
+  WSlice ws;
+  load_wslice(ws, W2T, w);
+  const pdg_ln_bwd lb = lnb_resolve(lb_p, pairs, npairs, st_p);
+  // the loop-invariant vectors in registers before the loop (pending at the loop head, their loads
+  // made the stage wait for every row load in flight)
+  pin_vgpr(g4);
+  pin_vgpr(w04);
+  pin_vgpr(b04);
+  auto round = [&](const int s, const int base) {
+    unsigned char* img_g = sm + s * EEB2_BUF;                  // gz2
+    unsigned char* img_a = img_g + IMG16;                      // a1
+    unsigned char* msk = img_g + 2 * IMG16;                    // [a1 > 0]
+    float* ev = reinterpret_cast<float*>(msk + MSK16);         // the round's 16 inputs
+    {
+      const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = base + rg < r1;
+      const f32x4 zg = ok ? ln_relu_bwd4(pg[s], pa2[s], st, lb, g4) : zero;
+      bsum += zg;
+      img_store4<T16>(img_g, rg, cg, zg);
+      f32x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = fmaxf(fmaf(w04[j], pe[s], 0.f) + b04[j], 0.f);   // encoder_kernel's a1
+      a = ok ? a : zero;
+      img_store4<T16>(img_a, rg, cg, a);
+      *reinterpret_cast<unsigned*>(msk + rg * MSK_STRIDE + 4 * cg) = relu_mask4(a);
+      if (cg == 0) ev[rg] = ok ? pe[s] : 0.f;
+    }
+    issue(s, base + 2 * R16);   // the set is free: the round after next
+    __syncthreads();            // this round's images complete (the other buffer is the previous round's)
+    wgrad_round<1, T16>(acc, img_g, img_a);                // dW2 += gz2^T a1
+    f32x4 d[1][1];
+    const unsigned char* imgs[1] = {img_g};
+    gemm_round<1, 1, T16>(d, ws, imgs);                    // W2^T gz2, features oc .. oc+3
+    const int r = l & 15;
+    const unsigned mm = *reinterpret_cast<const unsigned*>(msk + r * MSK_STRIDE + oc);
+    const double e = (double)ev[r];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float z = (mm >> (8 * j)) & 1u ? d[0][0][j] : 0.f;
+      sw[j] += (double)z * e;
+      sb[j] += (double)z;
+    }
+  };
+  // both rounds of a 32-row step always run: a round past r1 stages zero rows (exact zeros)
+  for (int base = r0; base < r1; base += 2 * R16) {
+    round(0, base);
+    round(1, base + R16);
+  }
+  __syncthreads();   // the last rounds' image reads precede the LDS reuse below
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sw[j] += __shfl_xor(sw[j], off);
+      sb[j] += __shfl_xor(sb[j], off);
+    }
+  if ((l & 15) == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      nsums[(size_t)blockIdx.x * 2 * L + oc + j] = sw[j];
+      nsums[(size_t)blockIdx.x * 2 * L + L + oc + j] = sb[j];
+    }
+  }
+}
+
 // ============================================================================ encoder backward
 // pdg_mlp2_bwd in the cooperative layout (the node encoder's backward, models.py:264-275 for the
 // 6-input encoder): gz2 = LN_bwd(gy) [a2 > 0] (whole rows -> HBM and a bf16x6 image),
@@ -1628,9 +1739,10 @@ extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, c
   PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2) && PDG_ALIGNED(w0) && PDG_ALIGNED(b0) && PDG_ALIGNED(ln_g) &&
                     PDG_ALIGNED(W2T) && PDG_ALIGNED(slabs),
                 "pdg_edge_enc_bwd: misaligned pointer");
-  const size_t shm = 2 * EBW_IMG + EBW_MASK + X6_ROWS * sizeof(float);
-  hipLaunchKernelGGL(edge_enc_bwd_kernel, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gy, a2, e_in, w0,
-                     b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs, narrow_sums, n_edges);
+  const size_t shm = PDG_EEB_2DEEP ? 2 * EEB2_BUF : 2 * EBW_IMG + EBW_MASK + X6_ROWS * sizeof(float);
+  hipLaunchKernelGGL(PDG_EEB_2DEEP ? edge_enc_bwd2_kernel : edge_enc_bwd_kernel, dim3(nslabs), dim3(EBW_THREADS), shm,
+                     (hipStream_t)stream, gy, a2, e_in, w0, b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs,
+                     narrow_sums, n_edges);
   PDG_CHECK_LAUNCH("pdg_edge_enc_bwd");
   return PDG_OK;
 }
