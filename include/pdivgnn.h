@@ -125,6 +125,13 @@ int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const
  * xhat_sum (nullable): sum_k (rows[k] - mean)/(std + eps), kept for the LayerNorm backward. */
 int pdg_segment_sum(int n_nodes, const int* rowptr, const float* rows, const pdg_ln_stat* st,
                     const float* ln_g, const float* ln_b, float* out, float* xhat_sum, void* stream);
+/* pdg_segment_sum with the message LayerNorm's statistics reduced in the kernel from the edge
+ * forward's per-block (sum, sumsq) partials part_a (nparts pairs, count = rows x 128 elements), bitwise
+ * pdg_ln_finalize's, stored to st_a; with part_b also the edge-update LayerNorm's, stored to st_b.
+ * Replaces pdg_ln_finalize2 + pdg_segment_sum (one launch fewer per message-passing step). */
+int pdg_segment_sum_fin(int n_nodes, const int* rowptr, const float* rows, const double* part_a,
+                        const double* part_b, int nparts, double count, pdg_ln_stat* st_a, pdg_ln_stat* st_b,
+                        const float* ln_g, const float* ln_b, float* out, float* xhat_sum, void* stream);
 
 /* Processor.update first layer (models.py:240-243, :202-204):
  * a1n = relu(Wn1[:, 0:128] aggr + Wn1[:, 128:256] x + bn1). */

@@ -576,16 +576,35 @@ extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat
 // segment order (= PyG scatter_add_ order for a coalesced edge_index).
 constexpr int SEG_U = 8;
 
+// part_a (pdg_segment_sum_fin): the message LayerNorm's statistics are reduced here from the edge
+// forward's per-block partials (ln_stat_from_partials: bitwise pdg_ln_finalize) instead of by a
+// finalize launch; block 0 stores them to st_a (read by the backward) and, from part_b, the
+// edge-update LayerNorm's to st_b (read by the next step's edge forward).
 __global__ __launch_bounds__(256) void segment_sum_kernel(int N, const int* __restrict__ rowptr,
                                                           const float* __restrict__ rows,
                                                           const pdg_ln_stat* __restrict__ stp,
                                                           const float* __restrict__ lg,
                                                           const float* __restrict__ lb,
-                                                          float* __restrict__ out, float* __restrict__ xsum) {
+                                                          float* __restrict__ out, float* __restrict__ xsum,
+                                                          const double* __restrict__ part_a,
+                                                          const double* __restrict__ part_b, int nparts, double count,
+                                                          pdg_ln_stat* __restrict__ st_a, pdg_ln_stat* __restrict__ st_b) {
   const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
   const int nhw = blockDim.x >> 5;
   float mean = 0.f, den = 1.f, rstd = 1.f;
   f32x4 g = {1.f, 1.f, 1.f, 1.f}, b = {0.f, 0.f, 0.f, 0.f};
+  __shared__ pdg_ln_stat st_sh;
+  __shared__ double red[8];
+  if (part_a) {
+    if (blockIdx.x == 0 && part_b) {
+      ln_stat_from_partials(part_b, nparts, count, st_b, red);
+      __syncthreads();
+    }
+    ln_stat_from_partials(part_a, nparts, count, &st_sh, red);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) *st_a = st_sh;
+    stp = &st_sh;
+  }
   const bool ln = stp != nullptr;
   if (ln) {
     mean = stp->mean;
@@ -635,8 +654,27 @@ extern "C" int pdg_segment_sum(int n_nodes, const int* rowptr, const float* rows
   long cap = (long)device_cus() * 8;
   const int grid = (int)(want < cap ? want : cap);
   hipLaunchKernelGGL(segment_sum_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, rowptr, rows,
-                     st, ln_g, ln_b, out, xhat_sum);
+                     st, ln_g, ln_b, out, xhat_sum, nullptr, nullptr, 0, 0.0, nullptr, nullptr);
   PDG_CHECK_LAUNCH("pdg_segment_sum");
+  return PDG_OK;
+}
+
+extern "C" int pdg_segment_sum_fin(int n_nodes, const int* rowptr, const float* rows, const double* part_a,
+                                   const double* part_b, int nparts, double count, pdg_ln_stat* st_a,
+                                   pdg_ln_stat* st_b, const float* ln_g, const float* ln_b, float* out,
+                                   float* xhat_sum, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0, "pdg_segment_sum_fin: n_nodes must be > 0");
+  PDG_CHECK_ARG(part_a && st_a && ln_g && ln_b && nparts > 0 && nparts <= MAX_BLOCKS && count > 0 &&
+                    (!part_b || st_b),
+                "pdg_segment_sum_fin: bad statistics arguments");
+  PDG_CHECK_ARG(PDG_ALIGNED(rows) && PDG_ALIGNED(out) && (!xhat_sum || PDG_ALIGNED(xhat_sum)),
+                "pdg_segment_sum_fin: misaligned pointer");
+  long want = (n_nodes + 7) / 8;
+  long cap = (long)device_cus() * 8;
+  const int grid = (int)(want < cap ? want : cap);
+  hipLaunchKernelGGL(segment_sum_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, rowptr, rows,
+                     nullptr, ln_g, ln_b, out, xhat_sum, part_a, part_b, nparts, count, st_a, st_b);
+  PDG_CHECK_LAUNCH("pdg_segment_sum_fin");
   return PDG_OK;
 }
 

@@ -361,7 +361,8 @@ class EPDEngine:
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
                         _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
                         _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
-            if E:
+            fin_in_segsum = bool(E) and not seg and self.sync is None   # reduced inside pdg_segment_sum_fin
+            if E and not fin_in_segsum:
                 if eu and self.sync is None:    # both edge LayerNorms in one launch
                     lib.pdg_ln_finalize2(self._part_a.data_ptr(), self._part_b.data_ptr(), self._nparts.value,
                                          float(E * L), st[i_m], st[i_e], s)
@@ -380,8 +381,13 @@ class EPDEngine:
             elif E:
                 aggr = self._empty(N, L)
                 xs = self._empty(N, L) if need_grad else None
-                self._t("segment_sum", lib.pdg_segment_sum, N, _p(plan.rowptr_dst), _p(a2m), st[i_m], _p(ge),
-                        _p(be), _p(aggr), _p(xs), s)
+                if fin_in_segsum:   # + both edge LayerNorms' statistics from the edge forward's partials
+                    self._t("segment_sum", lib.pdg_segment_sum_fin, N, _p(plan.rowptr_dst), _p(a2m),
+                            _p(self._part_a), _p(self._part_b) if eu else None, self._nparts.value, float(E * L),
+                            st[i_m], st[i_e] if eu else None, _p(ge), _p(be), _p(aggr), _p(xs), s)
+                else:
+                    self._t("segment_sum", lib.pdg_segment_sum, N, _p(plan.rowptr_dst), _p(a2m), st[i_m], _p(ge),
+                            _p(be), _p(aggr), _p(xs), s)
             else:
                 aggr = torch.zeros(N, L, dtype=torch.float32, device=self.device)
                 xs = torch.zeros(N, L, dtype=torch.float32, device=self.device) if need_grad else None

@@ -51,6 +51,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_node_pq_rw": [I, P, P, P, P, P, P, P, P, P, P],
     "pdg_edge_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
     "pdg_segment_sum": [I, P, P, P, P, P, P, P, P],
+    "pdg_segment_sum_fin": [I, P, P, P, P, I, c_double, P, P, P, P, P, P, P],
     "pdg_node_mlp1": [I, P, P, P, P, P, P],
     "pdg_mlp2_fwd": [I, P, P, P, P, P, P, P],
     "pdg_node_net": [I, P, P, P, P, P, P, P, P, P, P, P],

@@ -482,6 +482,49 @@ def test_register_weight_kernels_match_lds_kernels(env, N, res):
     assert rel(sp, torch.stack([(gd * got[:L]).sum(), (gd * got[L:]).sum()])) < 1e-9
 
 
+@pytest.mark.parametrize("N,E,nparts,both", [(7, 30, 1, True), (1031, 6000, 37, False), (40328, 239744, 256, True)])
+def test_segment_sum_fin_equals_finalize2_then_segment_sum(env, N, E, nparts, both):
+    """pdg_segment_sum_fin (the edge LayerNorms' statistics reduced inside the segment sum) is bitwise
+    pdg_ln_finalize2 (or pdg_ln_finalize) + pdg_segment_sum: the sums, the x-hat sums and both 40-byte
+    statistics it stores."""
+    lib, sh, _ = env
+    s = sh()
+    src, dst, rp = _csr(N, E)
+    rows = torch.relu(rnd(E, L))
+    other = torch.relu(rnd(E, L)) * 0.5
+    g, b = rnd(L) + 1.0, rnd(L)
+    rp_d = rp.int().cuda()
+    edges = torch.linspace(0, E, nparts + 1).round().long().tolist()
+
+    def partials(a):
+        a64 = a.double()
+        return torch.stack([torch.stack([a64[i:j].sum(), a64[i:j].square().sum()])
+                            for i, j in zip(edges[:-1], edges[1:])]).reshape(-1).cuda()
+    pa, pb = partials(rows), partials(other)
+    outs = []
+    for fin in (False, True):
+        st_a = torch.full((40,), 0xAB, dtype=torch.uint8, device="cuda")
+        st_b = torch.full((40,), 0xCD, dtype=torch.uint8, device="cuda")
+        out, xs = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
+        if fin:
+            assert lib.pdg_segment_sum_fin(N, rp_d.data_ptr(), rows.data_ptr(), pa.data_ptr(),
+                                           pb.data_ptr() if both else None, nparts, float(E * L), st_a.data_ptr(),
+                                           st_b.data_ptr() if both else None, g.data_ptr(), b.data_ptr(),
+                                           out.data_ptr(), xs.data_ptr(), s) == 0
+        else:
+            if both:
+                lib.pdg_ln_finalize2(pa.data_ptr(), pb.data_ptr(), nparts, float(E * L), st_a.data_ptr(),
+                                     st_b.data_ptr(), s)
+            else:
+                lib.pdg_ln_finalize(pa.data_ptr(), nparts, float(E * L), st_a.data_ptr(), s)
+            lib.pdg_segment_sum(N, rp_d.data_ptr(), rows.data_ptr(), st_a.data_ptr(), g.data_ptr(), b.data_ptr(),
+                                out.data_ptr(), xs.data_ptr(), s)
+        torch.cuda.synchronize()
+        outs.append((st_a, st_b if both else None, out, xs))
+    for u, v in zip(*outs):
+        assert (u is None and v is None) or torch.equal(u, v)
+
+
 @pytest.mark.parametrize("N,nparts,res", [(7, 1, True), (1031, 37, False), (40328, 256, True), (5000, 700, False)])
 def test_node_pq_rw_fin_equals_finalize_then_pq_rw(env, N, nparts, res):
     """pdg_node_pq_rw_fin (node LayerNorm statistics reduced inside the consumer) is bitwise
