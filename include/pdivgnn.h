@@ -323,7 +323,8 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
  * slab map is fixed and the slabs accumulate, reduced once by pdg_wgrad_reduce).
  *   pdg_edge_bwd_w2:  gz1m/gz1e/gC as pdg_edge_bwd; slabs (zeroed before the first call)
  *                     += gz2m^T a1m + gz2e^T a1e and the b2 column sums; gz2m/gz2e are not
- *                     materialised.  ge_next == NULL: message branch only, gC = gz1m.
+ *                     materialised.  ge_next == NULL: message branch only, gC = gz1m.  gC may
+ *                     be NULL (not written; pdg_edge_gout_wc2 forms it).
  *   pdg_edge_gout_wc: ge_out = [ge_next +] WcT gC; slabs += gC^T e and the b1 column sums.
  *                     a2ln != NULL: also the column sums of the backward of the LayerNorm that
  *                     produced e (input a2ln, statistics st_ln, upstream gradient ge_out), as
@@ -360,6 +361,13 @@ int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* 
                      const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
                      const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,
                      int accumulate, void* stream);
+/* pdg_edge_gout_wc with gC = gz1m + gz1e formed on load (the fp32 add pdg_edge_bwd_w2 would store as
+ * gC; gz1e == NULL: gC = gz1m), so pdg_edge_bwd_w2 runs with gC == NULL and writes one E-row stream
+ * fewer.  Same outputs bit for bit. */
+int pdg_edge_gout_wc2(int n_edges, const float* gz1m, const float* gz1e, const float* e,
+                      const float* ge_next, const float* WcT, float* ge_out, float* slabs, int nslabs,
+                      const float* a2ln, const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g,
+                      double* pairs, int accumulate, void* stream);
 
 /* Mesh graph on the device (pdg_graph.hip): FaceToEdge of a triangle
  * mesh (convert_utils.py:47-60), edge lengths (datasets.py:182-188) and, when `periodic`,

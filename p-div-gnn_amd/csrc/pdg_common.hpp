@@ -44,6 +44,7 @@ constexpr int EDGE_WAVES = PDG_EDGE_WAVES;
 constexpr float LN_EPS = 1e-5f;         // torch_geometric LayerNorm default eps
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 // Graph-LayerNorm statistics of one call (written by pdg_ln_finalize) and the
 // backward scalars of one call: include/pdivgnn.h.
@@ -121,6 +122,32 @@ __device__ __forceinline__ f32x4 ldg4(const float* p) {
   typedef __attribute__((address_space(1))) const f32x4 g_f32x4;
   return *(g_f32x4*)p;
 }
+// Branch-free row access for loops whose vmcnt waits must be counted exactly (a load or store skipped on
+// some path makes the compiler wait for every outstanding memory operation, vmcnt(0), at the merge).
+__device__ __forceinline__ int clamp_row(int r, int r1) { return r < r1 ? r : r1 - 1; }
+
+// An empty asm that reads x: its load has completed here, and cannot be sunk past this point.
+template <class T>
+__device__ __forceinline__ void pin_vgpr(const T& x) {
+  asm volatile("" ::"v"(x));
+}
+
+// Buffer resource over rows [r0, r1) of a (rows, 128) fp32 array: stores past row r1 fall outside
+// num_records and are dropped by the hardware range check (no branch around them).  A null array
+// gets an empty range (every store dropped).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int r0, int r1) {
+  return __builtin_amdgcn_make_buffer_rsrc(base ? base + (size_t)r0 * L : nullptr, (short)0,
+                                           base ? (r1 - r0) * L * 4 : 0, 0x00020000);
+}
+// 16-byte store of columns c .. c+3 of block-relative row r (dropped when r is past the range).
+__device__ __forceinline__ void rows_store4(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, 0);
+}
+// The same, nontemporal (aux nt: the policy of stnt4 / PDG_NT_ST).
+__device__ __forceinline__ void rows_store4_nt(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, PDG_NT_ST ? 2 : 0);
+}
+
 // A 16-byte row store with the fragment stores' policy (nontemporal with PDG_NT_ST).
 __device__ __forceinline__ void stnt4(float* __restrict__ p, const f32x4& x) { st4(p, 0, x); }
 // Feature index of fragment element s in lane quarter q.

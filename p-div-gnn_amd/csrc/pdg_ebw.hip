@@ -197,31 +197,6 @@ __device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const 
   }
 }
 
-__device__ __forceinline__ int clamp_row(int r, int r1) { return r < r1 ? r : r1 - 1; }
-
-// An empty asm that reads x: its load has completed here, and cannot be sunk past this point.
-template <class T>
-__device__ __forceinline__ void pin_vgpr(const T& x) {
-  asm volatile("" ::"v"(x));
-}
-
-// Buffer resource over rows [r0, r1) of a (rows, 128) fp32 array: stores past row r1 fall outside
-// num_records and are dropped by the hardware range check (no branch around them).  A null array
-// gets an empty range (every store dropped).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int r0, int r1) {
-  return __builtin_amdgcn_make_buffer_rsrc(base ? base + (size_t)r0 * L : nullptr, (short)0,
-                                           base ? (r1 - r0) * L * 4 : 0, 0x00020000);
-}
-// 16-byte store of columns c .. c+3 of block-relative row r (dropped when r is past the range).
-__device__ __forceinline__ void rows_store4(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, 0);
-}
-// The same, nontemporal (aux nt: the policy of stnt4 / PDG_NT_ST).
-__device__ __forceinline__ void rows_store4_nt(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, PDG_NT_ST ? 2 : 0);
-}
-
-
 }  // namespace
 
 // ============================================================================ W2 path
@@ -412,9 +387,12 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
 }
 
 // ============================================================================ Wc path
-template <bool RES>
+// C2 (pdg_edge_gout_wc2): gC is formed here as gz1m + gz1e (the two arrays pdg_edge_bwd_w2 writes
+// anyway, the same fp32 add it would store as gC), so the edge backward writes no gC stream.
+template <bool RES, bool C2 = false>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
-    const float* __restrict__ gC, const float* __restrict__ e, const float* __restrict__ ge_next,
+    const float* __restrict__ gC, const float* __restrict__ gC2, const float* __restrict__ e,
+    const float* __restrict__ ge_next,
     const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs,
     const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, double* __restrict__ part, int E,
     const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate) {
@@ -440,12 +418,13 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
   // LayerNorm column sums of this thread's columns 4cg .. 4cg+3 (ln_colsum_kernel, pdg_bwd.hip)
   double cs_g[4] = {0, 0, 0, 0}, cs_x[4] = {0, 0, 0, 0};
   // prefetched rows of the next round, all whole-row (a second slot measured no faster)
-  f32x4 pc[2], pe[2], pres[2], pa2[2];
+  f32x4 pc[2], pc2[2], pe[2], pres[2], pa2[2];
   auto issue = [&](int base) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
       pc[u] = *reinterpret_cast<const f32x4*>(gC + rc);
+      if (C2) pc2[u] = *reinterpret_cast<const f32x4*>(gC2 + rc);
       pe[u] = *reinterpret_cast<const f32x4*>(e + rc);
       if (RES) pres[u] = *reinterpret_cast<const f32x4*>(ge_next + rc);
       if (ln) pa2[u] = *reinterpret_cast<const f32x4*>(a2ln + rc);   // LayerNorm input of e
@@ -460,7 +439,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
       const int r = rg + 16 * u;
       const bool ok = base + r < r1;
       const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 c = ok ? pc[u] : zero;
+      const f32x4 c = ok ? (C2 ? pc[u] + pc2[u] : pc[u]) : zero;
       bsum += c;
       img_store4(img_c, r, cg, c);
       img_store4(img_e, r, cg, ok ? pe[u] : zero);
@@ -1652,7 +1631,8 @@ static int edge_bwd_w2_launch(int n_edges, const int* dst, const float* gaggr, c
   const bool rc = C != nullptr;
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_w2: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_bwd_w2: bad slabs");
-  PDG_CHECK_ARG(dst && gaggr && a2m && (rc || a1m) && st_m && (lb_m || pairs_m) && ln_g && W2T && gz1m && gC,
+  // gC may be NULL: not written (pdg_edge_gout_wc2 forms it from gz1m + gz1e)
+  PDG_CHECK_ARG(dst && gaggr && a2m && (rc || a1m) && st_m && (lb_m || pairs_m) && ln_g && W2T && gz1m,
                 "pdg_edge_bwd_w2: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && (rc || PDG_ALIGNED(a1m)) && PDG_ALIGNED(ln_g) &&
                     PDG_ALIGNED(W2T) && PDG_ALIGNED(gz1m) && PDG_ALIGNED(gC) && PDG_ALIGNED(slabs),
@@ -1704,10 +1684,12 @@ extern "C" int pdg_edge_bwd_w2_rc(int n_edges, const int* dst, const int* src, c
                             stream);
 }
 
-extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
-                                float* ge_out, float* slabs, int nslabs, const float* a2ln, const pdg_ln_stat* st_ln,
-                                double* ln_partials, const float* ln_g, double* pairs, int accumulate, void* stream) {
+static int edge_gout_wc_launch(int n_edges, const float* gC, const float* gC2, const float* e, const float* ge_next,
+                               const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
+                               const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,
+                               int accumulate, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_gout_wc: n_edges must be > 0");
+  PDG_CHECK_ARG(!gC2 || PDG_ALIGNED(gC2), "pdg_edge_gout_wc2: misaligned gz1e");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_gout_wc: bad slabs");
   PDG_CHECK_ARG(gC && e && WcT && ge_out, "pdg_edge_gout_wc: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gC) && PDG_ALIGNED(e) && PDG_ALIGNED(WcT) && PDG_ALIGNED(ge_out) &&
@@ -1718,14 +1700,32 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
   PDG_CHECK_ARG(!pairs || (a2ln && ln_g), "pdg_edge_gout_wc: pairs need a2ln and ln_g");
   // LDS: the two images, then (LayerNorm column sums) the row groups' sums + one row + its scratch
   const size_t shm = 2 * EBW_IMG + ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
-  if (ge_next)
-    hipLaunchKernelGGL(edge_gout_wc_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
-  else
-    hipLaunchKernelGGL(edge_gout_wc_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
+#define PDG_GOUT(R, C)                                                                                            \
+  hipLaunchKernelGGL((edge_gout_wc_kernel<R, C>), dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, gC2, \
+                     e, ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate)
+  if (ge_next) {
+    if (gC2) PDG_GOUT(true, true); else PDG_GOUT(true, false);
+  } else {
+    if (gC2) PDG_GOUT(false, true); else PDG_GOUT(false, false);
+  }
+#undef PDG_GOUT
   PDG_CHECK_LAUNCH("pdg_edge_gout_wc");
   return PDG_OK;
+}
+
+extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
+                                float* ge_out, float* slabs, int nslabs, const float* a2ln, const pdg_ln_stat* st_ln,
+                                double* ln_partials, const float* ln_g, double* pairs, int accumulate, void* stream) {
+  return edge_gout_wc_launch(n_edges, gC, nullptr, e, ge_next, WcT, ge_out, slabs, nslabs, a2ln, st_ln, ln_partials,
+                             ln_g, pairs, accumulate, stream);
+}
+
+extern "C" int pdg_edge_gout_wc2(int n_edges, const float* gz1m, const float* gz1e, const float* e,
+                                 const float* ge_next, const float* WcT, float* ge_out, float* slabs, int nslabs,
+                                 const float* a2ln, const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g,
+                                 double* pairs, int accumulate, void* stream) {
+  return edge_gout_wc_launch(n_edges, gz1m, gz1e, e, ge_next, WcT, ge_out, slabs, nslabs, a2ln, st_ln, ln_partials,
+                             ln_g, pairs, accumulate, stream);
 }
 
 extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, const float* e_in, const float* w0,

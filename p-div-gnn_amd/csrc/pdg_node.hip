@@ -718,20 +718,27 @@ constexpr int PQ_IMG = 3 * PQ_T16;           // one 16-row bf16x6 image (12 KB)
 // One block of 8 waves per CU, no loader waves (the weight terms need the 256-VGPR budget of 8
 // waves): every thread fetches one row chunk of tile i + 2 (a2_prev, x_prev) before the products of
 // tile i and stores it, LayerNorm applied and split, into buffer (i + 2) % 3 after the barrier.
+// Branch-free (node_pq_x6_kernel's tile loop): rows past N are loaded clamped (a real row) and the
+// x rows are stored through a per-tile buffer range that drops rows past N.
 template <bool RES>
 __device__ __forceinline__ void fetch_xt1(f32x4& av, f32x4& rv, int t, int N, const float* __restrict__ a2p,
                                           const float* __restrict__ xres) {
-  const int j = threadIdx.x & 31, node = t * TILE + (threadIdx.x >> 5);
-  const bool ok = node < N;
-  av = ok ? reinterpret_cast<const f32x4*>(a2p + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-  if (RES) rv = ok ? reinterpret_cast<const f32x4*>(xres + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+  const int j = threadIdx.x & 31, node = clamp_row(t * TILE + (threadIdx.x >> 5), N);
+  av = reinterpret_cast<const f32x4*>(a2p + (size_t)node * L)[j];
+  if (RES) rv = reinterpret_cast<const f32x4*>(xres + (size_t)node * L)[j];
+}
+
+// [t0, t1) of tile t, empty past the last tile
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(float* base, int t, int N) {
+  const int t0 = t * TILE, t1 = max(t0, min(N, t0 + TILE));
+  return rows_rsrc(base, t1 > t0 ? t0 : 0, t1 > t0 ? t1 : 0);
 }
 
 template <bool RES>
 __device__ __forceinline__ void store_xt1(unsigned char* __restrict__ img, int t, int N, const f32x4& av,
                                           const f32x4& rv, const LNStat& st, const f32x4& gg, const f32x4& bb,
                                           float* __restrict__ xout) {
-  const int j = threadIdx.x & 31, rr = threadIdx.x >> 5, node = t * TILE + rr;
+  const int j = threadIdx.x & 31, rr = threadIdx.x >> 5;
   f32x4 y;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {   // ln_res_frag (pdg_fwd.hip), element by element
@@ -740,7 +747,7 @@ __device__ __forceinline__ void store_xt1(unsigned char* __restrict__ img, int t
     y[e] = v;
   }
   x6_store4<PQ_T16>(img, rr, j, y);
-  if (node < N) stg4(xout + (size_t)node * L + 4 * j, y);
+  rows_store4(tile_rsrc(xout, t, N), rr, 4 * j, y);
 }
 
 template <bool RES>
@@ -762,6 +769,12 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_pq_x6_kernel(
   const LNStat st = part ? st_sh : *reinterpret_cast<const LNStat*>(stp);
   const f32x4 gg = reinterpret_cast<const f32x4*>(lg)[threadIdx.x & 31];
   const f32x4 bb = reinterpret_cast<const f32x4*>(lb)[threadIdx.x & 31];
+  // loaded before the loop: a wait for them inside it would count the loop's stores too
+  pin_vgpr(gg);
+  pin_vgpr(bb);
+  pin_vgpr(st.mean);
+  pin_vgpr(st.den);
+  pin_vgpr(st.rstd);
   const int r = l & 15, q = l >> 4;
   const int oc = 16 * w + 4 * q;
   f32x4 av, rv;
@@ -778,20 +791,18 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_pq_x6_kernel(
   for (int i = 0;; ++i) {
     const int tile = nu_tile(i);
     if (tile >= ntiles) break;   // uniform across the block
-    const bool ahead = nu_tile(i + 2) < ntiles;
-    if (ahead) fetch_xt1<RES>(av, rv, nu_tile(i + 2), N, a2p, xres);
-    const int row = tile * TILE + r;
+    // no memory operation below is conditional (a skipped one made every wait in the loop a vmcnt(0)):
+    // past the last tile the rows are loaded clamped and staged into a free buffer, stores dropped
+    fetch_xt1<RES>(av, rv, nu_tile(i + 2), N, a2p, xres);
     f32x4 dp[1] = {{0.f, 0.f, 0.f, 0.f}}, dq[1] = {{0.f, 0.f, 0.f, 0.f}};
     const unsigned char* im = xt + (i % 3) * PQ_IMG;
     gemm_x6f<1, PQ_T16>(dp, wa, im);
     gemm_x6f<1, PQ_T16>(dq, wb, im);
-    if (row < N) {
-      stg4(P + (size_t)row * L + oc, dp[0]);
-      stg4(Q + (size_t)row * L + oc, dq[0]);
-    }
+    rows_store4(tile_rsrc(P, tile, N), r, oc, dp[0]);
+    rows_store4(tile_rsrc(Q, tile, N), r, oc, dq[0]);
     __syncthreads();
-    if (ahead)   // buffer (i + 2) % 3 was last read in iteration i - 1
-      store_xt1<RES>(xt + ((i + 2) % 3) * PQ_IMG, nu_tile(i + 2), N, av, rv, st, gg, bb, xout);
+    // buffer (i + 2) % 3 was last read in iteration i - 1
+    store_xt1<RES>(xt + ((i + 2) % 3) * PQ_IMG, nu_tile(i + 2), N, av, rv, st, gg, bb, xout);
   }
 }
 

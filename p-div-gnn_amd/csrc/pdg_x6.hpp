@@ -60,8 +60,6 @@ __device__ __forceinline__ bf16x8 x6_operand(const unsigned char* img, int ofs0,
   return __builtin_bit_cast(bf16x8, r);
 }
 
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
 // A operand of rows 16w .. 16w+15 of a 128x128 matrix WT (o' x k, row-major), K chunk ks
 // (k = 32 ks + 8 (l >> 4) + 0..7), three bf16 terms.
 struct WSlice {

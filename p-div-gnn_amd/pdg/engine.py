@@ -98,6 +98,9 @@ VARIANTS = {
     # Bitwise the same; off: 8.85-8.91 vs 8.78 ms per config-2 step (same box; edge_bwd 214 vs 201 us,
     # the four P / Q row gathers cost more than the a1 row they replace, edge_fwd unchanged)
     "recompute_a1": ("PDG_RECOMPUTE_A1", False),
+    # the Wc pass reads gz1m + gz1e and forms gC on load (pdg_edge_gout_wc2), so the edge backward writes
+    # no gC stream (bitwise the same)
+    "gout_gz1": ("PDG_GOUT_GZ1", False),
 }
 
 
@@ -196,6 +199,7 @@ class EPDEngine:
         # kernel variants (VARIANTS above; tests and A/B tools flip these attributes)
         self.fused_edge_wgrad = var["fused_edge_wgrad"]
         self.pq_first = var["pq_first"]
+        self.gout_gz1 = var["gout_gz1"]
         self.coop_fwd = var["coop_fwd"]
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
@@ -516,7 +520,8 @@ class EPDEngine:
         gaggr, gx_part, gx_t = (self._empty(N, L) for _ in range(3))
         gz1m, gz1e = self._empty(E, L), self._empty(E, L)
         ge_bufs = [self._empty(E, L), self._empty(E, L)]
-        gC_fused = self._empty(E, L) if fused else None
+        gz1_in_gout = fused and self.gout_gz1   # gC formed by pdg_edge_gout_wc2 from gz1m + gz1e
+        gC_fused = self._empty(E, L) if (fused and not gz1_in_gout) else None
         gx_next = gx
         # node LayerNorm of the last step (upstream gradient: the decoder's); for the earlier steps
         # the previous iteration's pdg_gemm_sum2_rw produces these partials
@@ -575,10 +580,14 @@ class EPDEngine:
                                                      g_edge, PE(t - 1))
                     else:
                         a2ln, st_ln, accb, gl, pp = ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"], P_EENC
-                    gout_args = (E, _p(gC), _p(d["e"]), _p(ge_next), _p(T["WcT"]), _p(ge_out), _p(slabs_wc), nse,
-                                 _p(a2ln), st_ln, _p(accb), _p(gl), _p(pp), 1, s)
+                    tail = (_p(d["e"]), _p(ge_next), _p(T["WcT"]), _p(ge_out), _p(slabs_wc), nse, _p(a2ln), st_ln,
+                            _p(accb), _p(gl), _p(pp), 1, s)
+                    if gz1_in_gout:
+                        gout_fn, gout_args = lib.pdg_edge_gout_wc2, (E, _p(gz1m), _p(gz1e if eu else None)) + tail
+                    else:
+                        gout_fn, gout_args = lib.pdg_edge_gout_wc, (E, _p(gC)) + tail
                     if not self.pq_first:
-                        self._t("edge_gout", lib.pdg_edge_gout_wc, *gout_args)
+                        self._t("edge_gout", gout_fn, *gout_args)
                     n_edge = nse
                 else:
                     self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr),
@@ -588,7 +597,7 @@ class EPDEngine:
                 self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
                         _p(plan.perm_src), _p(gz1m), _p(gz1e if eu else None), _p(gP), _p(gQ), s)
                 if fused and self.pq_first:   # gz1m / gz1e read while still in the Infinity Cache
-                    self._t("edge_gout", lib.pdg_edge_gout_wc, *gout_args)
+                    self._t("edge_gout", gout_fn, *gout_args)
             # gx_t, with the column sums / pairs of the LayerNorm whose output it is the gradient of:
             # the node LayerNorm of step t-1, or the node encoder's
             if t > 0:
