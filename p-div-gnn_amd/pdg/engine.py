@@ -29,6 +29,7 @@ from dataclasses import dataclass, field
 
 import torch
 
+from . import hiptimer
 from .lib import LN_BWD_BYTES, LN_STAT_BYTES, lib, stream_handle
 from .plan import GraphPlan
 
@@ -212,7 +213,7 @@ class EPDEngine:
                                torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
         self._seg_part = torch.empty(2 * self._nslabs_e * L, dtype=torch.float64, device=self.device)
         self._seg_info = torch.empty(4 * self._nslabs_e, dtype=torch.int32, device=self.device)
-        # optional live kernel timing: name -> list of (start, end) torch.cuda.Event pairs
+        # optional live kernel timing: name -> list of (start, end) hiptimer.Event pairs
         self.timed: dict | None = None
 
     def variants(self) -> dict:
@@ -229,8 +230,7 @@ class EPDEngine:
         on the current stream (the stream every launch of this engine uses)."""
         if self.timed is None or name not in self.timed:
             return fn(*args)
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
+        a, b = hiptimer.Event(), hiptimer.Event()   # no system-scope fence per record (pdg/hiptimer.py)
         a.record()
         r = fn(*args)
         b.record()

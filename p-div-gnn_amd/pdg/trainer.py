@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import torch
 
+from . import hiptimer
 from .engine import PARAM_NAMES, PARAM_SHAPES, EPDEngine
 from .lib import lib, stream_handle
 from .plan import plan_for
@@ -99,11 +100,11 @@ class Trainer:
         timing is off)."""
         if self.timed is None:
             return lambda: None
-        a = torch.cuda.Event(enable_timing=True)
+        a = hiptimer.Event()
         a.record()
 
         def end():
-            b = torch.cuda.Event(enable_timing=True)
+            b = hiptimer.Event()
             b.record()
             self.timed.setdefault(name, []).append((a, b))
         return end
