@@ -1110,3 +1110,24 @@ def test_wgrad_segments_batch_matches_single(env):
                                  (ctypes.c_void_p * 3)(*[b.data_ptr() for b in batch]), ns, s)
     for a, b in zip(single, batch):
         torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+
+
+def test_fence_free_timing_events_agree_with_torch_events(env):
+    """pdg/hiptimer.py's events (hipEventDisableSystemFence, used by the bench's per-kernel timing)
+    time a long stream of launches like torch.cuda.Event does, and nest in order."""
+    from pdg import hiptimer
+    x = torch.randn(4096, 4096, device="cuda")
+    torch.cuda.synchronize()
+    a, b = hiptimer.Event(), hiptimer.Event()
+    ta, tb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ta.record()
+    a.record()
+    for _ in range(20):
+        x = x @ x.T * 1e-3
+    b.record()
+    tb.record()
+    torch.cuda.synchronize()
+    ours, ref = a.elapsed_time(b), ta.elapsed_time(tb)
+    assert ours > 0 and ref > 0
+    assert ours <= ref * 1.02 + 0.05, (ours, ref)
+    assert abs(ours - ref) / ref < 0.1, (ours, ref)
