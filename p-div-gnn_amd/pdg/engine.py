@@ -461,15 +461,20 @@ class EPDEngine:
         st = ctx.stats
         segs: dict[str, list] = {k: [] for k in ("W2", "Wc", "Wa", "Wb", "Wn2", "Wn1a", "Wn1b", "d1", "ne2", "ee2")}
         fused = self.fused_edge_wgrad
-        if fused:
-            nse = self._nslabs_e
-            slabs_w2 = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
-            slabs_wc = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
         # LayerNorm backward scalars without finalize launches: every column-sum producer adds its
         # per-block rows into the group accumulator and writes per-block (S1, S2) pairs; the consumer
         # kernel reduces the pairs (include/pdivgnn.h, pdg_ln_colsum)
-        acc = self._ln_acc
-        acc.zero_()
+        if fused:
+            # one zero fill per backward for the three fused weight-gradient slab sets (W2, Wc, the edge
+            # encoder's W2) and the LayerNorm column-sum accumulators: four fill launches became one
+            nse = self._nslabs_e
+            nsl, nacc = nse * (L * L + L), self._ln_acc.numel()
+            zb = torch.zeros(3 * nsl + 2 * nacc, dtype=torch.float32, device=self.device)
+            slabs_w2, slabs_wc, slabs_ee = (zb[i * nsl:(i + 1) * nsl].view(nse, L * L + L) for i in range(3))
+            acc = zb[3 * nsl:].view(torch.float64).view(self._ln_acc.shape)
+        else:
+            acc = self._ln_acc
+            acc.zero_()
         reds = []   # deferred slab reductions (one pdg_wgrad_reduce_batch launch at the end)
         ACC_N, ACC_E, ACC_NE, ACC_EE = (acc[i] for i in range(4))
         S = ctx.steps
@@ -640,8 +645,7 @@ class EPDEngine:
         if E:
             pp, n_e = edge_ln_pairs(P_EENC, ge_next, ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"])
             pe, ne = src(pp, n_e if not fused else n_edge)
-            if fused:   # one pass: weight gradients in slabs, the 1 -> 128 layer's as per-block sums
-                slabs_ee = torch.zeros(nse, L * L + L, dtype=torch.float32, device=self.device)
+            if fused:   # one pass: weight gradients in slabs (zeroed above), the 1 -> 128 layer's as per-block sums
                 nsum = torch.empty(nse, 2 * L, dtype=torch.float64, device=self.device)
                 self._t("edge_enc_bwd", lib.pdg_edge_enc_bwd, E, _p(ge_next), _p(ctx.a2_ee), _p(ctx.e_in),
                         _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]), st[1], None, pe, ne,

@@ -87,6 +87,7 @@ class Trainer:
         self._table = None
         self._table_key = None
         self._nz_cache: dict = {}
+        self._consts: dict = {}
         # captured forward+backward per batch object (dp_mode="sync" reads counts on the host: eager)
         self.capture = capture and not self.sync
         self._graph = None            # (id(batch), torch.cuda.CUDAGraph, static outputs)
@@ -116,6 +117,16 @@ class Trainer:
             self._gt_cache = {key: ((batch.local_stress - m.mean_local_stress) / m.std_local_stress).float().contiguous()}
         return self._gt_cache[key]
 
+    def _const(self, v: float) -> torch.Tensor:
+        """A (1,) fp32 device tensor holding v, kept while v is unchanged (one fill launch fewer per step:
+        the loss normalisers only change with the batch's graph count or the penalty)."""
+        t = self._consts.get(v)
+        if t is None:
+            if len(self._consts) > 64:
+                self._consts.clear()
+            t = self._consts[v] = torch.full((1,), v, dtype=torch.float32, device=self.device)
+        return t
+
     def _nonzero_flag(self, batch) -> torch.Tensor:
         """1.0 when any mean stress of `batch` is nonzero, else 0.0 (a device scalar): the guard of
         models.py:294-299 without its host sync.  Cached per batch object while mean_stress is
@@ -127,7 +138,7 @@ class Trainer:
             flag = torch.zeros(1, dtype=torch.int32, device=self.device)
             msf = ms.float().contiguous()
             lib.pdg_any_nonzero(msf.data_ptr(), msf.numel(), flag.data_ptr(), stream_handle(self.device))
-            self._nz_cache = {"k": key, "v": flag.float(), "batch": batch}
+            self._nz_cache = {"k": key, "v": flag.float(), "zero": flag.eq(0).int(), "batch": batch}
         return self._nz_cache["v"]
 
     def step(self, batch) -> dict:
@@ -187,7 +198,7 @@ class Trainer:
         gt = self._gt(batch)
         loss_g, den = torch.empty(B, **f32), torch.empty(B, 3, **f32)
         lib.pdg_nmse_fwd(B, plan.ptr.data_ptr(), gt.data_ptr(), y.data_ptr(), loss_g.data_ptr(), den.data_ptr(), s)
-        scale = torch.full((1,), 1.0 / Bn, **f32)
+        scale = self._const(1.0 / Bn)
         gy = torch.empty(N, 3, **f32)
         lib.pdg_nmse_bwd(B, plan.ptr.data_ptr(), N, gt.data_ptr(), y.data_ptr(), den.data_ptr(), scale.data_ptr(), 0,
                          gy.data_ptr(), s)
@@ -200,7 +211,7 @@ class Trainer:
             lib.pdg_div_fwd(B, plan.ptr.data_ptr(), plan.a_rowptr.data_ptr(), plan.a_col.data_ptr(),
                             plan.a_val.data_ptr(), types.data_ptr(), y.data_ptr(), 0, div.data_ptr(),
                             loss_d.data_ptr(), s)
-            sd = torch.full((1,), self.penalty / Bn, **f32)
+            sd = self._const(self.penalty / Bn)
             lib.pdg_div_bwd(B, plan.ptr.data_ptr(), N, plan.at_rowptr.data_ptr(), plan.at_row.data_ptr(),
                             plan.at_comp.data_ptr(), plan.at_val.data_ptr(), div.data_ptr(), sd.data_ptr(), 0, 1,
                             gy.data_ptr(), s)
@@ -216,8 +227,8 @@ class Trainer:
         # non-finite one (parameters, moments and Adam's count unchanged; out["skipped"] = 1), decided
         # on the device.  Under data parallelism the flag rides in the gradient bucket, so the step is
         # skipped on every rank exactly when the GLOBAL minibatch is all zero, as one device would.
-        self._bucket[-1:].copy_(nz)
         if self.pg is not None:
+            self._bucket[-1:].copy_(nz)
             end = self._mark("allreduce")
             torch.distributed.all_reduce(self._bucket, group=self.pg)
             end()
@@ -233,7 +244,10 @@ class Trainer:
                 self.flat_g.mul_(1.0 / torch.distributed.get_world_size(self.pg))
         self._ensure_table(self._count_bound + 1)
         lib.pdg_nonfinite(self.flat_g.data_ptr(), self.flat_g.numel(), self._skip.data_ptr(), s)
-        self._skip.bitwise_or_(self._bucket[-1:].eq(0))
+        if self.pg is not None:   # the global minibatch's flag (summed over the ranks with the bucket)
+            self._skip.bitwise_or_(self._bucket[-1:].eq(0))
+        else:                     # one device: this batch's flag, cached with it (two launches fewer)
+            self._skip.bitwise_or_(self._nz_cache["zero"])
         lib.pdg_adam(self.flat_p.numel(), self.flat_p.data_ptr(), self.flat_g.data_ptr(), self.exp_avg.data_ptr(),
                      self.exp_avg_sq.data_ptr(), self._table.data_ptr(), self._table.shape[0],
                      float(1.0 - self.betas[0]), self.betas[1], float(1.0 - self.betas[1]), self.eps,
