@@ -56,8 +56,10 @@ PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd
              "edge_bwd": "void edge_bwd_kernel<true>",
              "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_x6_kernel", "node_net_pair_kernel", "node_net_kernel"),
              "pq_scatter_bwd": "pq_scatter_bwd_kernel",
-             "wgrad_W2": "wgrad_x6_kernel", "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
-             "edge_gout": "void edge_gout_wc_kernel<true>"}
+             "wgrad_W2": "wgrad_x6_kernel",
+             # the edge-update instantiations (template <EU, RC> / <RES, C2>; RC / C2 variants off by default)
+             "edge_bwd_w2": ("void edge_bwd_w2_kernel<true, false>", "void edge_bwd_w2_kernel<true>"),
+             "edge_gout": ("void edge_gout_wc_kernel<true, false>", "void edge_gout_wc_kernel<true>")}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
 PEAK_BF16_MFMA = 16 * PEAK_FP32_MFMA   # dense bf16 MFMA (2.5 PF; the fp32 rate is 1/16 of it, same guide)
 X6 = 6                      # bf16x6: six bf16 products per fp32-accurate product
