@@ -49,7 +49,9 @@ sys.path[:0] = [str(ROOT), str(ROOT / "p-div-gnn_amd")]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-PMC_FILE = ROOT / "profiles" / "r03_pmc_traffic.json"   # rocprofv3 --pmc of this bench (tools/gpu_measure.sh)
+# rocprofv3 --pmc of this bench (tools/final_pass.sh writes profiles/rNN_pmc_traffic.json with the tree it
+# measured under "_meta"); the bench takes traffic only from a file of ITS OWN tree (pmc_file())
+PMC_GLOB = "profiles/r*_pmc_traffic.json"
 TREE_GLOBS = ("p-div-gnn_amd/pdg/libpdivgnn_hip.so", "p-div-gnn_amd/csrc/*.hip", "p-div-gnn_amd/csrc/*.hpp", "include/*.h", "p-div-gnn_amd/pdg/*.py",
               "p-div-gnn_amd/gnn_local_stress/*.py", "bench.py")
 PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
@@ -57,9 +59,12 @@ PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd
              "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_x6_kernel", "node_net_pair_kernel", "node_net_kernel"),
              "pq_scatter_bwd": "pq_scatter_bwd_kernel",
              "wgrad_W2": "wgrad_x6_kernel",
-             # the edge-update instantiations (template <EU, RC> / <RES, C2>; RC / C2 variants off by default)
-             "edge_bwd_w2": ("void edge_bwd_w2_kernel<true, false>", "void edge_bwd_w2_kernel<true>"),
-             "edge_gout": ("void edge_gout_wc_kernel<true, false>", "void edge_gout_wc_kernel<true>")}
+             # the edge-update instantiations (template <EU, RC> / <RES, C2>: the recompute_a1 / gout_gz1
+             # variants are the <true, true> ones)
+             "edge_bwd_w2": ("void edge_bwd_w2_kernel<true, false>", "void edge_bwd_w2_kernel<true, true>",
+                             "void edge_bwd_w2_kernel<true>"),
+             "edge_gout": ("void edge_gout_wc_kernel<true, false>", "void edge_gout_wc_kernel<true, true>",
+                           "void edge_gout_wc_kernel<true>")}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
 PEAK_BF16_MFMA = 16 * PEAK_FP32_MFMA   # dense bf16 MFMA (2.5 PF; the fp32 rate is 1/16 of it, same guide)
 X6 = 6                      # bf16x6: six bf16 products per fp32-accurate product
@@ -269,17 +274,37 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
     }
 
 
+def pmc_file(tree: str | None = None):
+    """(path, None) of the newest profiles/rNN_pmc_traffic.json measured on this tree (its "_meta"
+    "tree" equals tree_hash()), or (None, reason).  PMC bytes of another tree would price a kernel's
+    launches with the bytes of different code, so they are never used."""
+    tree = tree or tree_hash()
+    files = sorted(ROOT.glob(PMC_GLOB), reverse=True)
+    if not files:
+        return None, "no profiles/r*_pmc_traffic.json"
+    seen = []
+    for f in files:
+        try:
+            t = json.loads(f.read_text()).get("_meta", {}).get("tree")
+        except (OSError, ValueError):
+            continue
+        if t == tree:
+            return f, None
+        seen.append(f"{f.name}: {t}")
+    return None, f"no PMC file of tree {tree} ({'; '.join(seen)})"
+
+
 def pmc_tree() -> str | None:
-    """Tree hash the PMC file was measured on (tools/gpu_measure.sh writes it under "_meta")."""
-    if not PMC_FILE.exists():
-        return None
-    return json.loads(PMC_FILE.read_text()).get("_meta", {}).get("tree")
+    """Tree hash of the PMC file the bench uses (None when no file matches this tree)."""
+    f, _ = pmc_file()
+    return json.loads(f.read_text())["_meta"]["tree"] if f else None
 
 
-def load_pmc(fused: bool) -> dict:
+def load_pmc(fused: bool, path=None) -> dict:
+    """Per-launch PMC bytes by kernel from `path` (a pmc_file() result; {} when None)."""
     pmc = {}
-    if PMC_FILE.exists():
-        data = json.loads(PMC_FILE.read_text())
+    if path is not None and Path(path).exists():
+        data = json.loads(Path(path).read_text())
         data.pop("_meta", None)
         for k, prefix in PMC_NAMES.items():
             if fused and k == "edge_bwd":
@@ -290,7 +315,7 @@ def load_pmc(fused: bool) -> dict:
     return pmc
 
 
-def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None):
+def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None, pmc_source=None):
     nlaunch = nlaunch or {}
     terms, nbytes = work[k]
     t = kt[k]
@@ -309,7 +334,8 @@ def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None):
             # real DRAM rate: the PMC bytes of a launch (profiles/, same tree when traffic_tree matches)
             # over this run's event-timed launch average, against 8 TB/s
             "frac_pmc": round(traffic / t / PEAK_HBM, 4) if traffic else None,
-            "traffic_source": (f"profiles/{PMC_FILE.name}: 2*FETCH_SIZE+WRITE_SIZE per dispatch" if k in pmc else None),
+            "traffic_source": (f"profiles/{Path(pmc_source).name}: 2*FETCH_SIZE+WRITE_SIZE per dispatch"
+                               if k in pmc and pmc_source else None),
             "flops_per_launch": flops, "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4),
             "frac_hbm": round(f_hbm, 4), "avg_launch_ms": round(t * 1e3, 4), "launches_timed": nlaunch.get(k),
             "share_of_step": round(ktot[k] / step_s, 4)}
@@ -391,8 +417,11 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
             with torch.no_grad():
                 return {"total": model(batch, scale_output=True).local_stress.abs().mean()}
     else:
+        # the global minibatch's graph count (every rank's losses are / B_global, pdg/trainer.py)
+        n_global = cfg["graphs"] if cfg.get("global_batch") else cfg["graphs"] * world
+
         def run_step():
-            return trainer.step(batch)
+            return trainer.step(batch, n_global_graphs=n_global if pg is not None else None)
     for _ in range(args.warmup):
         run_step()
     torch.cuda.synchronize()
@@ -442,7 +471,8 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     seg = getattr(eng, "seg_sums", False) if infer else getattr(eng, "seg_sums_train", False)
     rc = (not infer and E > 0 and eng.recompute_a1 and fused and eng.coop_fwd and not eng.seg_sums_train)
     work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg, rc)
-    pmc = load_pmc(fused) if with_pmc else {}
+    pmc_path, pmc_reason = pmc_file() if with_pmc else (None, "not collected for this config")
+    pmc = load_pmc(fused, pmc_path)
     step_s = el * ev_steps / args.steps
     dominant = max([k for k in ("edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])
     strong = bool(cfg.get("global_batch"))
@@ -462,10 +492,12 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
                    "final_loss": round(loss, 6), "hip_graph_steps": graph_steps,
                    "per_rank": per_rank_rec},
         "kernel_variants": eng.variants(),
-        "roofline": roofline(dominant, work, kt, ktot, step_s, pmc, nlaunch),
-        "roofline_gather_scatter": [roofline(k, work, kt, ktot, step_s, pmc, nlaunch)
+        "roofline": roofline(dominant, work, kt, ktot, step_s, pmc, nlaunch, pmc_path),
+        "roofline_gather_scatter": [roofline(k, work, kt, ktot, step_s, pmc, nlaunch, pmc_path)
                                     for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
-        "roofline_node_net": roofline("node_net", work, kt, ktot, step_s, pmc, nlaunch) if "node_net" in kt else None,
+        "roofline_node_net": (roofline("node_net", work, kt, ktot, step_s, pmc, nlaunch, pmc_path)
+                              if "node_net" in kt else None),
+        "traffic_null_reason": pmc_reason,
         "kernel_ms": {k: round(v * 1e3, 4) for k, v in kt.items()},
     }
     del trainer, model, batch, plan

@@ -12,7 +12,12 @@ the config in the results folder.  What runs underneath is MI355X-native:
   minibatch is collated on the device in one launch;
 * each training step is ``pdg.trainer.Trainer.step`` (HIP forward, fused NMSE + divergence
   loss, HIP backward, Adam stepped with GradScaler's skip semantics) with no host sync;
-* the test pass runs the HIP forward under ``no_grad`` and the fused batch loss.
+* the test pass runs the HIP forward under ``no_grad`` and the fused batch loss;
+* under ``torchrun`` (WORLD_SIZE > 1) it trains with graph-batch data parallelism, one process per
+  GPU: every rank draws the same reference-ordered global minibatches, takes its
+  ``pdg.dist.shard_minibatch`` share of each (whole graphs, balanced by node count), divides its
+  losses by the GLOBAL minibatch's graph count and the gradients are summed over RCCL, so every
+  graph weighs 1/B as in gnn_train.py:193/196.  Rank 0 logs and writes the checkpoints.
 
 Minibatches come from ``torch.utils.data.DataLoader`` objects over the graph indices
 (``pdg.graph.index_loader``; PyG's ``DataLoader`` is that same torch loader with a graph collate),
@@ -24,9 +29,11 @@ graphs in the reference's order (tests/test_train_order.py).  TensorBoard loggin
 (SURVEY §8); the losses they would log are printed and returned.
 
     python -m gnn_local_stress.train configs_train/config_train_div.yml
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m gnn_local_stress.train configs_train/config_train_div.yml
 """
 from __future__ import annotations
 
+import os
 import random
 import shutil
 import sys
@@ -36,7 +43,10 @@ from typing import Any
 import numpy as np
 import torch
 
+import torch.distributed as dist
+
 from pdg.collate import DeviceGraphStore
+from pdg.dist import shard_minibatch
 from pdg.graph import index_loader
 from pdg.trainer import Trainer
 
@@ -51,25 +61,42 @@ def make_loaders(train_store: DeviceGraphStore, test_store: DeviceGraphStore, ba
             index_loader(test_store.num_graphs, batch_size, shuffle=False))
 
 
-def evaluate(model, store: DeviceGraphStore, loader, monitor_divergence: bool):
+def evaluate(model, store: DeviceGraphStore, loader, monitor_divergence: bool, process_group=None,
+             shard: bool = True):
     """The test pass of gnn_train.py:208-252: sum over batches of (NMSE/B [+ div/B]) and of the
     divergence term (unpenalised, as the reference monitors it), as device scalars.  ``loader``
-    yields graph-index lists (an int batch size builds an unshuffled one)."""
+    yields graph-index lists (an int batch size builds an unshuffled one).
+
+    With a process group and ``shard`` (replica data parallelism), every rank evaluates its
+    ``shard_minibatch`` share of each test minibatch with its losses scaled to / B_global and the
+    two sums are all-reduced once at the end; without ``shard`` (dp_mode "sync") every rank
+    evaluates the whole minibatches, so the test loss is the one-device value on every rank."""
     if isinstance(loader, int):
         loader = index_loader(store.num_graphs, loader, shuffle=False)
     total = torch.zeros((), dtype=torch.float32, device=store.device)
     div_sum = torch.zeros((), dtype=torch.float32, device=store.device)
     nb = 0
+    world = dist.get_world_size(process_group) if process_group is not None else 1
+    rank = dist.get_rank(process_group) if process_group is not None else 0
     with torch.no_grad():
-        for batch in (store.batch(idx) for idx in loader):
+        for idx in loader:
+            nb += 1
+            mine = shard_minibatch(idx, store.n, world, rank) if (world > 1 and shard) else list(idx)
+            if not mine:
+                continue
+            batch = store.batch(mine)
             pred = model.forward(batch, scale_output=False, scale_input=True).local_stress
             gt = data_utils.standardize(batch.local_stress, model.mean_local_stress, model.std_local_stress)
             t, _, d = losses.batch_loss(pred, batch, gt.float().contiguous(), divergence=monitor_divergence,
                                         divergence_penalty=1.0)
-            total = total + t
+            w = len(mine) / len(idx)        # / B_local -> / B_global (1 without sharding)
+            total = total + (t * w if w != 1 else t)
             if monitor_divergence:
-                div_sum = div_sum + d
-            nb += 1
+                div_sum = div_sum + (d * w if w != 1 else d)
+    if world > 1 and shard:
+        sums = torch.stack([total, div_sum])
+        dist.all_reduce(sums, group=process_group)
+        total, div_sum = sums[0], sums[1]
     return total, div_sum, nb
 
 
@@ -77,14 +104,20 @@ def train(model: models.EncodeProcessDecode, train_store: DeviceGraphStore, test
           epochs: int, batch_size: int, learning_rate: float = 0.001, weights_folder: str = "",
           early_stopping_limit: int = 10, optimize_divergence: bool = True, divergence_penalty: float = 1.0,
           train_all_epochs: bool = False, monitor_divergence_in_test: bool = False,
-          log=print, loaders=None) -> tuple[list[float], list[float]]:
+          log=print, loaders=None, process_group=None, dp_mode: str = "replica") -> tuple[list[float], list[float]]:
     """gnn_train.py:95-305 (without TensorBoard).  ``loaders``: the (train, test) index loaders
-    (make_loaders; built here when omitted)."""
+    (make_loaders; built here when omitted).  ``process_group``: graph-batch data parallelism over
+    its ranks (module docstring; every rank calls this with the same arguments, rank 0 writes)."""
     train_loader, test_loader = loaders if loaders is not None else make_loaders(train_store, test_store, batch_size)
+    pg = process_group
+    world = dist.get_world_size(pg) if pg is not None else 1
+    rank = dist.get_rank(pg) if pg is not None else 0
+    writer = rank == 0
     trainer = Trainer(model, lr=learning_rate, divergence=optimize_divergence,
-                      divergence_penalty=divergence_penalty)
+                      divergence_penalty=divergence_penalty, process_group=pg, dp_mode=dp_mode)
     folder = Path(weights_folder)
-    folder.mkdir(parents=True, exist_ok=False)
+    if writer:
+        folder.mkdir(parents=True, exist_ok=False)
     best_path = folder / "model_weights.pth"
     last_path = folder / "last_epoch_model_weights.pth"
     log(f"Device = {train_store.device};\nBatch size = {batch_size};\nLearning rate = {learning_rate};\n"
@@ -106,22 +139,28 @@ def train(model: models.EncodeProcessDecode, train_store: DeviceGraphStore, test
         total_sum = torch.zeros((), dtype=torch.float32, device=dev)
         n_train = 0
         for idx in train_loader:
-            out = trainer.step(train_store.batch(idx))
+            if world == 1:
+                out = trainer.step(train_store.batch(idx))
+            else:   # this rank's share of the reference-ordered global minibatch, losses / B_global
+                mine = shard_minibatch(idx, train_store.n, world, rank)
+                out = trainer.step(train_store.batch(mine) if mine else None, n_global_graphs=len(idx))
             nmse_sum = nmse_sum + out["nmse"]
             total_sum = total_sum + out["total"]
             if optimize_divergence:
                 div_sum = div_sum + out["div"]
             n_train += 1
         model.eval()
-        test_total, test_div, n_test = evaluate(model, test_store, test_loader, monitor_divergence_in_test)
+        test_total, test_div, n_test = evaluate(model, test_store, test_loader, monitor_divergence_in_test,
+                                                process_group=pg, shard=dp_mode == "replica")
         # one host sync per epoch (the reference's .item() calls, gnn_train.py:258-275)
         vals = torch.stack([nmse_sum, total_sum, div_sum, test_total, test_div]).tolist()
         train_mse_loss = vals[0] / n_train
         total_loss = vals[1] / n_train
         test_loss = vals[3] / n_test
-        if test_loss < best_loss:
-            models.save_model_checkpoint(model, trainer, epoch + 1, best_path.as_posix())
-            log(f"Checkpoint saved at {best_path}")
+        if test_loss < best_loss:   # the same decision on every rank: the losses are global
+            if writer:
+                models.save_model_checkpoint(model, trainer, epoch + 1, best_path.as_posix())
+                log(f"Checkpoint saved at {best_path}")
             best_loss = test_loss
             early_stopping_counter = 0
         else:
@@ -135,8 +174,9 @@ def train(model: models.EncodeProcessDecode, train_store: DeviceGraphStore, test
         log(msg)
         train_losses.append(total_loss)
         test_losses.append(test_loss)
-    models.save_model_checkpoint(model, trainer, epoch + 1, last_path.as_posix())
-    log(f"Last checkpoint at epoch {epoch + 1} saved at {last_path}")
+    if writer:
+        models.save_model_checkpoint(model, trainer, epoch + 1, last_path.as_posix())
+        log(f"Last checkpoint at epoch {epoch + 1} saved at {last_path}")
     return train_losses, test_losses
 
 
@@ -145,9 +185,13 @@ def run_experience(dataset_train_csv: str, dataset_test_csv: str, results_folder
                    early_stopping_limit: int, learning_rate: float, message_passing_steps: int,
                    train_all_epochs: bool = False, device: str = "cuda", periodic_graph: bool = True,
                    monitor_divergence_in_test: bool = False, config_path: Path = Path(""), *args: Any,
-                   log=print, **kwargs: Any) -> tuple[list[float], list[float]]:
-    """gnn_train.py:331-435."""
+                   log=print, process_group=None, dp_mode: str = "replica",
+                   **kwargs: Any) -> tuple[list[float], list[float]]:
+    """gnn_train.py:331-435.  ``process_group``: graph-batch data parallelism (module docstring);
+    every rank builds the same datasets and loaders, only rank 0 logs and writes."""
     import pandas as pd
+    if process_group is not None and dist.get_rank(process_group) != 0:
+        log = _quiet
     log(f"DATASET TRAIN CSV {dataset_train_csv}\nDATASET TEST CSV {dataset_test_csv}\nEPOCHS {epochs}\n"
         f"BATCH SIZE {batch_size}\nLEARNING RATE {learning_rate}\nPeriodic graph {periodic_graph}")
     torch.manual_seed(SEED)
@@ -167,27 +211,60 @@ def run_experience(dataset_train_csv: str, dataset_test_csv: str, results_folder
         latent_size=latent_size, output_nodes_features_size=3,
         **{k: v.to(device) for k, v in train_dataset.stats().items()})
     loaders = make_loaders(train_store, test_store, batch_size)
-    log(models.print_model(model, loaders[0], device))
+    log(models.print_model(model, loaders[0], device))   # every rank: it draws from the loader's RNG
     model.to(device)
     results = Path(results_folder)
-    results.mkdir(parents=True, exist_ok=True)
-    if config_path and Path(config_path).is_file():
-        shutil.copyfile(config_path, results / Path(config_path).name)
+    writer = process_group is None or dist.get_rank(process_group) == 0
+    if writer:
+        results.mkdir(parents=True, exist_ok=True)
+        if config_path and Path(config_path).is_file():
+            shutil.copyfile(config_path, results / Path(config_path).name)
     return train(model=model, train_store=train_store, test_store=test_store, epochs=epochs,
                  batch_size=batch_size, learning_rate=learning_rate,
                  weights_folder=(results / "weights").as_posix(), early_stopping_limit=early_stopping_limit,
                  optimize_divergence=divergence, divergence_penalty=divergence_penalty,
                  train_all_epochs=train_all_epochs, monitor_divergence_in_test=monitor_divergence_in_test,
-                 log=log, loaders=loaders)
+                 log=log, loaders=loaders, process_group=process_group, dp_mode=dp_mode)
+
+
+def _quiet(*_a, **_k) -> None:
+    """The log of ranks other than 0."""
+
+
+def init_distributed(device: str = "cuda"):
+    """(process group, device) for a torchrun launch (WORLD_SIZE > 1): one process per GPU,
+    ``cuda:LOCAL_RANK``, backend RCCL ("nccl") unless PDG_DIST_BACKEND names another (gloo rehearses
+    several ranks on one GPU).  (None, device) for a single process."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return None, device
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    idx = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(idx)
+    dev = torch.device("cuda", idx)
+    backend = os.environ.get("PDG_DIST_BACKEND", "nccl")
+    if not dist.is_initialized():
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return dist.group.WORLD, dev
 
 
 def main(config_path: str, **overrides: Any):
-    """gnn_train.py:438-...: read the YAML config and run the experience."""
+    """gnn_train.py:438-...: read the YAML config and run the experience (under torchrun: graph-batch
+    data parallelism over the launched ranks; ``dp_mode`` "replica" or "sync" may be given as an
+    override or a config key)."""
     import yaml
     with open(config_path) as f:
         params = yaml.safe_load(f)
     params.update(overrides)
     params["config_path"] = Path(config_path)
+    if "process_group" not in params:
+        pg, dev = init_distributed(params.get("device", "cuda"))
+        if pg is not None:
+            params["process_group"], params["device"] = pg, dev
     return run_experience(**params)
 
 

@@ -1,21 +1,24 @@
 """Graph-batch data parallelism.
 
-One process per GPU.  A global minibatch of graphs is split into `world`
-shards, whole graphs only, balanced by node count; every rank runs the full
-forward/backward on its shard and the flat fp32 gradient bucket is averaged
-with one all-reduce (RCCL over xGMI on the GPU box, gloo in the CPU tests).
+One process per GPU.  Every global minibatch of graphs (the reference's loader order,
+gnn_train.py:387-394) is split into `world` shards, whole graphs only, balanced by node count;
+every rank runs the full forward/backward on its shard and the flat fp32 gradient bucket is
+SUMMED with one all-reduce (RCCL over xGMI on the GPU box, gloo in the CPU tests).
 
-Semantics ("replica", the default): each shard is normalised as its own batch
-(the loss is divided by the local batch size, gnn_train.py:193/196, and the
-graph-global LayerNorm statistics are those of the shard), and the gradients
-are averaged.  For equal shards this is the mean over shards of the gradient
-each shard would produce alone, which is what the tests check.  (The
-reference's LayerNorm normalises over the whole minibatch, so DP over B graphs
-equals one device over B graphs only for B_local = B; DESIGN.md.)
+Loss weighting: every rank divides its graphs' losses by the GLOBAL minibatch's graph count B,
+so each graph's gradient enters the sum with the reference's weight 1/B (gnn_train.py:193/196)
+whichever rank it landed on, also for unequal shards (an odd minibatch, graphs of different
+sizes, a last partial batch).  A rank that gets no graph contributes zeros.
+
+LayerNorm statistics ("replica", the default): each graph-global LayerNorm is normalised over the
+rank's own shard.  The reference normalises over the whole minibatch (models.py:42-55), so replica
+DP equals one device only for B_local = B; Trainer(dp_mode="sync") exchanges the statistics and is
+exact.
 """
 from __future__ import annotations
 
 import heapq
+from typing import Sequence
 
 import torch
 import torch.distributed as dist
@@ -36,8 +39,23 @@ def shard_graphs(node_counts, world: int) -> list[list[int]]:
     return [sorted(s) for s in shards]
 
 
+def shard_minibatch(indices: Sequence[int], node_counts: Sequence[int], world: int, rank: int) -> list[int]:
+    """This rank's graphs of one global minibatch: `indices` are the dataset indices the reference's
+    loader yields (in its order), `node_counts[i]` the size of dataset graph i.  The shards of all
+    ranks partition `indices`; each keeps the loader's relative order."""
+    pos = shard_graphs([node_counts[i] for i in indices], world)[rank]
+    return [int(indices[p]) for p in pos]
+
+
+def allreduce_sum_(flat: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place sum of a flat bucket over the process group (one collective)."""
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    return flat
+
+
 def allreduce_mean_(flat: torch.Tensor, group=None) -> torch.Tensor:
-    """In-place mean of a flat gradient bucket over the process group (one collective)."""
+    """In-place mean of a flat bucket over the process group (one collective)."""
     if not dist.is_available() or not dist.is_initialized():
         return flat
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)

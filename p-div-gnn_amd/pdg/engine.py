@@ -217,13 +217,11 @@ class EPDEngine:
         self.timed: dict | None = None
 
     def variants(self) -> dict:
-        """The kernel variants in effect (recorded in the bench line)."""
+        """The kernel variants in effect (recorded in the bench line): every VARIANTS entry, so a new
+        variant cannot be left out of the record."""
         cus = torch.cuda.get_device_properties(self.device).multi_processor_count
-        return {"fused_edge_wgrad": self.fused_edge_wgrad, "pq_first": self.pq_first, "coop_fwd": self.coop_fwd,
-                "seg_sums": self.seg_sums, "seg_sums_train": self.seg_sums_train, "gsum2_coop": self.gsum2_coop,
-                "nbwd_coop": self.nbwd_coop, "recompute_a1": self.recompute_a1,
-                "pair_blocks_per_cu": self._nslabs_p // cus,
-                "enc_blocks_per_cu": self._enc_blocks // cus}
+        derived = {"pair_blocks_per_cu": self._nslabs_p // cus, "enc_blocks_per_cu": self._enc_blocks // cus}
+        return {k: derived[k] if k in derived else getattr(self, k) for k in VARIANTS}
 
     def _t(self, name: str, fn, *args):
         """Launch fn(*args); when timing is enabled for `name`, bracket it with HIP events

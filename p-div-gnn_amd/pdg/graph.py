@@ -186,11 +186,14 @@ class DataLoader(torch.utils.data.DataLoader):
     ``torch.utils.data.DataLoader`` whose collate is ``Batch.from_data_list``.  Being the torch
     loader itself, it draws from torch's global RNG exactly as the reference's loaders do (one
     base seed per iterator, plus the RandomSampler's seed when shuffling), so a seeded run visits
-    the graphs in the reference's order."""
+    the graphs in the reference's order.  As in PyG, the collate is fixed: a ``collate_fn`` is
+    refused (TypeError) rather than silently replaced."""
 
     def __init__(self, dataset, batch_size: int = 1, shuffle: bool = False,
                  generator: torch.Generator | None = None, **kwargs: Any) -> None:
-        kwargs.pop("collate_fn", None)
+        if "collate_fn" in kwargs:
+            raise TypeError("pdg.graph.DataLoader collates with Batch.from_data_list (as PyG's DataLoader); "
+                            "it takes no collate_fn")
         super().__init__(dataset, batch_size=batch_size, shuffle=shuffle, generator=generator,
                          collate_fn=Batch.from_data_list, **kwargs)
 

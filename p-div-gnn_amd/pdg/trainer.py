@@ -5,12 +5,16 @@ Per step (one minibatch already resident in HBM):
   target   standardize(local_stress, mean/std_local_stress)                (:162-167)
   loss     sum_g NMSE_g / B  [+ lambda * sum_g div_g / B]                  (:168-197)
   backward                                                                 (:205)
-  DP       one all-reduce (mean) of the flat fp32 gradient bucket over RCCL (graph-batch data
-           parallelism across GPUs; new in this build).  dp_mode="sync" instead
-           reproduces one device running the whole global minibatch: every graph-LayerNorm
-           all-reduces its (sum, sumsq) pair in the forward and its (S1, S2) pair in the
-           backward, the loss is divided by the GLOBAL number of graphs and the gradient
-           bucket is summed, not averaged (2 x 47 sixteen-byte collectives more per step).
+  DP       one all-reduce (sum) of the flat fp32 gradient bucket over RCCL (graph-batch data
+           parallelism across GPUs; new in this build).  Every rank divides its
+           graphs' losses by the GLOBAL minibatch's graph count, so each graph weighs 1/B in the
+           summed gradient whatever rank it landed on and however unequal the shards are (the
+           reference's 1/B, gnn_train.py:193/196).  The bucket also carries the zero-stress flag
+           and the two loss partials, so the reported losses are the global minibatch's with no
+           further collective.  dp_mode="replica" (default) normalises each graph-LayerNorm over
+           the rank's own shard; dp_mode="sync" reproduces one device running the whole global
+           minibatch: every graph-LayerNorm all-reduces its (sum, sumsq) pair in the forward and
+           its (S1, S2) pair in the backward (2 x 47 sixteen-byte collectives more per step).
   update   Adam(lr, betas=(0.9, 0.999), eps=1e-8) on the flat parameter buffer (:118, :206),
            stepped as GradScaler.step does it (:204-207): a step whose gradient holds an inf/NaN
            leaves parameters, moments and Adam's step count unchanged.  The step count lives
@@ -61,8 +65,9 @@ class Trainer:
         total = sum(sizes)
         self.flat_p = torch.empty(total, dtype=torch.float32, device=dev)
         # the all-reduced bucket: every parameter gradient, then one slot holding 1.0 when this rank's
-        # batch has a nonzero mean stress (the zero-mean-stress guard of models.py:294-299, below)
-        self._bucket = torch.zeros(total + 1, dtype=torch.float32, device=dev)
+        # batch has a nonzero mean stress (the zero-mean-stress guard of models.py:294-299, below), then
+        # this rank's shares of the global minibatch's NMSE and divergence terms
+        self._bucket = torch.zeros(total + 3, dtype=torch.float32, device=dev)
         self.flat_g = self._bucket[:total]
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -118,12 +123,12 @@ class Trainer:
         return self._gt_cache[key]
 
     def _const(self, v: float) -> torch.Tensor:
-        """A (1,) fp32 device tensor holding v, kept while v is unchanged (one fill launch fewer per step:
-        the loss normalisers only change with the batch's graph count or the penalty)."""
+        """A (1,) fp32 device tensor holding v, kept for the trainer's lifetime (one fill launch fewer per
+        step: the loss normalisers only change with the batch's graph count or the penalty, so the
+        cache holds a few entries per distinct minibatch size).  Never evicted: a captured HIP graph
+        reads these tensors by address."""
         t = self._consts.get(v)
         if t is None:
-            if len(self._consts) > 64:
-                self._consts.clear()
             t = self._consts[v] = torch.full((1,), v, dtype=torch.float32, device=self.device)
         return t
 
@@ -132,31 +137,63 @@ class Trainer:
         models.py:294-299 without its host sync.  Cached per batch object while mean_stress is
         unchanged (bench / training re-use resident batches)."""
         ms = batch.mean_stress
-        key = (id(batch), id(ms), ms._version)
-        hit = self._nz_cache.get("k")
-        if hit != key:
+        c = self._nz_cache
+        # identity, not id(): the entry holds the batch and its mean_stress tensor, so neither can be
+        # freed and its id reused by another tensor while the entry lives
+        if not (c and c["batch"] is batch and c["ms"] is ms and c["ver"] == ms._version):
             flag = torch.zeros(1, dtype=torch.int32, device=self.device)
             msf = ms.float().contiguous()
             lib.pdg_any_nonzero(msf.data_ptr(), msf.numel(), flag.data_ptr(), stream_handle(self.device))
-            self._nz_cache = {"k": key, "v": flag.float(), "zero": flag.eq(0).int(), "batch": batch}
+            self._nz_cache = {"batch": batch, "ms": ms, "ver": ms._version, "v": flag.float(),
+                              "zero": flag.eq(0).int()}
         return self._nz_cache["v"]
 
-    def step(self, batch) -> dict:
+    def _global_graphs(self, B: int) -> int:
+        """Graphs in the global minibatch when the caller did not say (one small all-reduce and a
+        host read; the harness and the bench pass it)."""
+        t = torch.tensor([B], dtype=torch.float64, device=self.device)
+        torch.distributed.all_reduce(t, group=self.pg)
+        return int(t.item())
+
+    def step(self, batch, n_global_graphs: int | None = None) -> dict:
         """One optimisation step; returns device scalars (no host sync, except one read of the
-        global row counts in dp_mode="sync")."""
+        global row counts in dp_mode="sync", or of the global graph count when a process group is
+        set and `n_global_graphs` is not given).
+
+        `n_global_graphs`: graphs in the global minibatch this rank's `batch` is a shard of (the
+        loss normaliser B of gnn_train.py:193/196); defaults to the batch's own count on one device.
+        `batch=None` under a process group: this rank got no graph of the minibatch; it contributes
+        zero gradient and zero loss to the collective and takes the same Adam step as every rank."""
         m = self.model
         s = stream_handle(self.device)
+        f32 = dict(dtype=torch.float32, device=self.device)
+        if batch is None:
+            if self.pg is None or self.sync:
+                raise ValueError("batch=None (an empty shard) needs a process group in dp_mode='replica'")
+            if n_global_graphs is None:
+                n_global_graphs = self._global_graphs(0)
+            self.flat_g.zero_()
+            zero = torch.zeros((), **f32)
+            out = {"nmse": zero}
+            if self.divergence:
+                out["div"] = zero
+            return self._update(out, f32, s, torch.zeros(1, **f32))
         plan = plan_for(batch)
         stats8 = m.stats_tensor(self.device)
         B, N = plan.n_graphs, plan.n_nodes
-        f32 = dict(dtype=torch.float32, device=self.device)
         Bn = B                                      # loss normaliser (gnn_train.py:193/196)
+        if self.pg is not None and not self.sync:
+            Bn = int(n_global_graphs) if n_global_graphs is not None else self._global_graphs(B)
+            if Bn < B:
+                raise ValueError(f"n_global_graphs={Bn} is smaller than this rank's {B} graphs")
         if self.sync:
             cnt = torch.tensor([N, plan.n_edges, B], dtype=torch.float64, device=self.device)
             end = self._mark("sync_collective")
             torch.distributed.all_reduce(cnt, group=self.pg)
             end()
             n_g, e_g, Bn = (int(v) for v in cnt.tolist())
+            if n_global_graphs is not None and int(n_global_graphs) != Bn:
+                raise ValueError(f"n_global_graphs={n_global_graphs} but the ranks hold {Bn} graphs")
             self.engine.set_sync(self.pg, n_g, e_g)
         try:
             if self.capture:
@@ -228,24 +265,25 @@ class Trainer:
         # on the device.  Under data parallelism the flag rides in the gradient bucket, so the step is
         # skipped on every rank exactly when the GLOBAL minibatch is all zero, as one device would.
         if self.pg is not None:
-            self._bucket[-1:].copy_(nz)
+            # every rank's loss is already / B_global: the bucket is SUMMED (gradients and the loss
+            # shares), so unequal shards keep the reference's 1/B weighting of every graph
+            self._bucket[-3:-2].copy_(nz)
+            self._bucket[-2:-1].copy_(out["nmse"].reshape(1))
+            if "div" in out:
+                self._bucket[-1:].copy_(out["div"].reshape(1))
+            else:
+                self._bucket[-1:].zero_()
             end = self._mark("allreduce")
             torch.distributed.all_reduce(self._bucket, group=self.pg)
             end()
-            if self.sync:                           # per-rank shares of the global-batch loss: sum
-                parts = torch.stack([out["nmse"], out.get("div", torch.zeros((), **f32))])
-                end = self._mark("sync_collective")
-                torch.distributed.all_reduce(parts, group=self.pg)
-                end()
-                out["nmse"] = parts[0]
-                if "div" in out:
-                    out["div"] = parts[1]
-            else:
-                self.flat_g.mul_(1.0 / torch.distributed.get_world_size(self.pg))
+            parts = self._bucket[-2:].clone()       # (the bucket is rewritten by the next step)
+            out["nmse"] = parts[0]
+            if "div" in out:
+                out["div"] = parts[1]
         self._ensure_table(self._count_bound + 1)
         lib.pdg_nonfinite(self.flat_g.data_ptr(), self.flat_g.numel(), self._skip.data_ptr(), s)
         if self.pg is not None:   # the global minibatch's flag (summed over the ranks with the bucket)
-            self._skip.bitwise_or_(self._bucket[-1:].eq(0))
+            self._skip.bitwise_or_(self._bucket[-3:-2].eq(0))
         else:                     # one device: this batch's flag, cached with it (two launches fewer)
             self._skip.bitwise_or_(self._nz_cache["zero"])
         lib.pdg_adam(self.flat_p.numel(), self.flat_p.data_ptr(), self.flat_g.data_ptr(), self.exp_avg.data_ptr(),

@@ -1,0 +1,50 @@
+"""bench.py takes PMC traffic only from a profiles/ file measured on its own tree:
+a file whose "_meta" tree differs is ignored and the line says why, so frac_pmc never prices a
+kernel's launches with another tree's bytes."""
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT)]
+
+import bench  # noqa: E402
+
+NAME = "void edge_fwd_coop_kernel<true, true, false>(int, ...)"
+
+
+def _write(d: Path, name: str, tree: str, total: float) -> Path:
+    (d / "profiles").mkdir(exist_ok=True)
+    p = d / "profiles" / name
+    p.write_text(json.dumps({"_meta": {"tree": tree}, NAME: {"total": total}}))
+    return p
+
+
+def test_pmc_file_of_another_tree_is_ignored(tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    _write(tmp_path, "r07_pmc_traffic.json", "aaaa", 1.0e9)
+    path, reason = bench.pmc_file("bbbb")
+    assert path is None
+    assert "bbbb" in reason and "aaaa" in reason
+    assert bench.load_pmc(True, path) == {}
+
+
+def test_pmc_file_of_this_tree_is_used(tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    _write(tmp_path, "r08_pmc_traffic.json", "aaaa", 2.0e9)           # newer, but another tree
+    good = _write(tmp_path, "r07_pmc_traffic.json", "bbbb", 1.5e9)
+    path, reason = bench.pmc_file("bbbb")
+    assert path == good and reason is None
+    assert bench.load_pmc(True, path)["edge_fwd"] == 1_500_000_000
+
+
+def test_no_pmc_file(tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    path, reason = bench.pmc_file("bbbb")
+    assert path is None and "no profiles" in reason
+
+
+def test_roofline_without_traffic_has_no_pmc_fraction():
+    work = {"edge_fwd": ([(1e9, bench.PEAK_FP32_MFMA)], 1.0e9)}
+    r = bench.roofline("edge_fwd", work, {"edge_fwd": 2e-4}, {"edge_fwd": 2e-3}, 8e-3, {}, {"edge_fwd": 10}, None)
+    assert r["traffic"] is None and r["frac_pmc"] is None and r["traffic_source"] is None

@@ -1,8 +1,10 @@
-"""Graph-batch DP on CPU with gloo, world_size 2: the all-reduced
-flat gradient bucket equals the mean of the per-shard gradients, each shard
-computed as its own batch (replica semantics).  The per-shard gradients come
-from the CPU oracle (test infrastructure); the DP logic under test is
-pdg.dist (sharding + flat-bucket all-reduce), the same code the GPU Trainer uses."""
+"""Graph-batch DP on CPU with gloo, world_size 2: every rank's shard loss is divided
+by the GLOBAL minibatch's graph count and the flat gradient buckets are summed, so on an odd
+minibatch of unequal graphs (shards of 2 and 1 graphs) every graph still weighs 1/B
+(gnn_train.py:193/196).  The per-shard gradients come from the CPU oracle (test infrastructure);
+the DP logic under test is pdg.dist (sharding, the flat-bucket all-reduce), the same code the GPU
+Trainer and the training harness use.  Also: the harness's per-rank share of every reference
+minibatch (pdg.dist.shard_minibatch) partitions it in the loader's order."""
 import os
 import socket
 
@@ -20,7 +22,7 @@ def _free_port():
     return p
 
 
-def _shard_grads(samples, idx):
+def _shard_grads(samples, idx, b_global=None):
     from oracle import epd_oracle as O
     from pdg import graph
     from pdg.engine import PARAM_NAMES
@@ -37,6 +39,8 @@ def _shard_grads(samples, idx):
     gt = (b.local_stress.double() - st["mean_local_stress"]) / st["std_local_stress"]
     total, _, _ = O.batch_loss(pred, gt, b.ptr, [d.op_div_matrix.double() for d in datas], b.nodes_types,
                                True, 10.0)
+    if b_global is not None:        # / B_global instead of / B_shard
+        total = total * (len(idx) / b_global)
     total.backward()
     return torch.cat([P[n].grad.reshape(-1) for n in PARAM_NAMES])
 
@@ -50,19 +54,21 @@ def _worker(rank, world, port, q):
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from pdg import meshgen
-    from pdg.dist import allreduce_mean_, shard_graphs
-    samples = meshgen.make_dataset(4, n=7, hole_radius=(0.0, 0.0), seed=9)
+    from pdg.dist import allreduce_sum_, shard_graphs
+    samples = meshgen.make_dataset(3, n=7, hole_radius=(0.1, 0.3), seed=9)
+    B = len(samples)
     shards = shard_graphs([s.num_nodes for s in samples], world)
-    flat = _shard_grads(samples, shards[rank])
-    allreduce_mean_(flat)
+    assert sorted(len(s) for s in shards) == [1, 2]
+    flat = _shard_grads(samples, shards[rank], B)
+    allreduce_sum_(flat)
     if rank == 0:
-        ref = sum(_shard_grads(samples, s) for s in shards) / world
+        ref = sum(_shard_grads(samples, s, B) for s in shards)
         q.put(float((flat - ref).abs().max() / ref.abs().max()))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_dp_allreduce_equals_mean_of_shard_gradients():
+def test_dp_allreduce_sums_shard_gradients_over_global_batch():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -74,3 +80,26 @@ def test_dp_allreduce_equals_mean_of_shard_gradients():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert err < 1e-12
+
+
+def test_shard_minibatch_partitions_reference_batches():
+    """Every rank's graphs of every minibatch the reference's loader yields (the seeded torch
+    DataLoader order, gnn_train.py:387-394): disjoint, together the whole minibatch, each in the
+    loader's order, balanced by node count (max shard within the largest graph of the mean)."""
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "p-div-gnn_amd")]
+    from pdg.dist import shard_minibatch
+    from pdg.graph import index_loader
+    gen = torch.Generator().manual_seed(5)
+    counts = [int(c) for c in torch.randint(300, 2000, (23,), generator=gen)]
+    for world in (1, 2, 3, 4, 8):
+        torch.manual_seed(69)
+        for idx in index_loader(len(counts), 7, shuffle=True):
+            parts = [shard_minibatch(idx, counts, world, r) for r in range(world)]
+            assert sorted(i for p in parts for i in p) == sorted(idx)
+            for p in parts:
+                assert p == [i for i in idx if i in p]          # the loader's relative order
+            loads = [sum(counts[i] for i in p) for p in parts]
+            assert max(loads) <= sum(loads) / world + max(counts[i] for i in idx)

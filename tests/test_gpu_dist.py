@@ -3,9 +3,12 @@
 Both ranks run pdg.trainer.Trainer on cuda:0 with a gloo process group (RCCL
 refuses two ranks on one device; the Trainer's collective is the same
 `all_reduce` either way).  Checked: the all-reduced flat gradient bucket equals
-the mean of the per-shard fp64 oracle gradients (dp_mode "replica") or the fp64
-oracle gradient of the whole global minibatch on one device (dp_mode "sync",
-graph-LayerNorm statistics exchanged), and the parameters stay bit-identical
+the sum over shards of the fp64 oracle's shard gradients with every shard's loss
+divided by the GLOBAL graph count (dp_mode "replica": each graph weighs 1/B as in
+gnn_train.py:193/196, also for the odd 3-graph minibatch of unequal graphs whose
+shards hold 2 and 1 graphs) or the fp64 oracle gradient of the whole global
+minibatch on one device (dp_mode "sync", graph-LayerNorm statistics exchanged);
+the reported loss is the global minibatch's; the parameters stay bit-identical
 across ranks after several Adam steps.
 """
 import os
@@ -63,8 +66,12 @@ def _worker(rank, world, port, q, mode):
         from pdg import graph, meshgen
         from pdg.dist import shard_graphs
         from pdg.trainer import Trainer
-        samples = meshgen.make_dataset(4, n=9, hole_radius=(0.0, 0.0), seed=11)
+        if mode == "replica_unequal":   # three hole plates of different sizes: shards of 2 and 1 graphs
+            samples = meshgen.make_dataset(3, n=9, hole_radius=(0.1, 0.3), seed=11)
+        else:
+            samples = meshgen.make_dataset(4, n=9, hole_radius=(0.0, 0.0), seed=11)
         shards = shard_graphs([s.num_nodes for s in samples], world)
+        B = len(samples)
         batch = graph.Batch.from_data_list([graph.sample_to_data(samples[i]) for i in shards[rank]]).to(dev)
         torch.manual_seed(69)
         model = EncodeProcessDecode(input_edges_features_size=1, message_passing_steps=STEPS_MP, latent_size=128,
@@ -72,13 +79,13 @@ def _worker(rank, world, port, q, mode):
                                     **{k: torch.tensor(v) for k, v in STATS.items()}).to(dev)
         P0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
         tr = Trainer(model, lr=1e-3, divergence=True, divergence_penalty=10.0, process_group=dist.group.WORLD,
-                     dp_mode=mode)
-        out = tr.step(batch)
+                     dp_mode="sync" if mode == "sync" else "replica")
+        out = tr.step(batch, n_global_graphs=B)
         torch.cuda.synchronize()
         g = tr.flat_g.detach().double().cpu()
         loss = float(out["total"])
         for _ in range(3):
-            tr.step(batch)
+            tr.step(batch, n_global_graphs=B)
         torch.cuda.synchronize()
         p = tr.flat_p.detach().cpu()
         ps = [torch.empty_like(p) for _ in range(world)]
@@ -86,10 +93,11 @@ def _worker(rank, world, port, q, mode):
         if rank == 0:
             if mode == "sync":
                 ref, ref_loss = _oracle_grads(P0, samples, sorted(i for s in shards for i in s))
-            else:
+            else:   # every shard's loss / B_global: its batch_loss (/ B_shard) scaled by B_shard / B
+                assert len({len(s) for s in shards}) == (2 if mode == "replica_unequal" else 1), shards
                 rs = [_oracle_grads(P0, samples, s) for s in shards]
-                ref = sum(r[0] for r in rs) / world
-                ref_loss = rs[0][1]                    # replica: rank 0 reports its own shard's loss
+                ref = sum(r[0] * (len(s) / B) for r, s in zip(rs, shards))
+                ref_loss = sum(r[1] * (len(s) / B) for r, s in zip(rs, shards))
             q.put((float((g - ref).norm() / ref.norm()), max(float((x - ps[0]).abs().max()) for x in ps),
                    abs(loss - ref_loss) / abs(ref_loss)))
         dist.barrier()
@@ -97,7 +105,7 @@ def _worker(rank, world, port, q, mode):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["replica", "sync"])
+@pytest.mark.parametrize("mode", ["replica", "replica_unequal", "sync"])
 def test_trainer_dp_world2_on_one_gpu(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

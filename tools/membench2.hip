@@ -1,0 +1,224 @@
+// Streaming ceiling for the exact row mix of the edge forward (not part of the library; VERDICT r03
+// "reconcile the streaming ceiling"): per edge R streamed 512-B row reads, G gathered 512-B rows from
+// two node-sized tables (P / Q: N = E / 6 rows each, the edge forward's P[dst], Q[src], P[src], Q[dst]
+// with dst-sorted edges, so the gathers are mostly L2 hits) and W streamed 512-B row writes.
+//
+// Persistent blocks own contiguous row ranges and walk them in 32-row rounds (the edge kernels'
+// layout: whole-row access, 16 B per lane, a wave instruction covers 2 rows); the loads of DEPTH
+// rounds are in flight (a register ring, the next round's gathers issued a round ahead when
+// DEPTH > 1); stores default or nontemporal.  Swept: DEPTH 1..3, 8 or 16 waves per CU (1 or 2
+// blocks of 512 threads), default / nt stores, the edge forward's 2R + 4G + 5W and its parts.  A
+// grid-stride float4 copy over 1 GiB arrays (the guide's "float4 copy", MI355X_MICROARCH.md:36)
+// anchors the table.  No compute: this is the memory system's rate for the shape, the floor under
+// the kernel.
+//
+//   hipcc -O3 --offload-arch=gfx950 -o tools/membench2 tools/membench2.hip && tools/membench2
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int L = 128;
+constexpr int ROUND = 32;
+constexpr int THREADS = 512;
+constexpr int U = ROUND * 32 / THREADS;   // row slots per thread per round (2)
+
+__device__ __forceinline__ int clampr(int r, int r1) { return r < r1 ? r : r1 - 1; }
+
+template <int R, int G, int W, int DEPTH, bool NT, int BPC>
+__global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC, 2 * BPC))) void mix(const float* const* __restrict__ in, float* const* __restrict__ out,
+                                               const int* __restrict__ gd, const int* __restrict__ gs,
+                                               const float* __restrict__ P, const float* __restrict__ Q, int E) {
+  const int nb = gridDim.x;
+  int per = (E + nb - 1) / nb;
+  per = (per + ROUND - 1) / ROUND * ROUND;
+  const int r0 = min(E, per * (int)blockIdx.x), r1 = min(E, per * ((int)blockIdx.x + 1));
+  if (r0 >= r1) return;
+  const int t = threadIdx.x, c = 4 * (t & 31), rr = t >> 5;
+  constexpr int RG = R > 0 ? R : 1;
+  constexpr int GG = G > 0 ? G : 1;
+  f32x4 v[DEPTH][RG][U];
+  int di[DEPTH][U], si[DEPTH][U];
+  f32x4 g[DEPTH][GG][U];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int s, int base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = clampr(base + rr + 16 * u, r1);
+#pragma unroll
+      for (int a = 0; a < R; ++a) v[s][a][u] = *reinterpret_cast<const f32x4*>(in[a] + (size_t)row * L + c);
+      if (G) {
+        di[s][u] = gd[row];
+        si[s][u] = gs[row];
+      }
+    }
+  };
+  auto gather = [&](int gslot, int s) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int a = 0; a < G; ++a) {
+        const float* tb = (a & 1) ? Q : P;
+        const int node = ((a >> 1) ^ (a & 1)) ? si[s][u] : di[s][u];
+        g[gslot][a][u] = *reinterpret_cast<const f32x4*>(tb + (size_t)node * L + c);
+      }
+  };
+#pragma unroll
+  for (int s = 0; s < DEPTH; ++s) issue(s, r0 + ROUND * s);
+  if (G && DEPTH > 1) gather(0, 0);
+  for (int base = r0; base < r1; base += DEPTH * ROUND) {
+#pragma unroll
+    for (int s = 0; s < DEPTH; ++s) {
+      const int b = base + ROUND * s;
+      // DEPTH > 1: round b's gathers were issued a round ahead (slot s); the next round's now
+      if (G && DEPTH == 1) gather(0, 0);
+      if (G && DEPTH > 1) gather((s + 1) % DEPTH, (s + 1) % DEPTH);
+      f32x4 x = acc;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int a = 0; a < R; ++a) x += v[s][a][u];
+#pragma unroll
+        for (int a = 0; a < G; ++a) x += g[s][a][u];
+      }
+      acc = x;
+      issue(s, b + DEPTH * ROUND);   // clamped past r1
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = clampr(b + rr + 16 * u, r1);
+#pragma unroll
+        for (int a = 0; a < W; ++a) {
+          f32x4* p = reinterpret_cast<f32x4*>(out[a] + (size_t)row * L + c);
+          const f32x4 y = x + (float)a;
+          if (NT) __builtin_nontemporal_store(y, p);
+          else *p = y;
+        }
+      }
+    }
+  }
+  if (W == 0 && acc[0] == 123.456f) out[0][0] = acc[1];   // keep the loads live
+}
+
+__global__ void copy4(const f32x4* __restrict__ a, f32x4* __restrict__ b, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
+}
+
+struct Bufs {
+  float** d_in;
+  float** d_out;
+  int* gd;
+  int* gs;
+  float* P;
+  float* Q;
+  int E;
+  int N;
+};
+
+template <typename F>
+double time_us(F launch, int reps = 20) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&b);
+  for (int i = 0; i < 3; ++i) launch();
+  (void)hipEventRecord(a);
+  for (int i = 0; i < reps; ++i) launch();
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, a, b);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return ms * 1e3 / reps;
+}
+
+template <int R, int G, int W, int DEPTH, bool NT, int BPC = 1>
+void run(const Bufs& B, int cus) {
+  const int blocks_per_cu = BPC;
+  const int nblk = cus * blocks_per_cu;
+  const double us = time_us([&] {
+    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out, B.gd, B.gs, B.P,
+                       B.Q, B.E);
+  });
+  const double streamed = (double)B.E * 512.0 * (R + W);
+  const double gathered = (double)B.E * 512.0 * G;
+  printf("{\"mix\": \"%dR+%dG+%dW\", \"depth\": %d, \"waves_per_cu\": %d, \"stores\": \"%s\", \"us\": %.1f, "
+         "\"streamed_TBps\": %.3f, \"with_gathers_TBps\": %.3f}\n",
+         R, G, W, DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
+         (streamed + gathered) / us * 1e-6);
+  fflush(stdout);
+}
+
+int main() {
+  const int E = 239744;   // config 2's edges
+  const int N = 40328;    // config 2's nodes
+  int cus = 0;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+  std::vector<float*> bufs(14);
+  for (auto& p : bufs) {
+    (void)hipMalloc(&p, (size_t)E * 512);
+    (void)hipMemset(p, 0, (size_t)E * 512);
+  }
+  Bufs B{};
+  B.E = E;
+  B.N = N;
+  (void)hipMalloc(&B.d_in, 7 * sizeof(float*));
+  (void)hipMalloc(&B.d_out, 7 * sizeof(float*));
+  (void)hipMemcpy(B.d_in, bufs.data(), 7 * sizeof(float*), hipMemcpyHostToDevice);
+  (void)hipMemcpy(B.d_out, bufs.data() + 7, 7 * sizeof(float*), hipMemcpyHostToDevice);
+  // dst-sorted edges of a periodic 71 x 71-like mesh: ~6 per node, sources at mesh-neighbour offsets
+  std::vector<int> hd(E), hs(E);
+  const int offs[6] = {1, -1, 71, -71, 72, -72};
+  for (int e = 0; e < E; ++e) {
+    hd[e] = (int)((long long)e * N / E);
+    hs[e] = ((hd[e] + offs[e % 6]) % N + N) % N;
+  }
+  (void)hipMalloc(&B.gd, E * sizeof(int));
+  (void)hipMalloc(&B.gs, E * sizeof(int));
+  (void)hipMemcpy(B.gd, hd.data(), E * sizeof(int), hipMemcpyHostToDevice);
+  (void)hipMemcpy(B.gs, hs.data(), E * sizeof(int), hipMemcpyHostToDevice);
+  (void)hipMalloc(&B.P, (size_t)N * 512);
+  (void)hipMalloc(&B.Q, (size_t)N * 512);
+  (void)hipMemset(B.P, 0, (size_t)N * 512);
+  (void)hipMemset(B.Q, 0, (size_t)N * 512);
+
+  {  // the guide's anchor: grid-stride float4 copy over 1 GiB arrays
+    const size_t n = (size_t)1 << 26;   // f32x4 elements = 1 GiB
+    f32x4 *a, *b;
+    (void)hipMalloc(&a, n * 16);
+    (void)hipMalloc(&b, n * 16);
+    (void)hipMemset(a, 0, n * 16);
+    (void)hipMemset(b, 0, n * 16);
+    const double us = time_us([&] { hipLaunchKernelGGL(copy4, dim3(cus * 16), dim3(256), 0, 0, a, b, n); }, 10);
+    printf("{\"mix\": \"copy 1 GiB float4 grid-stride\", \"us\": %.1f, \"streamed_TBps\": %.3f}\n", us,
+           2.0 * n * 16 / us * 1e-6);
+    (void)hipFree(a);
+    (void)hipFree(b);
+  }
+  // the edge forward's mix, swept
+  run<2, 4, 5, 1, true>(B, cus);
+  run<2, 4, 5, 1, false>(B, cus);
+  run<2, 4, 5, 2, true>(B, cus);
+  run<2, 4, 5, 2, false>(B, cus);
+  run<2, 4, 5, 3, true>(B, cus);
+  run<2, 4, 5, 1, true, 2>(B, cus);
+  run<2, 4, 5, 1, false, 2>(B, cus);
+  // without the gathers, and the pure directions
+  run<2, 0, 5, 1, true>(B, cus);
+  run<2, 0, 5, 2, true>(B, cus);
+  run<2, 0, 5, 2, true, 2>(B, cus);
+  run<2, 0, 5, 2, false, 2>(B, cus);
+  run<7, 0, 0, 2, true>(B, cus);
+  run<7, 0, 0, 1, true, 2>(B, cus);
+  run<1, 0, 6, 2, true, 2>(B, cus);
+  run<0, 0, 7, 2, true, 2>(B, cus);
+  run<0, 0, 7, 2, false, 2>(B, cus);
+  // the edge backward's mixes (edge_bwd_w2: 6 streamed reads + 1 gathered gaggr row, 3 writes;
+  // edge_gout_wc: 3R + 2W), one-block and two-block
+  run<6, 1, 3, 2, true>(B, cus);
+  run<6, 1, 3, 1, true, 2>(B, cus);
+  run<3, 0, 2, 2, true>(B, cus);
+  run<3, 0, 2, 2, true, 2>(B, cus);
+  return 0;
+}
