@@ -154,3 +154,19 @@ def test_quad_mesh_graph(tmp_path):
     assert float(gp.edge_attr[gp.edge_attr == 0].sum()) == 0.0 and int((gp.edge_attr == 0).sum()) > 0
     with pytest.raises(ValueError):
         datasets.mesh_to_graph(pts, quads[:, :2])
+
+
+def test_mesh_to_graph_matches_reference_fixture():
+    """gnn_local_stress.datasets.mesh_to_graph against the reference's own convert_utils.mesh_to_graph /
+    _quad_face_to_edge (convert_utils.py:47-81), run by tests/golden/make_golden_graphs.py on a quad
+    grid with scrambled node ids, clockwise quads and a triangulated hole plate: edge_index bit for bit."""
+    from pathlib import Path
+    from gnn_local_stress import datasets
+    g = np.load(Path(__file__).resolve().parent / "golden" / "mesh_to_graph.npz")
+    names = sorted({k.rsplit("_", 1)[0] for k in g.files if k.endswith("_points")})
+    assert names == ["quad_clockwise", "quad_scrambled", "tri_hole_plate"]
+    for name in names:
+        out = datasets.mesh_to_graph(g[f"{name}_points"], g[f"{name}_cells"])
+        ref = g[f"{name}_edge_index"]
+        assert out.edge_index.dtype == torch.int64
+        assert np.array_equal(out.edge_index.numpy(), ref), name
