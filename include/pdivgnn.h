@@ -465,6 +465,16 @@ int pdg_wgrad_reduce_batch(int njobs, const float* const* slabs, const int* nsla
 int pdg_transpose128_batch(int n, const float* const* in_ptrs, const int* lds, float* const* out_ptrs, void* stream);
 /* *flag = 1 if any grad element is inf/NaN (GradScaler's skip test, gnn_train.py:205-207). */
 int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream);
+/* pdg_nonfinite + the zero-mean-stress skip in one launch, no memset: flags[2] double-buffered by call
+ * parity; flags[parity] = any non-finite x[i] || (zero_flag && *zero_flag == 0), and flags[parity ^ 1] is
+ * cleared for the next call (replaces GradScaler's inf check, gnn_train.py:205-207, and the guard of
+ * models.py:294-299; pdg_adam then reads flags + parity as its skip flag). */
+int pdg_nonfinite2(const float* x, int64_t n, const float* zero_flag, int* flags, int parity, void* stream);
+/* The step's loss scalars (gnn_train.py:189-197) in one launch: out[0] = *zero_flag (1 when NULL),
+ * out[1] = scale_nmse * sum_g loss_nmse[g], out[2] = scale_div * sum_g loss_div[g] (0 when loss_div is
+ * NULL), out[3] = out[1] + out[2]; fp64 sums in graph order, rounded once. */
+int pdg_loss_reduce(int n_graphs, const float* loss_nmse, const float* loss_div, float scale_nmse,
+                    float scale_div, const float* zero_flag, float* out, void* stream);
 /* Adam as torch.optim.Adam (amsgrad=False, weight_decay=0) stepped by GradScaler.step
  * (gnn_train.py:111,118,204-207) on a flat parameter buffer.  Adam's step count lives on the
  * device: step_count[parity] = optimizer steps taken so far (c); the update uses

@@ -321,6 +321,66 @@ extern "C" int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream)
   return PDG_OK;
 }
 
+// The step's non-finite test and the zero-mean-stress skip in one launch, with no memset: flags[2] is
+// double-buffered by call parity (as Adam's step count): every block ORs into flags[parity], block 0
+// clears flags[parity ^ 1] for the next call (which runs after this one on the stream).  *zero_flag (a
+// float, nullable) of 0 forces the skip: the zero-mean-stress guard of models.py:294-299.
+__global__ void nonfinite2_kernel(const float* __restrict__ x, long n, const float* __restrict__ nz,
+                                  int* __restrict__ flags, int parity) {
+  int bad = 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    bad |= !isfinite(x[i]);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    flags[parity ^ 1] = 0;
+    if (nz && *nz == 0.f) bad = 1;
+  }
+  if (__any(bad) && lane_id() == 0) atomicOr(flags + parity, 1);
+}
+
+extern "C" int pdg_nonfinite2(const float* x, int64_t n, const float* zero_flag, int* flags, int parity,
+                              void* stream) {
+  PDG_CHECK_ARG(n >= 0 && flags != nullptr && (parity == 0 || parity == 1), "pdg_nonfinite2: bad args");
+  long blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(nonfinite2_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, (long)n,
+                     zero_flag, flags, parity);
+  PDG_CHECK_LAUNCH("pdg_nonfinite2");
+  return PDG_OK;
+}
+
+// The step's loss scalars (gnn_train.py:189-197) in one launch: out[0] = *zero_flag (or 1 when NULL),
+// out[1] = scale_nmse * sum_g loss_nmse[g], out[2] = scale_div * sum_g loss_div[g] (0 when NULL),
+// out[3] = out[1] + out[2].  Sums in fp64, graph order, rounded once.
+__global__ void loss_reduce_kernel(int B, const float* __restrict__ ln, const float* __restrict__ ld, float sn,
+                                   float sd, const float* __restrict__ nz, float* __restrict__ out) {
+  __shared__ double red[2 * 16];
+  double a = 0, b = 0;
+  for (int g = threadIdx.x; g < B; g += blockDim.x) {
+    a += (double)ln[g];
+    if (ld) b += (double)ld[g];
+  }
+  double v[2] = {a, b};
+  block_sum_k<2>(v, red);
+  if (threadIdx.x == 0) {
+    const float fn = (float)v[0] * sn;
+    const float fd = ld ? (float)v[1] * sd : 0.f;
+    out[0] = nz ? *nz : 1.f;
+    out[1] = fn;
+    out[2] = fd;
+    out[3] = fn + fd;
+  }
+}
+
+extern "C" int pdg_loss_reduce(int n_graphs, const float* loss_nmse, const float* loss_div, float scale_nmse,
+                               float scale_div, const float* zero_flag, float* out, void* stream) {
+  PDG_CHECK_ARG(n_graphs > 0 && loss_nmse != nullptr && out != nullptr, "pdg_loss_reduce: bad args");
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, n_graphs, loss_nmse, loss_div,
+                     scale_nmse, scale_div, zero_flag, out);
+  PDG_CHECK_LAUNCH("pdg_loss_reduce");
+  return PDG_OK;
+}
+
 // torch.optim.Adam._single_tensor_adam (amsgrad=False, weight_decay=0, maximize=False) driven by
 // GradScaler.step (gnn_train.py:111,118,204-207): a skipped step (non-finite gradient) leaves the
 // parameters, both moments AND Adam's step count untouched.  The step count therefore lives on the

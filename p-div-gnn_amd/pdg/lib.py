@@ -102,6 +102,8 @@ SIGNATURES: dict[str, list] = {
     "pdg_div_bwd": [I, P, I, P, P, P, P, P, P, I, I, P, P],
     "pdg_transpose": [I, I, I, P, P, P],
     "pdg_nonfinite": [P, c_int64, P, P],
+    "pdg_nonfinite2": [P, c_int64, P, P, I, P],
+    "pdg_loss_reduce": [I, P, P, c_float, c_float, P, P, P],
     "pdg_collate": [P, I, ctypes.c_long, P],
     "pdg_adam": [c_int64, P, P, P, P, P, I, c_float, c_float, c_float, c_float, P, P, I, P],
 }

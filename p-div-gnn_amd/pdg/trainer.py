@@ -64,10 +64,11 @@ class Trainer:
         sizes = [int(torch.Size(s).numel()) for _, s in PARAM_SHAPES]
         total = sum(sizes)
         self.flat_p = torch.empty(total, dtype=torch.float32, device=dev)
-        # the all-reduced bucket: every parameter gradient, then one slot holding 1.0 when this rank's
-        # batch has a nonzero mean stress (the zero-mean-stress guard of models.py:294-299, below), then
-        # this rank's shares of the global minibatch's NMSE and divergence terms
-        self._bucket = torch.zeros(total + 3, dtype=torch.float32, device=dev)
+        # the all-reduced bucket: every parameter gradient, then (pdg_loss_reduce's four scalars) one slot
+        # holding 1.0 when this rank's batch has a nonzero mean stress (the zero-mean-stress guard of
+        # models.py:294-299, below) and this rank's shares of the global minibatch's NMSE, divergence and
+        # total loss
+        self._bucket = torch.zeros(total + 4, dtype=torch.float32, device=dev)
         self.flat_g = self._bucket[:total]
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -83,7 +84,9 @@ class Trainer:
                 self.G[name] = self.flat_g[off:off + n].view(shape)
                 off += n
         self._gt_cache: dict = {}
-        self._skip = torch.zeros(1, dtype=torch.int32, device=dev)
+        # the step's skip flag (non-finite gradient or all-zero mean stress), double-buffered by call
+        # parity like Adam's step count (pdg_nonfinite2 clears the other slot: no memset per step)
+        self._flags = torch.zeros(2, dtype=torch.int32, device=dev)
         # Adam's step count on the device, double-buffered by call parity (pdg_adam), and the
         # host's bound on it (optimizer calls since the count was last set)
         self._count = torch.zeros(2, dtype=torch.int32, device=dev)
@@ -144,8 +147,7 @@ class Trainer:
             flag = torch.zeros(1, dtype=torch.int32, device=self.device)
             msf = ms.float().contiguous()
             lib.pdg_any_nonzero(msf.data_ptr(), msf.numel(), flag.data_ptr(), stream_handle(self.device))
-            self._nz_cache = {"batch": batch, "ms": ms, "ver": ms._version, "v": flag.float(),
-                              "zero": flag.eq(0).int()}
+            self._nz_cache = {"batch": batch, "ms": ms, "ver": ms._version, "v": flag.float()}
         return self._nz_cache["v"]
 
     def _global_graphs(self, B: int) -> int:
@@ -173,11 +175,7 @@ class Trainer:
             if n_global_graphs is None:
                 n_global_graphs = self._global_graphs(0)
             self.flat_g.zero_()
-            zero = torch.zeros((), **f32)
-            out = {"nmse": zero}
-            if self.divergence:
-                out["div"] = zero
-            return self._update(out, f32, s, torch.zeros(1, **f32))
+            return self._update({"B": 0}, f32, s, None)
         plan = plan_for(batch)
         stats8 = m.stats_tensor(self.device)
         B, N = plan.n_graphs, plan.n_nodes
@@ -239,7 +237,8 @@ class Trainer:
         gy = torch.empty(N, 3, **f32)
         lib.pdg_nmse_bwd(B, plan.ptr.data_ptr(), N, gt.data_ptr(), y.data_ptr(), den.data_ptr(), scale.data_ptr(), 0,
                          gy.data_ptr(), s)
-        out = {"nmse": loss_g.sum() / Bn}
+        # per-graph losses; _update reduces them (pdg_loss_reduce: sum / B_global [x penalty])
+        out = {"B": B, "Bn": Bn, "loss_g": loss_g}
         if self.divergence:
             types = batch.surfaces_nodes_for_div if batch.surfaces_nodes_for_div is not None else batch.nodes_types
             types = types.reshape(-1).to(torch.int64).contiguous()
@@ -252,48 +251,51 @@ class Trainer:
             lib.pdg_div_bwd(B, plan.ptr.data_ptr(), N, plan.at_rowptr.data_ptr(), plan.at_row.data_ptr(),
                             plan.at_comp.data_ptr(), plan.at_val.data_ptr(), div.data_ptr(), sd.data_ptr(), 0, 1,
                             gy.data_ptr(), s)
-            out["div"] = loss_d.sum() * (self.penalty / Bn)
+            out["loss_d"] = loss_d
         self.flat_g.zero_()
         self.engine.backward(self.P, ctx, gy, self.G)
         del ctx
         return out
 
-    def _update(self, out, f32, s, nz) -> dict:
+    def _update(self, fb, f32, s, nz) -> dict:
+        """Loss scalars, the data-parallel all-reduce, the skip test and Adam.  `fb`: _fwd_bwd's per-graph
+        losses (or {"B": 0} for an empty shard); `nz`: this rank's nonzero-mean-stress flag (a device
+        float, None for an empty shard)."""
         # zero-mean-stress guard (models.py:294-299): the reference's forward returns zeros without a
         # graph there, so its backward() raises and no update happens.  Here the step is skipped like a
         # non-finite one (parameters, moments and Adam's count unchanged; out["skipped"] = 1), decided
         # on the device.  Under data parallelism the flag rides in the gradient bucket, so the step is
         # skipped on every rank exactly when the GLOBAL minibatch is all zero, as one device would.
+        # pdg_loss_reduce writes [flag, nmse / B_global, penalty * div / B_global, total] (one launch for
+        # what were torch's sum / scale / add kernels): into the bucket's tail under data parallelism (every
+        # rank's shares are already / B_global, so the summed bucket holds the global minibatch's losses)
+        tail = self._bucket[-4:] if self.pg is not None else torch.empty(4, **f32)
+        if fb["B"] > 0:
+            ld = fb.get("loss_d")
+            lib.pdg_loss_reduce(fb["B"], fb["loss_g"].data_ptr(), ld.data_ptr() if ld is not None else None,
+                                1.0 / fb["Bn"], self.penalty / fb["Bn"], nz.data_ptr(), tail.data_ptr(), s)
+        else:
+            tail.zero_()
         if self.pg is not None:
-            # every rank's loss is already / B_global: the bucket is SUMMED (gradients and the loss
-            # shares), so unequal shards keep the reference's 1/B weighting of every graph
-            self._bucket[-3:-2].copy_(nz)
-            self._bucket[-2:-1].copy_(out["nmse"].reshape(1))
-            if "div" in out:
-                self._bucket[-1:].copy_(out["div"].reshape(1))
-            else:
-                self._bucket[-1:].zero_()
             end = self._mark("allreduce")
             torch.distributed.all_reduce(self._bucket, group=self.pg)
             end()
-            parts = self._bucket[-2:].clone()       # (the bucket is rewritten by the next step)
-            out["nmse"] = parts[0]
-            if "div" in out:
-                out["div"] = parts[1]
+        parity = self._calls & 1
         self._ensure_table(self._count_bound + 1)
-        lib.pdg_nonfinite(self.flat_g.data_ptr(), self.flat_g.numel(), self._skip.data_ptr(), s)
-        if self.pg is not None:   # the global minibatch's flag (summed over the ranks with the bucket)
-            self._skip.bitwise_or_(self._bucket[-3:-2].eq(0))
-        else:                     # one device: this batch's flag, cached with it (two launches fewer)
-            self._skip.bitwise_or_(self._nz_cache["zero"])
+        # skip = non-finite gradient OR the (global) minibatch's stress flag == 0, one launch
+        lib.pdg_nonfinite2(self.flat_g.data_ptr(), self.flat_g.numel(), tail.data_ptr(), self._flags.data_ptr(),
+                           parity, s)
+        skip = self._flags[parity:parity + 1]
         lib.pdg_adam(self.flat_p.numel(), self.flat_p.data_ptr(), self.flat_g.data_ptr(), self.exp_avg.data_ptr(),
                      self.exp_avg_sq.data_ptr(), self._table.data_ptr(), self._table.shape[0],
                      float(1.0 - self.betas[0]), self.betas[1], float(1.0 - self.betas[1]), self.eps,
-                     self._skip.data_ptr(), self._count.data_ptr(), self._calls & 1, s)
+                     skip.data_ptr(), self._count.data_ptr(), parity, s)
         self._calls += 1
         self._count_bound += 1
-        out["skipped"] = self._skip
-        out["total"] = out["nmse"] + out.get("div", 0.0)
+        vals = tail[1:].clone() if self.pg is not None else tail[1:]   # (the bucket is rewritten next step)
+        out = {"nmse": vals[0], "total": vals[2], "skipped": skip}      # skipped: valid until the next step
+        if self.divergence:
+            out["div"] = vals[1]
         return out
 
 

@@ -16,15 +16,19 @@ oracle (oracle/epd_oracle.py) in float32 AND float64 on this host.
 
 Tolerances (north_star "within 1e-5 rel fp32"; the same rules as tests/test_gpu_model.py):
 output field and losses within 1e-5 relative (L2) of both oracles; every parameter gradient
-within max(1e-4, 2 x the fp32 oracle's own distance to fp64) of the fp64 oracle.  These are the
+within max(3e-5, 2 x the fp32 oracle's own distance to fp64) of the fp64 oracle (round 4: the
+fixed floor tightened from 1e-4 to 3e-5, 1.5x the worst gradient error on record, config 4's
+edge_encoder.0.weight at 2.0e-5).  These are the
 sizes at which the bf16x6 products (W2 in the edge kernels, every weight gradient) and the fp64
 graph-LayerNorm reductions accumulate the most terms (up to 9.6e5 rows per LayerNorm and 2e7
 rows per weight gradient), so they are where a precision shortfall would show.
 
 At configs 3 and 4 the oracle keeps activations of one message-passing step at a time
 (checkpoint_steps: ~35 GB of host memory in float64 instead of ~170 GB) and the float32 oracle
-runs only when a gradient is outside the fixed 1e-4 bound (it can only loosen the bound): the
-float64 run alone takes a few minutes of host CPU.  A heartbeat line is appended to
+runs only when a gradient is outside the fixed 3e-5 bound (it can only loosen the bound) or when
+PDG_PARITY_FP32=1 asks for the record (profiles/r04_parity.jsonl holds such a run: the fp32
+oracle's own distance to fp64 beside the GPU's, per tensor): the float64 run alone takes a few
+minutes of host CPU.  A heartbeat line is appended to
 gpurun_out/fullsize_heartbeat.log every 20 s while a test runs (long silent runs look hung).
 Every test appends its measured errors as one JSON line to gpurun_out/parity.jsonl (and to
 $PDG_PARITY_LOG when set), so the margins to the tolerances are on record, not only "passed".
@@ -43,7 +47,7 @@ from gpu_common import dev, rel
 pytestmark = pytest.mark.gpu
 
 OUT_TOL = 1e-5
-GRAD_TOL = 1e-4
+GRAD_TOL = 3e-5
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -140,7 +144,8 @@ def test_training_step_at_baseline_size(config):
            "internal_boundary_nodes": int((batch.nodes_types == -1).sum()),
            "pred_vs_f64": rel(pred, p64), "loss_vs_f64": abs(total - t64) / abs(t64),
            "nmse_vs_f64": abs(nmse - n64) / abs(n64), "grads": {}}
-    need32 = not big or any(rel(grads[n], g64[n]) > GRAD_TOL for n in g64)
+    need32 = (not big or os.environ.get("PDG_PARITY_FP32") == "1"
+              or any(rel(grads[n], g64[n]) > GRAD_TOL for n in g64))
     g32 = None
     if need32:
         p32, t32, _, g32 = _oracle(params, stats, batch, cfg["steps"], torch.float32, cfg["divergence"], True, big)

@@ -9,9 +9,12 @@
 Tolerance (north_star: "within 1e-5 rel fp32"): relative L2 error of the
 output field and of the losses <= 1e-5.  Gradients: each parameter's gradient
 must be as close to the float64 restatement as the reference's own fp32 CPU
-result is, within a factor 2, and never worse than 1e-4 relative L2 (they
+result is, within a factor 2, and never worse than 3e-5 relative L2 (they
 aggregate 10^5-10^7 fp32 products through the tied steps and graph-global
-LayerNorms; DESIGN.md "Parity").
+LayerNorms; DESIGN.md "Parity").  Two fp32 evaluations of the HIP path with
+different kernel variants are compared at VARIANT_TOL = 1e-4: they may differ
+in a relu mask bit whose pre-activation is within rounding of zero.  Every
+gradient comparison against fp64 is appended to gpurun_out/parity.jsonl.
 """
 import pytest
 import torch
@@ -22,7 +25,28 @@ from gpu_common import dataset_stats, golden_batch, make_batch, rel
 pytestmark = pytest.mark.gpu
 
 OUT_TOL = 1e-5
-GRAD_TOL = 1e-4
+GRAD_TOL = 3e-5
+VARIANT_TOL = 1e-4
+
+
+def _log_grads(case, model, g64, ref32):
+    """Append every parameter's gradient error vs fp64 beside the fp32 reference's own to
+    gpurun_out/parity.jsonl (the margins to GRAD_TOL on record, not only "passed")."""
+    import json
+    import os
+    from pathlib import Path
+    errs = {n: (rel(p.grad, g64[n]), ref32[n]) for n, p in model.named_parameters()}
+    worst = max(errs, key=lambda n: errs[n][0] / max(GRAD_TOL, 2 * errs[n][1]))
+    rec = {"case": case, "worst_grad": [worst, *errs[worst]],
+           "worst_margin": errs[worst][0] / max(GRAD_TOL, 2 * errs[worst][1]),
+           "max_grad_err": max(e[0] for e in errs.values()), "grad_tol_rule": f"max({GRAD_TOL}, 2 x fp32 vs fp64)"}
+    out = Path(os.environ.get("GRAFT_REPO_ROOT", Path(__file__).resolve().parents[1])) / "gpurun_out"
+    try:
+        out.mkdir(exist_ok=True)
+        with open(out / "parity.jsonl", "a") as f:
+            f.write(json.dumps(rec) + "\n")
+    except OSError:
+        pass
 
 
 def _model(steps, stats, params=None):
@@ -63,6 +87,7 @@ def test_forward_and_grads_match_golden(case):
     # float64 restatement of the same step: the noise floor of the fp32 reference
     _, _, g64 = _oracle_grads(g["params"], {k: float(v) for k, v in g["stats"].items()}, batch, steps,
                               torch.float64, bool(g["divergence"]), float(g["penalty"]))
+    _log_grads(f"golden:{case}", model, g64, {n: rel(g["grads"][n], g64[n]) for n in g64})
     for name, p in model.named_parameters():
         ref32 = rel(g["grads"][name], g64[name])
         assert rel(p.grad, g64[name]) <= max(GRAD_TOL, 2 * ref32), (name, rel(p.grad, g64[name]), ref32)
@@ -138,6 +163,7 @@ def test_training_step_matches_oracle_fp32_and_fp64(nmesh, ngraph, steps, diverg
     assert rel(pred.detach(), p32) < OUT_TOL, (rel(pred.detach(), p32), floor)
     assert rel(pred.detach(), p64) < OUT_TOL
     assert abs(float(total) - t64) <= OUT_TOL * abs(t64)
+    _log_grads(f"oracle:{nmesh}x{ngraph}:s{steps}", model, g64, {n: rel(g32[n], g64[n]) for n in g64})
     for name, p in model.named_parameters():
         ref32 = rel(g32[name], g64[name])
         assert rel(p.grad, g64[name]) <= max(GRAD_TOL, 2 * ref32), (name, rel(p.grad, g64[name]), ref32)
@@ -224,8 +250,8 @@ def test_forward_variants_agree(nmesh, ngraph, steps):
     sums formed in the edge forward, message LayerNorm applied by node_net's loaders; default),
     pdg_edge_fwd_coop + pdg_segment_sum, and pdg_edge_fwd + pdg_segment_sum.  Output (training and
     inference, where the seg variant stores no a2m) agree to 1e-5 and every parameter gradient to
-    GRAD_TOL (the golden tests' bound against fp64: two fp32 evaluations may differ in a relu mask bit
-    whose pre-activation is within rounding of zero)."""
+    VARIANT_TOL (two fp32 evaluations may differ in a relu mask bit whose pre-activation is within
+    rounding of zero)."""
     from gnn_local_stress import losses
     from pdg import meshgen
     samples = meshgen.make_dataset(ngraph, n=nmesh, hole_radius=(0.15, 0.3), seed=7)
@@ -249,7 +275,7 @@ def test_forward_variants_agree(nmesh, ngraph, steps):
         y1, p1, g1 = res[key]
         assert rel(y1, y0) < 1e-5 and rel(p1, p0) < 1e-5, key
         for name, g in g1.items():
-            assert rel(g, g0[name]) < GRAD_TOL, (key, name, rel(g, g0[name]))
+            assert rel(g, g0[name]) < VARIANT_TOL, (key, name, rel(g, g0[name]))
 
 
 @pytest.mark.parametrize("variant", ["recompute_a1", "gout_gz1"])
