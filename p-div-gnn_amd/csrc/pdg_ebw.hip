@@ -690,7 +690,13 @@ typedef double d64x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 
-template <bool RES, bool EU, bool SEG>
+// D (deferred a2 stores, training and plain inference; not with SEG): a2 goes into two tiles of its own
+// and its rows are stored after the NEXT round's first barrier, behind that round's gathers and row
+// loads, so a round has two barriers instead of four (the barrier that freed the a1 tiles for a2 and
+// the one that completed the a2 tiles go: the loop-top barrier completes both the e tile and the
+// previous round's a2 tiles), and the C product's wait for its gathers no longer covers the previous
+// round's a2 stores.  Bitwise the same outputs; 32 KB more LDS (131 KB).
+template <bool RES, bool EU, bool SEG, bool D = false>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
@@ -708,6 +714,9 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   float* t_s = t_e + X6_ROWS * EFC_ES;                         // SEG: a2m tiles (by round parity)
   int* sdst0 = reinterpret_cast<int*>(t_s + 2 * EFC_TILE);     //      dst of the rounds' rows
   double* carry = reinterpret_cast<double*>(sdst0 + 2 * X6_ROWS);   // open segment's sum, 2 rows
+  float* t_am = t_e + X6_ROWS * EFC_ES;                        // D: a2m / a2e tiles (in place of SEG's)
+  float* t_ae = t_am + EFC_TILE;
+  static_assert(!(SEG && D), "deferred a2 stores and the segment sums use the same LDS");
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
@@ -865,6 +874,15 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     __builtin_amdgcn_sched_barrier(0);
     issue(base + X6_ROWS);   // clamped past r1: unconditional
     __builtin_amdgcn_sched_barrier(0);
+    if (D) {   // the previous round's a2 rows (tiles completed by the barrier above; none before round 0:
+               // the first round's base - r0 - 32 lies below the range and its stores are dropped)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = rg + 16 * u;
+        rows_store4_nt(rs_a2m, base - X6_ROWS + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_am + r * OT_STRIDE + 4 * cg));
+        if (EU) rows_store4_nt(rs_a2e, base - X6_ROWS + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_ae + r * OT_STRIDE + 4 * cg));
+      }
+    }
     // ---- C = Wc e + b1 and the two first layers at this wave's 16 features
     f32x4 d[2];
 #pragma unroll
@@ -908,14 +926,15 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     // the previous round's sums (the row after its last is this round's row 0)
     if (SEG && base > r0) walk(base - X6_ROWS, par ^ 1, sdst0[par * X6_ROWS], true);
     // ---- a2 = relu(W2 a1 + b2) for both evaluations
-    float* t_a2 = SEG ? t_s + par * EFC_TILE : t_m;
+    float* t_a2 = SEG ? t_s + par * EFC_TILE : D ? t_am : t_m;
+    float* t_a2e = D ? t_ae : t_x;
     constexpr int NI = EU ? 2 : 1;
     f32x4 d2[NI][2];
     const unsigned char* ia[NI];
     ia[0] = img_m;
     if (EU) ia[NI - 1] = img_x;
     gemm_round<NI>(d2, ws2, ia);
-    __syncthreads();   // the a1 tiles are read; reuse them for a2
+    if (!D) __syncthreads();   // the a1 tiles are read; reuse them for a2
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
       const int r = 16 * nb + (l & 15);
@@ -925,7 +944,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         f32x4 a;
 #pragma unroll
         for (int j = 0; j < 4; ++j) a[j] = fmaxf(d2[u][nb][j] + b2o[j], 0.f);
-        *reinterpret_cast<f32x4*>((u ? t_x : t_a2) + r * OT_STRIDE + oc) = a;
+        *reinterpret_cast<f32x4*>((u ? t_a2e : t_a2) + r * OT_STRIDE + oc) = a;
         if (ok) {
           const double p1 = (double)((a[0] + a[1]) + (a[2] + a[3]));
           const double p2 = (double)((a[0] * a[0] + a[1] * a[1]) + (a[2] * a[2] + a[3] * a[3]));
@@ -933,14 +952,26 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         }
       }
     }
-    __syncthreads();   // a2 tiles complete
+    if (!D) {
+      __syncthreads();   // a2 tiles complete
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = rg + 16 * u;
+        rows_store4_nt(rs_a2m, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_a2 + r * OT_STRIDE + 4 * cg));
+        if (EU) rows_store4_nt(rs_a2e, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
+      }
+    }
+    stage(base + X6_ROWS);   // past r1: stores dropped, the tile unused; the e tile was last read before the second barrier
+  }
+  if (D) {   // the last round's a2 rows
+    __syncthreads();
+    const int last = r0 < r1 ? r0 + (r1 - 1 - r0) / X6_ROWS * X6_ROWS : r0;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
-      rows_store4_nt(rs_a2m, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_a2 + r * OT_STRIDE + 4 * cg));
-      if (EU) rows_store4_nt(rs_a2e, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
+      rows_store4_nt(rs_a2m, last + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_am + r * OT_STRIDE + 4 * cg));
+      if (EU) rows_store4_nt(rs_a2e, last + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_ae + r * OT_STRIDE + 4 * cg));
     }
-    stage(base + X6_ROWS);   // past r1: stores dropped, the tile unused; the e tile was last read before the second barrier
   }
   if (SEG && r0 < r1) walk(r0 + (r1 - 1 - r0) / X6_ROWS * X6_ROWS, ((r1 - 1 - r0) / X6_ROWS) & 1, after, false);
   if (SEG && threadIdx.x == 0) {   // the block's partials: head (+ whether it also runs past r1), tail
@@ -1763,6 +1794,11 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
                                 double* part_e, int with_edge_update, double* sums, double* seg_part, int* seg_info,
                                 int nblocks, int store_c, void* stream);
 
+// deferred a2 stores in the cooperative edge forward (edge_fwd_coop_kernel's D)
+#ifndef PDG_EFC_DEFER
+#define PDG_EFC_DEFER 0
+#endif
+
 extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                                  const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
                                  const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
@@ -1814,10 +1850,12 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
   PDG_CHECK_ARG(seg || a2m, "pdg_edge_fwd_coop: a2m may be omitted only with the segment sums");
   PDG_CHECK_ARG(!seg || (seg_part && seg_info && PDG_ALIGNED(sums) && PDG_ALIGNED(seg_part)),
                 "pdg_edge_fwd_coop_seg: sums / seg_part / seg_info missing or misaligned");
-  const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float) + (seg ? EFC_SEG_BYTES : 0);
+  const bool defer = PDG_EFC_DEFER && !seg;
+  const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float) + (seg ? EFC_SEG_BYTES : 0) +
+                     (defer ? 2 * EFC_TILE * sizeof(float) : 0);
   hipStream_t s = (hipStream_t)stream;
 #define PDG_EFC(R, U, S)                                                                                              \
-  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S>), dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
+  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER>), dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
                      ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e,  \
                      sums, seg_part, seg_info, store_c)
 #define PDG_EFC2(S)                                                \
