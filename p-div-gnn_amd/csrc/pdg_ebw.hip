@@ -696,7 +696,14 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // the one that completed the a2 tiles go: the loop-top barrier completes both the e tile and the
 // previous round's a2 tiles), and the C product's wait for its gathers no longer covers the previous
 // round's a2 stores.  Bitwise the same outputs; 32 KB more LDS (131 KB).
-template <bool RES, bool EU, bool SEG, bool D = false>
+//
+// X (XCD-interleaved rounds, not with SEG): the blocks that share an XCD's L2 (b and b + 8; the grid
+// a multiple of 8) sweep one contiguous eighth of the rows together, taking its 32-row rounds
+// round-robin, instead of each block owning a contiguous range.  The P / Q rows an edge gathers are
+// reused by the edges of the mesh neighbours of its nodes, about +-13 rounds away in dst order: with
+// per-block ranges every block of an XCD keeps such a window live (32 x ~280 KB, over the 4 MiB L2, so
+// the reuse was served by the Infinity Cache), with interleaved rounds the XCD has one window.
+template <bool RES, bool EU, bool SEG, bool D = false, bool X = false>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
@@ -717,11 +724,25 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   float* t_am = t_e + X6_ROWS * EFC_ES;                        // D: a2m / a2e tiles (in place of SEG's)
   float* t_ae = t_am + EFC_TILE;
   static_assert(!(SEG && D), "deferred a2 stores and the segment sums use the same LDS");
+  static_assert(!(SEG && X), "the segment sums need contiguous block ranges");
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
-  int r0, r1;
-  block_rows(E, r0, r1);
+  // rows: [r0, r1) is the range the block's buffer resources span and its loads clamp to; the block's
+  // rounds start at `first` and are `stride` rows apart (X: the XCD's range, every (G/8)-th round)
+  int r0, r1, first, stride;
+  if (X) {
+    const int rounds = (E + X6_ROWS - 1) / X6_ROWS, perx = (rounds + 7) / 8;
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    r0 = min(E, x * perx * X6_ROWS);
+    r1 = min(E, (x + 1) * perx * X6_ROWS);
+    first = min(E, r0 + j * X6_ROWS);
+    stride = (gridDim.x >> 3) * X6_ROWS;
+  } else {
+    block_rows(E, r0, r1);
+    first = r0;
+    stride = X6_ROWS;
+  }
   // the weights as A operands, rows = output features 16w .. 16w + 15 (W is out x in, row-major):
   // Wc = W1[:, 256:384] (row stride 384), W2
   f32x4 wcf[8];   // Wc rows 16w + (l & 15), inputs 16T + 4(l >> 4) .. +3 (node_pq_rw's A fragments)
@@ -826,7 +847,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     }
     prev_last = sdst[nr - 1];
   };
-  issue(r0);   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
+  issue(first);   // E > 0: an empty block (first = r1 = E) reads row E - 1
   {
     const float* pc = W1 + (size_t)(16 * w + (l & 15)) * (3 * L) + 2 * L + 4 * (l >> 4);
 #pragma unroll
@@ -852,8 +873,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     pin_vgpr(dq[u]);
     pin_vgpr(sq[u]);
   }
-  stage(r0);
-  for (int base = r0; base < r1; base += X6_ROWS) {
+  stage(first);
+  for (int base = first; base < r1; base += stride) {
     __syncthreads();   // e tile complete
     int dc[2] = {dq[0], dq[1]}, sc[2] = {sq[0], sq[1]};
     const int par = ((base - r0) / X6_ROWS) & 1;
@@ -872,15 +893,15 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    issue(base + X6_ROWS);   // clamped past r1: unconditional
+    issue(base + stride);   // clamped past r1: unconditional
     __builtin_amdgcn_sched_barrier(0);
-    if (D) {   // the previous round's a2 rows (tiles completed by the barrier above; none before round 0:
-               // the first round's base - r0 - 32 lies below the range and its stores are dropped)
+    if (D) {   // the previous round's a2 rows (tiles completed by the barrier above; none before the first
+               // round: base - stride lies below the range and its stores are dropped)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = rg + 16 * u;
-        rows_store4_nt(rs_a2m, base - X6_ROWS + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_am + r * OT_STRIDE + 4 * cg));
-        if (EU) rows_store4_nt(rs_a2e, base - X6_ROWS + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_ae + r * OT_STRIDE + 4 * cg));
+        rows_store4_nt(rs_a2m, base - stride + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_am + r * OT_STRIDE + 4 * cg));
+        if (EU) rows_store4_nt(rs_a2e, base - stride + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_ae + r * OT_STRIDE + 4 * cg));
       }
     }
     // ---- C = Wc e + b1 and the two first layers at this wave's 16 features
@@ -961,11 +982,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         if (EU) rows_store4_nt(rs_a2e, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
       }
     }
-    stage(base + X6_ROWS);   // past r1: stores dropped, the tile unused; the e tile was last read before the second barrier
+    stage(base + stride);   // past r1: stores dropped, the tile unused; the e tile was last read before the second barrier
   }
   if (D) {   // the last round's a2 rows
     __syncthreads();
-    const int last = r0 < r1 ? r0 + (r1 - 1 - r0) / X6_ROWS * X6_ROWS : r0;
+    const int last = first < r1 ? first + (r1 - 1 - first) / stride * stride : first;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
@@ -1798,6 +1819,10 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
 #ifndef PDG_EFC_DEFER
 #define PDG_EFC_DEFER 0
 #endif
+// XCD-interleaved rounds in the cooperative edge forward (edge_fwd_coop_kernel's X; needs nblocks % 8 == 0)
+#ifndef PDG_EFC_XCD
+#define PDG_EFC_XCD 0
+#endif
 
 extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                                  const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
@@ -1851,11 +1876,13 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
   PDG_CHECK_ARG(!seg || (seg_part && seg_info && PDG_ALIGNED(sums) && PDG_ALIGNED(seg_part)),
                 "pdg_edge_fwd_coop_seg: sums / seg_part / seg_info missing or misaligned");
   const bool defer = PDG_EFC_DEFER && !seg;
+  PDG_CHECK_ARG(!PDG_EFC_XCD || seg || nblocks % 8 == 0, "pdg_edge_fwd_coop: nblocks must be a multiple of 8");
   const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float) + (seg ? EFC_SEG_BYTES : 0) +
                      (defer ? 2 * EFC_TILE * sizeof(float) : 0);
   hipStream_t s = (hipStream_t)stream;
 #define PDG_EFC(R, U, S)                                                                                              \
-  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER>), dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
+  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER, S ? false : (bool)PDG_EFC_XCD>), \
+                     dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
                      ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e,  \
                      sums, seg_part, seg_info, store_c)
 #define PDG_EFC2(S)                                                \

@@ -27,14 +27,28 @@ constexpr int U = ROUND * 32 / THREADS;   // row slots per thread per round (2)
 
 __device__ __forceinline__ int clampr(int r, int r1) { return r < r1 ? r : r1 - 1; }
 
-template <int R, int G, int W, int DEPTH, bool NT, int BPC>
+// XI: XCD-interleaved rounds (blocks b and b + 8 share an XCD's L2: each XCD owns a contiguous eighth of
+// the rows and its blocks take its 32-row rounds round-robin, so the XCD's blocks sweep its range
+// together and the gathered rows' reuse stays inside its L2); otherwise one contiguous range per block.
+template <int R, int G, int W, int DEPTH, bool NT, int BPC, bool XI = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC, 2 * BPC))) void mix(const float* const* __restrict__ in, float* const* __restrict__ out,
                                                const int* __restrict__ gd, const int* __restrict__ gs,
                                                const float* __restrict__ P, const float* __restrict__ Q, int E) {
   const int nb = gridDim.x;
-  int per = (E + nb - 1) / nb;
-  per = (per + ROUND - 1) / ROUND * ROUND;
-  const int r0 = min(E, per * (int)blockIdx.x), r1 = min(E, per * ((int)blockIdx.x + 1));
+  int r0, r1, step;
+  if (XI) {
+    const int rounds = (E + ROUND - 1) / ROUND, perx = (rounds + 7) / 8;
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    r0 = min(E, (x * perx + j) * ROUND);
+    r1 = min(E, (x + 1) * perx * ROUND);
+    step = (nb >> 3) * ROUND;
+  } else {
+    int per = (E + nb - 1) / nb;
+    per = (per + ROUND - 1) / ROUND * ROUND;
+    r0 = min(E, per * (int)blockIdx.x);
+    r1 = min(E, per * ((int)blockIdx.x + 1));
+    step = ROUND;
+  }
   if (r0 >= r1) return;
   const int t = threadIdx.x, c = 4 * (t & 31), rr = t >> 5;
   constexpr int RG = R > 0 ? R : 1;
@@ -46,7 +60,7 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC
   auto issue = [&](int s, int base) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int row = clampr(base + rr + 16 * u, r1);
+      const int row = clampr(base + rr + 16 * u, min(r1, max(base, 0) + ROUND));
 #pragma unroll
       for (int a = 0; a < R; ++a) v[s][a][u] = *reinterpret_cast<const f32x4*>(in[a] + (size_t)row * L + c);
       if (G) {
@@ -66,12 +80,12 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC
       }
   };
 #pragma unroll
-  for (int s = 0; s < DEPTH; ++s) issue(s, r0 + ROUND * s);
+  for (int s = 0; s < DEPTH; ++s) issue(s, r0 + step * s);
   if (G && DEPTH > 1) gather(0, 0);
-  for (int base = r0; base < r1; base += DEPTH * ROUND) {
+  for (int base = r0; base < r1; base += DEPTH * step) {
 #pragma unroll
     for (int s = 0; s < DEPTH; ++s) {
-      const int b = base + ROUND * s;
+      const int b = base + step * s;
       // DEPTH > 1: round b's gathers were issued a round ahead (slot s); the next round's now
       if (G && DEPTH == 1) gather(0, 0);
       if (G && DEPTH > 1) gather((s + 1) % DEPTH, (s + 1) % DEPTH);
@@ -84,10 +98,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC
         for (int a = 0; a < G; ++a) x += g[s][a][u];
       }
       acc = x;
-      issue(s, b + DEPTH * ROUND);   // clamped past r1
+      issue(s, b + DEPTH * step);   // clamped past r1
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int row = clampr(b + rr + 16 * u, r1);
+        const int row = clampr(b + rr + 16 * u, min(r1, b + ROUND));
 #pragma unroll
         for (int a = 0; a < W; ++a) {
           f32x4* p = reinterpret_cast<f32x4*>(out[a] + (size_t)row * L + c);
@@ -133,19 +147,19 @@ double time_us(F launch, int reps = 20) {
   return ms * 1e3 / reps;
 }
 
-template <int R, int G, int W, int DEPTH, bool NT, int BPC = 1>
+template <int R, int G, int W, int DEPTH, bool NT, int BPC = 1, bool XI = false>
 void run(const Bufs& B, int cus) {
   const int blocks_per_cu = BPC;
   const int nblk = cus * blocks_per_cu;
   const double us = time_us([&] {
-    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out, B.gd, B.gs, B.P,
+    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC, XI>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out, B.gd, B.gs, B.P,
                        B.Q, B.E);
   });
   const double streamed = (double)B.E * 512.0 * (R + W);
   const double gathered = (double)B.E * 512.0 * G;
-  printf("{\"mix\": \"%dR+%dG+%dW\", \"depth\": %d, \"waves_per_cu\": %d, \"stores\": \"%s\", \"us\": %.1f, "
+  printf("{\"mix\": \"%dR+%dG+%dW\", \"rows\": \"%s\", \"depth\": %d, \"waves_per_cu\": %d, \"stores\": \"%s\", \"us\": %.1f, "
          "\"streamed_TBps\": %.3f, \"with_gathers_TBps\": %.3f}\n",
-         R, G, W, DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
+         R, G, W, XI ? "xcd-interleaved" : "contiguous", DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
          (streamed + gathered) / us * 1e-6);
   fflush(stdout);
 }
@@ -196,29 +210,20 @@ int main() {
     (void)hipFree(a);
     (void)hipFree(b);
   }
-  // the edge forward's mix, swept
+  // the edge forward's mix: contiguous block ranges (the kernels' block_rows) vs XCD-interleaved rounds
   run<2, 4, 5, 1, true>(B, cus);
-  run<2, 4, 5, 1, false>(B, cus);
+  run<2, 4, 5, 1, true, 1, true>(B, cus);
   run<2, 4, 5, 2, true>(B, cus);
+  run<2, 4, 5, 2, true, 1, true>(B, cus);
   run<2, 4, 5, 2, false>(B, cus);
-  run<2, 4, 5, 3, true>(B, cus);
-  run<2, 4, 5, 1, true, 2>(B, cus);
-  run<2, 4, 5, 1, false, 2>(B, cus);
-  // without the gathers, and the pure directions
-  run<2, 0, 5, 1, true>(B, cus);
+  run<2, 4, 5, 2, false, 1, true>(B, cus);
   run<2, 0, 5, 2, true>(B, cus);
-  run<2, 0, 5, 2, true, 2>(B, cus);
-  run<2, 0, 5, 2, false, 2>(B, cus);
-  run<7, 0, 0, 2, true>(B, cus);
-  run<7, 0, 0, 1, true, 2>(B, cus);
-  run<1, 0, 6, 2, true, 2>(B, cus);
-  run<0, 0, 7, 2, true, 2>(B, cus);
-  run<0, 0, 7, 2, false, 2>(B, cus);
+  run<2, 0, 5, 2, true, 1, true>(B, cus);
   // the edge backward's mixes (edge_bwd_w2: 6 streamed reads + 1 gathered gaggr row, 3 writes;
-  // edge_gout_wc: 3R + 2W), one-block and two-block
-  run<6, 1, 3, 2, true>(B, cus);
-  run<6, 1, 3, 1, true, 2>(B, cus);
-  run<3, 0, 2, 2, true>(B, cus);
-  run<3, 0, 2, 2, true, 2>(B, cus);
+  // edge_gout_wc: 4R + 1W)
+  run<5, 1, 3, 2, true>(B, cus);
+  run<5, 1, 3, 2, true, 1, true>(B, cus);
+  run<4, 0, 1, 2, true>(B, cus);
+  run<4, 0, 1, 2, true, 1, true>(B, cus);
   return 0;
 }

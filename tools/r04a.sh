@@ -1,19 +1,22 @@
 #!/bin/bash
-# round-4 first GPU pass: DP / trainer / model tests, the streaming probe, the SQ counter passes
+# round-4 GPU pass: DP / trainer / model tests, the streaming probe, edge-forward variant A/B
 set -o pipefail
-mkdir -p gpurun_out/r04a
-timeout -k 10 700 python -u -m pytest tests/test_gpu_adam.py tests/test_gpu_dist.py tests/test_gpu_train_harness.py \
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R" || exit 1
+O=gpurun_out/r04a
+mkdir -p $O
+timeout -k 10 120 tools/membench2 > $O/membench2.jsonl 2>&1 || { tail -5 $O/membench2.jsonl; exit 1; }
+cat $O/membench2.jsonl
+timeout -k 10 600 python -u -m pytest tests/test_gpu_adam.py tests/test_gpu_dist.py tests/test_gpu_train_harness.py \
   tests/test_gpu_trainer_graph.py tests/test_gpu_model.py -x -v --timeout 400 --timeout-method thread \
-  > gpurun_out/r04a/tests.log 2>&1
+  > $O/tests.log 2>&1
 rc=$?
-tail -25 gpurun_out/r04a/tests.log
+tail -12 $O/tests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-timeout -k 10 120 tools/membench2 > gpurun_out/r04a/membench2.jsonl 2>&1 || exit 1
-cat gpurun_out/r04a/membench2.jsonl
-bash tools/sq_pass.sh r04a
-# A/B: deferred a2 stores in the edge forward (variants/efcd), bitwise check then timing pairs
-cd "${GRAFT_REPO_ROOT:-$(pwd)}"
-timeout -k 10 200 python tools/grads_dump.py gpurun_out/r04a/g_default.pt > gpurun_out/r04a/gd.log 2>&1 || { tail -5 gpurun_out/r04a/gd.log; exit 1; }
-PDG_LIB=variants/efcd/libpdivgnn_hip.so timeout -k 10 200 python tools/grads_dump.py gpurun_out/r04a/g_efcd.pt >> gpurun_out/r04a/gd.log 2>&1 || { tail -5 gpurun_out/r04a/gd.log; exit 1; }
-python tools/grads_dump.py --compare gpurun_out/r04a/g_default.pt gpurun_out/r04a/g_efcd.pt
-bash tools/ab.sh r04a 2 default efcd default efcd
+# edge-forward variants: bitwise / close check, then timing pairs
+for v in default efcd efcx efcdx; do
+  lib=p-div-gnn_amd/pdg/libpdivgnn_hip.so; [ $v = default ] || lib=variants/$v/libpdivgnn_hip.so
+  PDG_LIB=$lib timeout -k 10 200 python tools/grads_dump.py $O/g_$v.pt >> $O/gd.log 2>&1 || { tail -5 $O/gd.log; exit 1; }
+done
+for v in efcd efcx efcdx; do echo "== $v vs default"; python tools/grads_dump.py --compare $O/g_default.pt $O/g_$v.pt | tail -4; done
+bash tools/ab.sh r04a 2 default efcd efcx efcdx default efcx efcdx
