@@ -161,6 +161,37 @@ __device__ __forceinline__ void block_rows(int M, int& r0, int& r1) {
   r1 = min(M, per * ((int)blockIdx.x + 1));
 }
 
+// The rows a block walks, in 32-row units: [r0, r1) is the range its buffer resources span and its
+// loads clamp to, its units start at `first` and are `stride` rows apart.  XI (XCD-interleaved): the
+// blocks that share an XCD's L2 (b and b + 8, MI355X_MICROARCH.md 'Workgroup dispatch'; the grid a
+// multiple of 8) sweep one contiguous eighth of the rows together, taking its units round-robin,
+// instead of each block owning one contiguous range (block_rows).  Rows gathered by index (the edge
+// forward's P / Q rows, reused by the edges of the mesh neighbours of a node, ~+-13 units apart in dst
+// order) then have one live window per XCD instead of one per block.
+// The interleaved form is compiled for a grid of XCD_GRID blocks (one per CU of MI355X: the stride is then
+// a constant; a runtime stride cost the edge backward 13 spilled VGPRs); the launchers check the grid.
+constexpr int XCD_GRID = 256;
+__device__ __forceinline__ void row_schedule(bool xi, int M, int& r0, int& r1, int& first, int& stride) {
+  if (xi) {
+    const int units = (M + X6_ROWS - 1) / X6_ROWS, perx = (units + 7) / 8;
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    r0 = min(M, x * perx * X6_ROWS);
+    r1 = min(M, (x + 1) * perx * X6_ROWS);
+    first = min(M, r0 + j * X6_ROWS);
+    stride = (XCD_GRID >> 3) * X6_ROWS;
+  } else {
+    block_rows(M, r0, r1);
+    first = r0;
+    stride = X6_ROWS;
+  }
+}
+
+// XCD-interleaved units in the edge backward kernels (pdg_edge_bwd_w2, pdg_edge_gout_wc; the grid a
+// multiple of 8)
+#ifndef PDG_EBW_XCD
+#define PDG_EBW_XCD 0
+#endif
+
 // slab += acc (the block's own slab, fixed block -> slab map) and the bias sums:
 // thread (cg, rg) holds column sums of columns 4cg .. 4cg+3 over its rows; reduced over
 // the 16 row groups in order through LDS (`red`, 8 KB, the images being dead).
@@ -234,8 +265,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;    // the thread's staged row: rg (0..15)
   const int oc = 16 * w + 4 * (l >> 4);
-  int r0, r1;
-  block_rows(E, r0, r1);
+  int r0, r1, first, stride;   // 32-row units: rounds base and base + 16, the next unit stride rows on
+  row_schedule(PDG_EBW_XCD, E, r0, r1, first, stride);
   WSlice ws;
   const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
@@ -281,21 +312,21 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   // skipped store or load on some path made it wait for all of them (vmcnt(0)) in the stage
   const __amdgpu_buffer_rsrc_t out_m = rows_rsrc(gz1m, r0, r1), out_c = rows_rsrc(gC, r0, r1);
   const __amdgpu_buffer_rsrc_t out_e = rows_rsrc(EU ? gz1e : gz1m, r0, r1);
-  dn[0] = dst[clamp_row(r0 + rg, r1)];   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
-  dn[1] = dst[clamp_row(r0 + R16 + rg, r1)];
+  dn[0] = dst[clamp_row(first + rg, r1)];   // E > 0: an empty block (first = r1 = E) reads row E - 1
+  dn[1] = dst[clamp_row(first + R16 + rg, r1)];
   if (RC) {   // round 0's gathered rows first, then round 1's ids
-    ids(r0);
+    ids(first);
     gather();
-    ids(r0 + R16);
+    ids(first + R16);
     __builtin_amdgcn_sched_barrier(0);
   }
   // each set's loads strictly before the next set's (sched_barrier), in the order the loop re-issues
   // them: the loop waits for one set by count, and an interleaved prologue lowers that count
-  issue(0, r0);
-  dn[0] = dst[clamp_row(r0 + 2 * R16 + rg, r1)];
+  issue(0, first);
+  dn[0] = dst[clamp_row(first + stride + rg, r1)];
   __builtin_amdgcn_sched_barrier(0);
-  issue(1, r0 + R16);
-  dn[1] = dst[clamp_row(r0 + 3 * R16 + rg, r1)];
+  issue(1, first + R16);
+  dn[1] = dst[clamp_row(first + stride + R16 + rg, r1)];
   __builtin_amdgcn_sched_barrier(0);
   // the weights and the LayerNorm scalars after the first rounds' row loads: the round trips overlap
   load_wslice(ws, W2T, w);
@@ -339,14 +370,15 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     }
     // ---- RC: the next round's gathered rows, then the ids of the round after it (both ahead of the
     // row loads below, which the next stage must not wait for)
-    if (RC) {
+    if (RC) {   // the next round's rows, then the ids of the round after it (this half of the next unit)
       gather();
-      ids(base + 2 * R16);
+      ids(base + stride);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // ---- the set is free: its rows of the round after next, then the dst ids of the one after that
-    issue(s, base + 2 * R16);
-    dn[s] = dst[clamp_row(base + 4 * R16 + rg, r1)];
+    // ---- the set is free: its rows of the round after next (the same half of the next unit), then
+    // the dst ids of the one after that
+    issue(s, base + stride);
+    dn[s] = dst[clamp_row(base + 2 * stride + rg, r1)];
     __syncthreads();   // this round's images complete (the other buffer is the previous round's)
     // ---- dW2 += gz2m^T a1m (+ gz2e^T a1e)
     wgrad_round<1, T16>(acc, img_gm, img_am);
@@ -378,7 +410,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   };
   // both rounds of a 32-row step always run: a round past r1 stages zero rows (adding exact zeros to
   // the weight gradient) and stores nothing
-  for (int base = r0; base < r1; base += 2 * R16) {
+  for (int base = first; base < r1; base += stride) {
     round(0, base);
     round(1, base + R16);
   }
@@ -406,8 +438,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
-  int r0, r1;
-  block_rows(E, r0, r1);
+  int r0, r1, first, stride;
+  row_schedule(PDG_EBW_XCD, E, r0, r1, first, stride);
   WSlice ws;
   f32x16 acc[2];
 #pragma unroll
@@ -430,9 +462,9 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
       if (ln) pa2[u] = *reinterpret_cast<const f32x4*>(a2ln + rc);   // LayerNorm input of e
     }
   };
-  if (r0 < r1) issue(r0);
+  if (first < r1) issue(first);
   load_wslice(ws, WcT, w);   // after the first round's row loads: both round trips in flight together
-  for (int base = r0; base < r1; base += X6_ROWS) {
+  for (int base = first; base < r1; base += stride) {
     f32x4 res[2], a2[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -447,7 +479,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
       a2[u] = ln ? pa2[u] : zero;
     }
     __syncthreads();
-    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
+    if (base + stride < r1) issue(base + stride);
     // ---- dWc += gC^T e
     wgrad_round(acc, img_c, img_e);
     // ---- Wc^T gC in the product's output layout -> row tile
@@ -731,18 +763,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   // rows: [r0, r1) is the range the block's buffer resources span and its loads clamp to; the block's
   // rounds start at `first` and are `stride` rows apart (X: the XCD's range, every (G/8)-th round)
   int r0, r1, first, stride;
-  if (X) {
-    const int rounds = (E + X6_ROWS - 1) / X6_ROWS, perx = (rounds + 7) / 8;
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-    r0 = min(E, x * perx * X6_ROWS);
-    r1 = min(E, (x + 1) * perx * X6_ROWS);
-    first = min(E, r0 + j * X6_ROWS);
-    stride = (gridDim.x >> 3) * X6_ROWS;
-  } else {
-    block_rows(E, r0, r1);
-    first = r0;
-    stride = X6_ROWS;
-  }
+  row_schedule(X, E, r0, r1, first, stride);
   // the weights as A operands, rows = output features 16w .. 16w + 15 (W is out x in, row-major):
   // Wc = W1[:, 256:384] (row stride 384), W2
   f32x4 wcf[8];   // Wc rows 16w + (l & 15), inputs 16T + 4(l >> 4) .. +3 (node_pq_rw's A fragments)
@@ -1683,6 +1704,7 @@ static int edge_bwd_w2_launch(int n_edges, const int* dst, const float* gaggr, c
   const bool rc = C != nullptr;
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_w2: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_bwd_w2: bad slabs");
+  PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_bwd_w2: the XCD-interleaved build needs 256 blocks");
   // gC may be NULL: not written (pdg_edge_gout_wc2 forms it from gz1m + gz1e)
   PDG_CHECK_ARG(dst && gaggr && a2m && (rc || a1m) && st_m && (lb_m || pairs_m) && ln_g && W2T && gz1m,
                 "pdg_edge_bwd_w2: null argument");
@@ -1743,6 +1765,7 @@ static int edge_gout_wc_launch(int n_edges, const float* gC, const float* gC2, c
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_gout_wc: n_edges must be > 0");
   PDG_CHECK_ARG(!gC2 || PDG_ALIGNED(gC2), "pdg_edge_gout_wc2: misaligned gz1e");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_gout_wc: bad slabs");
+  PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_gout_wc: the XCD-interleaved build needs 256 blocks");
   PDG_CHECK_ARG(gC && e && WcT && ge_out, "pdg_edge_gout_wc: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gC) && PDG_ALIGNED(e) && PDG_ALIGNED(WcT) && PDG_ALIGNED(ge_out) &&
                     PDG_ALIGNED(slabs) && (!ge_next || PDG_ALIGNED(ge_next)),
@@ -1876,7 +1899,7 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
   PDG_CHECK_ARG(!seg || (seg_part && seg_info && PDG_ALIGNED(sums) && PDG_ALIGNED(seg_part)),
                 "pdg_edge_fwd_coop_seg: sums / seg_part / seg_info missing or misaligned");
   const bool defer = PDG_EFC_DEFER && !seg;
-  PDG_CHECK_ARG(!PDG_EFC_XCD || seg || nblocks % 8 == 0, "pdg_edge_fwd_coop: nblocks must be a multiple of 8");
+  PDG_CHECK_ARG(!PDG_EFC_XCD || seg || nblocks == XCD_GRID, "pdg_edge_fwd_coop: the XCD-interleaved build needs 256 blocks");
   const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float) + (seg ? EFC_SEG_BYTES : 0) +
                      (defer ? 2 * EFC_TILE * sizeof(float) : 0);
   hipStream_t s = (hipStream_t)stream;

@@ -14,9 +14,9 @@ rc=$?
 tail -12 $O/tests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 # edge-forward variants: bitwise / close check, then timing pairs
-for v in default efcd efcx efcdx; do
+for v in default efcd efcx efcdx ebwx allx; do
   lib=p-div-gnn_amd/pdg/libpdivgnn_hip.so; [ $v = default ] || lib=variants/$v/libpdivgnn_hip.so
   PDG_LIB=$lib timeout -k 10 200 python tools/grads_dump.py $O/g_$v.pt >> $O/gd.log 2>&1 || { tail -5 $O/gd.log; exit 1; }
 done
-for v in efcd efcx efcdx; do echo "== $v vs default"; python tools/grads_dump.py --compare $O/g_default.pt $O/g_$v.pt | tail -4; done
-bash tools/ab.sh r04a 2 default efcd efcx efcdx default efcx efcdx
+for v in efcd efcx efcdx ebwx allx; do echo "== $v vs default"; python tools/grads_dump.py --compare $O/g_default.pt $O/g_$v.pt | tail -4; done
+bash tools/ab.sh r04a 2 default efcd efcx efcdx ebwx allx default allx efcdx
