@@ -186,8 +186,9 @@ __device__ __forceinline__ void row_schedule(bool xi, int M, int& r0, int& r1, i
   }
 }
 
-// XCD-interleaved units in the edge backward kernels (pdg_edge_bwd_w2, pdg_edge_gout_wc; the grid a
-// multiple of 8)
+// XCD-interleaved units in the edge backward kernels (pdg_edge_bwd_w2, pdg_edge_gout_wc; the grid of
+// XCD_GRID blocks).  Off: 195-198 vs 195-198 us per edge_bwd_w2 call (no gather whose reuse it could
+// help: gaggr[dst] is read in dst order), and the slab sums change order.
 #ifndef PDG_EBW_XCD
 #define PDG_EBW_XCD 0
 #endif
@@ -1839,12 +1840,14 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
                                 int nblocks, int store_c, void* stream);
 
 // deferred a2 stores in the cooperative edge forward (edge_fwd_coop_kernel's D)
+// (default: bitwise the same outputs; with X below 216 -> 210.5 us per config-2 call, the step -0.05 ms, in
+// two same-box A/B pairs; D alone or X alone measured no faster)
 #ifndef PDG_EFC_DEFER
-#define PDG_EFC_DEFER 0
+#define PDG_EFC_DEFER 1
 #endif
 // XCD-interleaved rounds in the cooperative edge forward (edge_fwd_coop_kernel's X; needs nblocks % 8 == 0)
 #ifndef PDG_EFC_XCD
-#define PDG_EFC_XCD 0
+#define PDG_EFC_XCD 1
 #endif
 
 extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,

@@ -84,16 +84,21 @@ def test_forward_and_grads_match_golden(case):
     assert abs(float(total.detach()) - float(g["loss_total"])) <= OUT_TOL * abs(float(g["loss_total"]))
     model.zero_grad()
     total.backward()
-    # float64 restatement of the same step: the noise floor of the fp32 reference
-    _, _, g64 = _oracle_grads(g["params"], {k: float(v) for k, v in g["stats"].items()}, batch, steps,
-                              torch.float64, bool(g["divergence"]), float(g["penalty"]))
-    _log_grads(f"golden:{case}", model, g64, {n: rel(g["grads"][n], g64[n]) for n in g64})
+    # float64 restatement of the same step, and the fp32 reference's own distance to it: the golden's
+    # (the reference run on the generating host) and the fp32 oracle's on this host (an fp32 CPU result
+    # depends on the host: the same ops 4e-5 apart on two CPUs, DESIGN.md "Parity"); the larger is the
+    # reference's noise floor here
+    st = {k: float(v) for k, v in g["stats"].items()}
+    _, _, g64 = _oracle_grads(g["params"], st, batch, steps, torch.float64, bool(g["divergence"]), float(g["penalty"]))
+    _, _, g32 = _oracle_grads(g["params"], st, batch, steps, torch.float32, bool(g["divergence"]), float(g["penalty"]))
+    ref32s = {n: max(rel(g["grads"][n], g64[n]), rel(g32[n], g64[n])) for n in g64}
+    _log_grads(f"golden:{case}", model, g64, ref32s)
     for name, p in model.named_parameters():
-        ref32 = rel(g["grads"][name], g64[name])
+        ref32 = ref32s[name]
         assert rel(p.grad, g64[name]) <= max(GRAD_TOL, 2 * ref32), (name, rel(p.grad, g64[name]), ref32)
         # direct check against the reference's fp32 gradient: bounded by the two errors to fp64
         d = rel(p.grad, g["grads"][name])
-        assert d <= max(GRAD_TOL, 1.5 * (rel(p.grad, g64[name]) + ref32)), (name, d)
+        assert d <= max(GRAD_TOL, 1.5 * (rel(p.grad, g64[name]) + rel(g["grads"][name], g64[name]))), (name, d)
 
 
 def test_per_graph_losses_match_oracle():

@@ -124,6 +124,8 @@ struct Bufs {
   float** d_out;
   int* gd;
   int* gs;
+  int* gd_small;   // the same pattern folded onto 1,024 nodes (1 MB of P / Q rows: surely L2-resident)
+  int* gs_small;
   float* P;
   float* Q;
   int E;
@@ -148,18 +150,18 @@ double time_us(F launch, int reps = 20) {
 }
 
 template <int R, int G, int W, int DEPTH, bool NT, int BPC = 1, bool XI = false>
-void run(const Bufs& B, int cus) {
+void run(const Bufs& B, int cus, bool small = false) {
   const int blocks_per_cu = BPC;
   const int nblk = cus * blocks_per_cu;
   const double us = time_us([&] {
-    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC, XI>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out, B.gd, B.gs, B.P,
-                       B.Q, B.E);
+    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC, XI>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out,
+                       small ? B.gd_small : B.gd, small ? B.gs_small : B.gs, B.P, B.Q, B.E);
   });
   const double streamed = (double)B.E * 512.0 * (R + W);
   const double gathered = (double)B.E * 512.0 * G;
-  printf("{\"mix\": \"%dR+%dG+%dW\", \"rows\": \"%s\", \"depth\": %d, \"waves_per_cu\": %d, \"stores\": \"%s\", \"us\": %.1f, "
+  printf("{\"mix\": \"%dR+%dG+%dW\", \"table\": \"%s\", \"rows\": \"%s\", \"depth\": %d, \"waves_per_cu\": %d, \"stores\": \"%s\", \"us\": %.1f, "
          "\"streamed_TBps\": %.3f, \"with_gathers_TBps\": %.3f}\n",
-         R, G, W, XI ? "xcd-interleaved" : "contiguous", DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
+         R, G, W, small ? "1k nodes" : "N nodes", XI ? "xcd-interleaved" : "contiguous", DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
          (streamed + gathered) / us * 1e-6);
   fflush(stdout);
 }
@@ -192,6 +194,14 @@ int main() {
   (void)hipMalloc(&B.gs, E * sizeof(int));
   (void)hipMemcpy(B.gd, hd.data(), E * sizeof(int), hipMemcpyHostToDevice);
   (void)hipMemcpy(B.gs, hs.data(), E * sizeof(int), hipMemcpyHostToDevice);
+  for (int e = 0; e < E; ++e) {
+    hd[e] &= 1023;
+    hs[e] &= 1023;
+  }
+  (void)hipMalloc(&B.gd_small, E * sizeof(int));
+  (void)hipMalloc(&B.gs_small, E * sizeof(int));
+  (void)hipMemcpy(B.gd_small, hd.data(), E * sizeof(int), hipMemcpyHostToDevice);
+  (void)hipMemcpy(B.gs_small, hs.data(), E * sizeof(int), hipMemcpyHostToDevice);
   (void)hipMalloc(&B.P, (size_t)N * 512);
   (void)hipMalloc(&B.Q, (size_t)N * 512);
   (void)hipMemset(B.P, 0, (size_t)N * 512);
@@ -210,20 +220,16 @@ int main() {
     (void)hipFree(a);
     (void)hipFree(b);
   }
-  // the edge forward's mix: contiguous block ranges (the kernels' block_rows) vs XCD-interleaved rounds
-  run<2, 4, 5, 1, true>(B, cus);
-  run<2, 4, 5, 1, true, 1, true>(B, cus);
-  run<2, 4, 5, 2, true>(B, cus);
-  run<2, 4, 5, 2, true, 1, true>(B, cus);
-  run<2, 4, 5, 2, false>(B, cus);
-  run<2, 4, 5, 2, false, 1, true>(B, cus);
-  run<2, 0, 5, 2, true>(B, cus);
-  run<2, 0, 5, 2, true, 1, true>(B, cus);
-  // the edge backward's mixes (edge_bwd_w2: 6 streamed reads + 1 gathered gaggr row, 3 writes;
-  // edge_gout_wc: 4R + 1W)
-  run<5, 1, 3, 2, true>(B, cus);
-  run<5, 1, 3, 2, true, 1, true>(B, cus);
-  run<4, 0, 1, 2, true>(B, cus);
-  run<4, 0, 1, 2, true, 1, true>(B, cus);
+  // the edge forward's mix: contiguous block ranges (the kernels' block_rows) vs XCD-interleaved rounds,
+  // gathers from the N-node tables vs the same pattern on a 1k-node (L2-resident) table, and no gathers
+  for (int rep = 0; rep < 2; ++rep) {
+    run<2, 4, 5, 1, true>(B, cus);
+    run<2, 4, 5, 1, true, 1, true>(B, cus);
+    run<2, 4, 5, 1, true>(B, cus, true);
+    run<2, 2, 5, 1, true>(B, cus);
+    run<2, 0, 5, 1, true>(B, cus);
+    run<0, 4, 0, 1, true>(B, cus);
+    run<0, 4, 0, 1, true>(B, cus, true);
+  }
   return 0;
 }
