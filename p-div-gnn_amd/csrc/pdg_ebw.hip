@@ -1902,15 +1902,25 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
   PDG_CHECK_ARG(!seg || (seg_part && seg_info && PDG_ALIGNED(sums) && PDG_ALIGNED(seg_part)),
                 "pdg_edge_fwd_coop_seg: sums / seg_part / seg_info missing or misaligned");
   const bool defer = PDG_EFC_DEFER && !seg;
-  PDG_CHECK_ARG(!PDG_EFC_XCD || seg || nblocks == XCD_GRID, "pdg_edge_fwd_coop: the XCD-interleaved build needs 256 blocks");
+  // the XCD-interleaved rounds are compiled for the 256-block grid; any other grid (tests, other parts)
+  // walks contiguous block ranges
+  const bool xcd = PDG_EFC_XCD && !seg && nblocks == XCD_GRID;
   const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float) + (seg ? EFC_SEG_BYTES : 0) +
                      (defer ? 2 * EFC_TILE * sizeof(float) : 0);
   hipStream_t s = (hipStream_t)stream;
-#define PDG_EFC(R, U, S)                                                                                              \
-  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER, S ? false : (bool)PDG_EFC_XCD>), \
+#define PDG_EFC_X(R, U, S, X)                                                                                         \
+  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER, X>), \
                      dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
                      ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e,  \
                      sums, seg_part, seg_info, store_c)
+#define PDG_EFC(R, U, S)                           \
+  do {                                             \
+    if (!(S) && PDG_EFC_XCD && xcd) {              \
+      PDG_EFC_X(R, U, S, (!(S) && PDG_EFC_XCD));   \
+    } else {                                       \
+      PDG_EFC_X(R, U, S, false);                   \
+    }                                              \
+  } while (0)
 #define PDG_EFC2(S)                                                \
   if (e_res) {                                                     \
     if (with_edge_update) PDG_EFC(true, true, S); else PDG_EFC(true, false, S);   \
@@ -1924,6 +1934,7 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
   }
 #undef PDG_EFC2
 #undef PDG_EFC
+#undef PDG_EFC_X
   PDG_CHECK_LAUNCH("pdg_edge_fwd_coop");
   return PDG_OK;
 }
