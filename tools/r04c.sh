@@ -6,11 +6,11 @@ O=gpurun_out/r04c
 mkdir -p $O
 timeout -k 10 300 python tools/grad_err_golden.py batch2_div_s10 > $O/grad_err.txt 2>&1 || { tail -5 $O/grad_err.txt; exit 1; }
 cat $O/grad_err.txt
-timeout -k 10 300 python tools/grad_err_golden.py batch3_div > $O/grad_err3.txt 2>&1 || { tail -5 $O/grad_err3.txt; exit 1; }
-cat $O/grad_err3.txt
+PDG_LIB=variants/unb/libpdivgnn_hip.so timeout -k 10 300 python tools/grad_err_golden.py batch2_div_s10 > $O/grad_err_unb.txt 2>&1 || { tail -5 $O/grad_err_unb.txt; exit 1; }
+cat $O/grad_err_unb.txt
 timeout -k 10 500 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_model.py -v --timeout 300 \
   --timeout-method thread > $O/tests.log 2>&1
 rc=$?
 grep -E "FAILED|ERROR|passed|failed" $O/tests.log | tail -8
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
-bash tools/ab.sh r04c 2 default old default old
+bash tools/ab.sh r04c 2 default old unb default old unb
