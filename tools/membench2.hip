@@ -115,6 +115,71 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC
   if (W == 0 && acc[0] == 123.456f) out[0][0] = acc[1];   // keep the loads live
 }
 
+// SPLIT: the same rows and bytes as mix<2, 4, 5, 1, true>, but waves 0-3 only stream (2 reads, 5 nt writes
+// of each row) and waves 4-7 only gather (the 4 P / Q rows of each edge, summed into a register): is the
+// gathers' cost their own, or the streams' waits behind them in the same waves?
+__global__ __launch_bounds__(THREADS) void split_mix(const float* const* __restrict__ in, float* const* __restrict__ out,
+                                                     const int* __restrict__ gd, const int* __restrict__ gs,
+                                                     const float* __restrict__ P, const float* __restrict__ Q, int E) {
+  const int nb = gridDim.x;
+  int per = (E + nb - 1) / nb;
+  per = (per + ROUND - 1) / ROUND * ROUND;
+  const int r0 = min(E, per * (int)blockIdx.x), r1 = min(E, per * ((int)blockIdx.x + 1));
+  if (r0 >= r1) return;
+  const int t = threadIdx.x & 255, c = 4 * (t & 31), rr = t >> 5;   // 8 rows per instruction, 4 slots
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (threadIdx.x < 256) {
+    f32x4 v[2][4];
+    auto issue = [&](int base) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = clampr(base + rr + 8 * u, r1);
+#pragma unroll
+        for (int a = 0; a < 2; ++a) v[a][u] = *reinterpret_cast<const f32x4*>(in[a] + (size_t)row * L + c);
+      }
+    };
+    issue(r0);
+    for (int base = r0; base < r1; base += ROUND) {
+      f32x4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = v[0][u] + v[1][u];
+      issue(base + ROUND);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = clampr(base + rr + 8 * u, r1);
+#pragma unroll
+        for (int a = 0; a < 5; ++a)
+          __builtin_nontemporal_store(x[u] + (float)a, reinterpret_cast<f32x4*>(out[a] + (size_t)row * L + c));
+      }
+    }
+  } else {
+    int di[4], si[4];
+    f32x4 g[4][4];
+    auto ids = [&](int base) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int row = clampr(base + rr + 8 * u, r1);
+        di[u] = gd[row];
+        si[u] = gs[row];
+      }
+    };
+    ids(r0);
+    for (int base = r0; base < r1; base += ROUND) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        g[0][u] = *reinterpret_cast<const f32x4*>(P + (size_t)di[u] * L + c);
+        g[1][u] = *reinterpret_cast<const f32x4*>(Q + (size_t)si[u] * L + c);
+        g[2][u] = *reinterpret_cast<const f32x4*>(P + (size_t)si[u] * L + c);
+        g[3][u] = *reinterpret_cast<const f32x4*>(Q + (size_t)di[u] * L + c);
+      }
+      ids(base + ROUND);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += (g[0][u] + g[1][u]) + (g[2][u] + g[3][u]);
+    }
+    if (acc[0] == 123.456f) out[0][0] = acc[1];
+  }
+}
+
 __global__ void copy4(const f32x4* __restrict__ a, f32x4* __restrict__ b, size_t n) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) b[i] = a[i];
 }
@@ -220,16 +285,17 @@ int main() {
     (void)hipFree(a);
     (void)hipFree(b);
   }
-  // the edge forward's mix: contiguous block ranges (the kernels' block_rows) vs XCD-interleaved rounds,
-  // gathers from the N-node tables vs the same pattern on a 1k-node (L2-resident) table, and no gathers
+  // the edge forward's mix in one set of waves vs split over stream waves and gather waves
   for (int rep = 0; rep < 2; ++rep) {
     run<2, 4, 5, 1, true>(B, cus);
-    run<2, 4, 5, 1, true, 1, true>(B, cus);
-    run<2, 4, 5, 1, true>(B, cus, true);
-    run<2, 2, 5, 1, true>(B, cus);
     run<2, 0, 5, 1, true>(B, cus);
     run<0, 4, 0, 1, true>(B, cus);
-    run<0, 4, 0, 1, true>(B, cus, true);
+    const double us = time_us([&] {
+      hipLaunchKernelGGL(split_mix, dim3(cus), dim3(THREADS), 0, 0, B.d_in, B.d_out, B.gd, B.gs, B.P, B.Q, B.E);
+    });
+    printf("{\"mix\": \"2R+4G+5W split waves (0-3 stream, 4-7 gather)\", \"us\": %.1f, \"streamed_TBps\": %.3f}\n", us,
+           (double)B.E * 512.0 * 7 / us * 1e-6);
+    fflush(stdout);
   }
   return 0;
 }

@@ -4,6 +4,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R" || exit 1
 O=gpurun_out/r04c
 mkdir -p $O
+timeout -k 10 120 tools/membench2 > $O/membench2.jsonl 2>&1 || { tail -5 $O/membench2.jsonl; exit 1; }
+cat $O/membench2.jsonl
 timeout -k 10 300 python tools/grad_err_golden.py batch2_div_s10 > $O/grad_err.txt 2>&1 || { tail -5 $O/grad_err.txt; exit 1; }
 cat $O/grad_err.txt
 PDG_LIB=variants/unb/libpdivgnn_hip.so timeout -k 10 300 python tools/grad_err_golden.py batch2_div_s10 > $O/grad_err_unb.txt 2>&1 || { tail -5 $O/grad_err_unb.txt; exit 1; }
