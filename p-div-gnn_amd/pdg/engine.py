@@ -279,8 +279,15 @@ class EPDEngine:
         a1_ne, a2_ne = self._empty(N, L), self._empty(N, L)
         lib.pdg_encoder_fwd(N, 6, _p(x_in), _p(P["node_encoder.0.weight"]), _p(P["node_encoder.0.bias"]),
                             _p(P["node_encoder.2.weight"]), _p(P["node_encoder.2.bias"]), _p(a1_ne), _p(a2_ne),
-                            _p(self._part_a), np_, s)
-        self._finalize(self._part_a, N * L, st[0], s)
+                            _p(self._part_b), np_, s)
+        # the node encoder's LayerNorm statistics are reduced inside step 0's node_pq (pdg_node_pq_rw_fin, as
+        # every later step's; one launch fewer), its partials in _part_b until then (the edge encoder and the
+        # first edge forward write _part_a / _part_b only after that node_pq)
+        pend_n, pend_buf = None, self._part_b
+        if self.sync is None:
+            pend_n = self._nparts.value
+        else:
+            self._finalize(self._part_b, N * L, st[0], s)
         # the edge encoder's layer-1 output is stored only for the unfused backward (pdg_mlp2_bwd);
         # pdg_edge_enc_bwd recomputes it from the scalar input
         a1_ee = self._empty(E, L) if (need_grad and not self.fused_edge_wgrad) else None
@@ -315,14 +322,14 @@ class EPDEngine:
         rc = (need_grad and bool(E) and self.recompute_a1 and self.fused_edge_wgrad and self.coop_fwd
               and not self.seg_sums_train)
         Pm, Qm = self._empty(N, L), self._empty(N, L)
-        pend_n = None                        # deferred node LayerNorm statistics (nparts)
+        # pend_n: deferred node LayerNorm statistics (nparts of the partials in pend_buf)
         for t in range(steps):
             i_m, i_e, i_n = 2 + 3 * t, 3 + 3 * t, 4 + 3 * t
             x_t = self._empty(N, L)
             if rc and t > 0:
                 Pm, Qm = self._empty(N, L), self._empty(N, L)
             if pend_n is not None:    # the previous step's node statistics, reduced inside node_pq
-                self._t("node_pq", lib.pdg_node_pq_rw_fin, N, _p(a2n_prev), self._part_a.data_ptr(), pend_n,
+                self._t("node_pq", lib.pdg_node_pq_rw_fin, N, _p(a2n_prev), pend_buf.data_ptr(), pend_n,
                         float(N * L), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_t), _p(W1), _p(Pm),
                         _p(Qm), s)
                 pend_n = None
@@ -396,7 +403,7 @@ class EPDEngine:
             self._t("node_net", lib.pdg_node_net, N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(Wn2), _p(bn2), _p(a1n),
                     _p(a2n), _p(self._part_a), np_, s)
             if t < steps - 1 and self.sync is None:
-                pend_n = self._nparts.value          # finalised by the next step's node_pq
+                pend_n, pend_buf = self._nparts.value, self._part_a   # finalised by the next step's node_pq
             else:
                 self._finalize(self._part_a, N * L, st[i_n], s)
             if need_grad:
