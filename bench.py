@@ -64,7 +64,9 @@ PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd
              "edge_bwd_w2": ("void edge_bwd_w2_kernel<true, false>", "void edge_bwd_w2_kernel<true, true>",
                              "void edge_bwd_w2_kernel<true>"),
              "edge_gout": ("void edge_gout_wc_kernel<true, false>", "void edge_gout_wc_kernel<true, true>",
-                           "void edge_gout_wc_kernel<true>")}
+                           "void edge_gout_wc_kernel<true>"),
+             "node_bwd": "node_bwd_coop_kernel", "node_pq": "void node_pq_x6_kernel<true>",
+             "gemm_sum2": "void gemm_sum2_coop_kernel<true>", "wgrad_pairs": "void wgrad_x6_pair2_kernel"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
 PEAK_BF16_MFMA = 16 * PEAK_FP32_MFMA   # dense bf16 MFMA (2.5 PF; the fp32 rate is 1/16 of it, same guide)
 X6 = 6                      # bf16x6: six bf16 products per fp32-accurate product
@@ -315,6 +317,38 @@ def load_pmc(fused: bool, path=None) -> dict:
     return pmc
 
 
+SQ_GLOB = "profiles/r*_sq.json"   # tools/sq_pass.sh (SQ_VALU_MFMA_BUSY_CYCLES per dispatch, tools/sq_summary.py)
+
+
+def sq_file(tree: str | None = None):
+    """(path, None) of the newest profiles/rNN_sq.json measured on this tree, or (None, reason)."""
+    tree = tree or tree_hash()
+    files = sorted(ROOT.glob(SQ_GLOB), reverse=True)
+    if not files:
+        return None, "no profiles/r*_sq.json"
+    for f in files:
+        try:
+            if json.loads(f.read_text()).get("_meta", {}).get("tree") == tree:
+                return f, None
+        except (OSError, ValueError):
+            continue
+    return None, f"no SQ counter file of tree {tree}"
+
+
+def load_sq(path) -> dict:
+    """Counter MFMA busy fraction (at the nominal 2.4 GHz) per bench kernel key, from an sq_file()."""
+    out = {}
+    if path is None:
+        return out
+    rows = json.loads(Path(path).read_text()).get("kernels", [])
+    for k, prefix in PMC_NAMES.items():
+        pre = prefix if isinstance(prefix, tuple) else (prefix,)
+        hit = [r for r in rows if r["kernel"].startswith(pre) and r.get("mfma_busy_at_2.4GHz") is not None]
+        if hit:
+            out[k] = round(hit[0]["mfma_busy_at_2.4GHz"], 4)
+    return out
+
+
 def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None, pmc_source=None):
     nlaunch = nlaunch or {}
     terms, nbytes = work[k]
@@ -473,6 +507,8 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg, rc)
     pmc_path, pmc_reason = pmc_file() if with_pmc else (None, "not collected for this config")
     pmc = load_pmc(fused, pmc_path)
+    sq_path, sq_reason = sq_file() if with_pmc else (None, "not collected for this config")
+    sq = load_sq(sq_path)
     step_s = el * ev_steps / args.steps
     dominant = max([k for k in ("edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2") if k in ktot], key=lambda k: ktot[k])
     strong = bool(cfg.get("global_batch"))
@@ -498,6 +534,10 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
         "roofline_node_net": (roofline("node_net", work, kt, ktot, step_s, pmc, nlaunch, pmc_path)
                               if "node_net" in kt else None),
         "traffic_null_reason": pmc_reason,
+        # MFMA busy from rocprofv3 SQ counters of this tree (tools/sq_pass.sh), beside each roofline's
+        # flop-derived frac_mfma: {bench kernel key: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x 2.4 GHz x duration)}
+        "mfma_busy_counters": sq or None,
+        "mfma_busy_source": (f"profiles/{Path(sq_path).name}" if sq_path else sq_reason),
         "kernel_ms": {k: round(v * 1e3, 4) for k, v in kt.items()},
     }
     del trainer, model, batch, plan

@@ -48,3 +48,14 @@ def test_roofline_without_traffic_has_no_pmc_fraction():
     work = {"edge_fwd": ([(1e9, bench.PEAK_FP32_MFMA)], 1.0e9)}
     r = bench.roofline("edge_fwd", work, {"edge_fwd": 2e-4}, {"edge_fwd": 2e-3}, 8e-3, {}, {"edge_fwd": 10}, None)
     assert r["traffic"] is None and r["frac_pmc"] is None and r["traffic_source"] is None
+
+
+def test_sq_counters_only_from_this_tree(tmp_path, monkeypatch):
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    (tmp_path / "profiles").mkdir()
+    rec = {"_meta": {"tree": "aaaa"}, "kernels": [{"kernel": NAME, "mfma_busy_at_2.4GHz": 0.42}]}
+    (tmp_path / "profiles" / "r09_sq.json").write_text(json.dumps(rec))
+    path, reason = bench.sq_file("bbbb")
+    assert path is None and "bbbb" in reason
+    path, reason = bench.sq_file("aaaa")
+    assert reason is None and bench.load_sq(path) == {"edge_fwd": 0.42}

@@ -51,6 +51,7 @@ if [ "$WHAT" = measure ]; then
   # SQ counters of the same tree (MFMA busy, wave-cycle split), two passes with kernel traces
   bash tools/sq_pass.sh "$TAG/sq" > "$O/sq_pass.log" 2>&1 || { tail -5 "$O/sq_pass.log"; exit 1; }
   cp "$R/gpurun_out/$TAG/sq/sq.txt" "$R/profiles/${ROUND:-r04}_sq.txt"
+  cp "$R/gpurun_out/$TAG/sq/sq.json" "$R/profiles/${ROUND:-r04}_sq.json"
   python -c "import json; d = json.load(open('$O/bench_line.json')); print(d['value'], d['ms_per_step'], d['tree'], d['traffic_tree_match'], d['roofline'])"
 fi
 echo "all done"
