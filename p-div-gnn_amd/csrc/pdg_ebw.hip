@@ -124,21 +124,13 @@ __device__ __forceinline__ void wgrad_round(f32x16 (&acc)[2], const unsigned cha
 
 // d[nb] = (W^T-slice x image rows 16 nb .. 16 nb + 15): D row = output feature 16w + 4(l >> 4) + j,
 // column = staged row 16 nb + (l & 15).  NI images share the weight operands.
-// PDG_X6_UNBIASED: each 32-wide K chunk's five small products chained from zero and hi x hi formed from
-// zero, both added to d by fp32 VALU adds (gemm_x6f's unbiased accumulation, pdg_x6.hpp), instead of one
-// chain through d (the bf16 MFMA rounds its accumulator input with a bias of about -6e-10 of the
-// magnitude, tools/mfma_round.py).
-#ifndef PDG_X6_UNBIASED
-#define PDG_X6_UNBIASED 0
-#endif
 template <int NI, int NB = 2, int TERM = X6_TERM>
 __device__ __forceinline__ void gemm_round(f32x4 (&d)[NI][NB], const WSlice& ws, const unsigned char* const (&img)[NI]) {
   const int l = lane_id(), n = l & 15, kg = l >> 4;
-  f32x4 sm[NI][NB];   // PDG_X6_UNBIASED: the small-term chain (2^-8 of the product: its bias is negligible)
 #pragma unroll
   for (int u = 0; u < NI; ++u)
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) d[u][nb] = sm[u][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int nb = 0; nb < NB; ++nb) d[u][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
@@ -149,19 +141,6 @@ __device__ __forceinline__ void gemm_round(f32x4 (&d)[NI][NB], const WSlice& ws,
         bf16x8 B[3];
 #pragma unroll
         for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(img[u] + p * TERM + off);
-        if (PDG_X6_UNBIASED) {   // small terms chained in sm (all K chunks), hi x hi from zero into d
-          const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-          f32x4 t = sm[u][nb];
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][2], B[0], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][1], B[1], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][0], B[2], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][1], B[0], t, 0, 0, 0);
-          sm[u][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][0], B[1], t, 0, 0, 0);
-          const f32x4 hh = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][0], B[0], z, 0, 0, 0);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) d[u][nb][j] += hh[j];
-          continue;
-        }
         f32x4 t = d[u][nb];
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][2], B[0], t, 0, 0, 0);
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][1], B[1], t, 0, 0, 0);
@@ -171,11 +150,6 @@ __device__ __forceinline__ void gemm_round(f32x4 (&d)[NI][NB], const WSlice& ws,
         d[u][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][0], B[0], t, 0, 0, 0);
       }
   }
-  if (PDG_X6_UNBIASED)
-#pragma unroll
-    for (int u = 0; u < NI; ++u)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) d[u][nb] += sm[u][nb];
 }
 
 // Block's row range: contiguous, a multiple of 32 rows except at the end.

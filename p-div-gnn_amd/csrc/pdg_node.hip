@@ -347,8 +347,8 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
     const int row = tile * TILE + r;
     // layer 1: a1 = relu(W1a aggr + W1b x + b1), the aggr chunks first
     f32x4 d1[1] = {{0.f, 0.f, 0.f, 0.f}};
-    gemm_x6f<1, NN_T16>(d1, w1a, xin + (2 * (i % 3)) * NN_IMG);
-    gemm_x6f<1, NN_T16>(d1, w1b, xin + (2 * (i % 3) + 1) * NN_IMG);
+    gemm_x6f<1, NN_T16, true>(d1, w1a, xin + (2 * (i % 3)) * NN_IMG);
+    gemm_x6f<1, NN_T16, true>(d1, w1b, xin + (2 * (i % 3) + 1) * NN_IMG);
     f32x4 a1;
 #pragma unroll
     for (int c = 0; c < 4; ++c) a1[c] = fmaxf(d1[0][c] + bias1[c], 0.f);
@@ -360,7 +360,7 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
 #endif
     // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
     f32x4 d2[1] = {{0.f, 0.f, 0.f, 0.f}};
-    gemm_x6f<1, NN_T16>(d2, w2, a1i + (i & 1) * NN_IMG);
+    gemm_x6f<1, NN_T16, true>(d2, w2, a1i + (i & 1) * NN_IMG);
     f32x4 a2;
 #pragma unroll
     for (int c = 0; c < 4; ++c) a2[c] = fmaxf(d2[0][c] + bias2[c], 0.f);

@@ -92,13 +92,12 @@ __device__ __forceinline__ void load_wslice(WSlice& ws, const float* __restrict_
 // it is unbiased, and over K = 128 this scheme measured a mean error of -2.7e-11 of the product scale
 // (fp32 MFMA chain: -2.9e-11; one bf16x6 chain: -1.1e-9) at 3.6x less rms error than the fp32 MFMA
 // chain.  Six bf16 MFMAs per chunk cost 2.7x less matrix time than the fp32 MFMAs of the same K.
-// PDG_X6F_CHAIN: the five small products of all four K chunks in ONE chain (its accumulator bias is
-// relative to the small terms, 2^-8 of the product) added to d once at the end, hi x hi still from zero
-// per chunk: one VALU add per element and chunk instead of two.
-#ifndef PDG_X6F_CHAIN
-#define PDG_X6F_CHAIN 0
-#endif
-template <int NB, int TERM>
+// CHAIN: the five small products of all four K chunks in ONE chain (its accumulator bias is relative to
+// the small terms, 2^-8 of the product) added to d once at the end, hi x hi still from zero per chunk:
+// one VALU add per element and chunk instead of two.  node_net: 37.2-37.7 -> 33.9-34.4 us per config-2
+// call (two same-box A/B pairs; op tests against fp64 with the bias check green); node_pq measured
+// 26.7-26.9 -> 28.0-28.4 us with it and keeps the per-chunk form.
+template <int NB, int TERM, bool CHAIN = false>
 __device__ __forceinline__ void gemm_x6f(f32x4 (&d)[NB], const WSlice& ws, const unsigned char* img) {
   const int l = lane_id(), n = l & 15, kg = l >> 4;
   const f32x4 z = {0.f, 0.f, 0.f, 0.f};
@@ -113,7 +112,7 @@ __device__ __forceinline__ void gemm_x6f(f32x4 (&d)[NB], const WSlice& ws, const
       bf16x8 B[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(img + p * TERM + off);
-      if (PDG_X6F_CHAIN) {
+      if (CHAIN) {
         f32x4 t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][2], B[0], smc[nb], 0, 0, 0);
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][1], B[1], t, 0, 0, 0);
         t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[ks][0], B[2], t, 0, 0, 0);
@@ -133,7 +132,7 @@ __device__ __forceinline__ void gemm_x6f(f32x4 (&d)[NB], const WSlice& ws, const
 #pragma unroll
       for (int j = 0; j < 4; ++j) d[nb][j] += hh[j] + sm[j];
     }
-  if (PDG_X6F_CHAIN)
+  if (CHAIN)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) d[nb] += smc[nb];
 }
