@@ -200,9 +200,6 @@ int pdg_ln_colsum_finalize(const double* partials, int nparts, const float* ln_g
  * acc/rows/grad_g/grad_b are HOST arrays of device pointers. */
 int pdg_ln_param_grads(int ngroups, const double* const* acc, const int* rows, float* const* grad_g,
                        float* const* grad_b, void* stream);
-/* Sync DP mode, backward: after lb->S1 and lb->S2 were all-reduced over ranks, recompute
- * lb->c1 = S1/M and lb->c2 = S2/(M std) with the global statistics in st. */
-int pdg_ln_bwd_rescale(const pdg_ln_stat* st, pdg_ln_bwd* lb, void* stream);
 
 /* MLP tail backward (LN -> relu -> Linear2 -> relu): ga2 = LNbwd(gy); gz2 = ga2 * [a2 > 0];
  * gz1 = (W2^T gz2) * [a1 > 0].  gy row k = gy_rows[gidx ? gidx[k] : k]. */
@@ -463,8 +460,6 @@ int pdg_wgrad_segments_batch(int njobs, const int* nseg, const float* const* g_p
 int pdg_wgrad_reduce_batch(int njobs, const float* const* slabs, const int* nslabs, float* const* grad_W,
                            const int* ld, const int* col0, float* const* grad_b, void* stream);
 int pdg_transpose128_batch(int n, const float* const* in_ptrs, const int* lds, float* const* out_ptrs, void* stream);
-/* *flag = 1 if any grad element is inf/NaN (GradScaler's skip test, gnn_train.py:205-207). */
-int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream);
 /* pdg_nonfinite + the zero-mean-stress skip in one launch, no memset: flags[2] double-buffered by call
  * parity; flags[parity] = any non-finite x[i] || (zero_flag && *zero_flag == 0), and flags[parity ^ 1] is
  * cleared for the next call (replaces GradScaler's inf check, gnn_train.py:205-207, and the guard of

@@ -327,24 +327,6 @@ extern "C" int pdg_ln_param_grads(int ngroups, const double* const* acc, const i
   return PDG_OK;
 }
 
-// Exact data-parallel LayerNorm backward: after S1/S2 of `lb` have been all-reduced
-// over the process group, recompute c1 = S1/M, c2 = S2/(M sd) with the global count
-// and std held in `st` (same formulas as ln_colsum_finalize_kernel).
-__global__ void ln_bwd_rescale_kernel(const pdg_ln_stat* __restrict__ stp, pdg_ln_bwd* __restrict__ lb) {
-  if (threadIdx.x != 0) return;
-  const double M = stp->count, sd = stp->std_d;
-  const double s1 = lb->S1, s2 = lb->S2;
-  lb->c1 = (float)(s1 / M);
-  lb->c2 = sd > 0 ? (float)(s2 / (M * sd)) : 0.f;
-}
-
-extern "C" int pdg_ln_bwd_rescale(const pdg_ln_stat* st, pdg_ln_bwd* lb, void* stream) {
-  PDG_CHECK_ARG(st && lb, "pdg_ln_bwd_rescale: null");
-  hipLaunchKernelGGL(ln_bwd_rescale_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, st, lb);
-  PDG_CHECK_LAUNCH("pdg_ln_bwd_rescale");
-  return PDG_OK;
-}
-
 // ============================================================================ MLP tail backward
 __global__ __launch_bounds__(384, 3) void mlp2_bwd_kernel(int M, const float* __restrict__ gyr,
                                                            const int* __restrict__ gidx,

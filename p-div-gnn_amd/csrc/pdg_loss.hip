@@ -299,28 +299,6 @@ extern "C" int pdg_transpose128_batch(int n, const float* const* in_ptrs, const 
   return PDG_OK;
 }
 
-// GradScaler's skip test (gnn_train.py:205-207).
-__global__ void nonfinite_kernel(const float* __restrict__ x, long n, int* __restrict__ flag) {
-  int bad = 0;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    bad |= !isfinite(x[i]);
-  if (__any(bad) && lane_id() == 0) atomicOr(flag, 1);
-}
-
-extern "C" int pdg_nonfinite(const float* x, int64_t n, int* flag, void* stream) {
-  PDG_CHECK_ARG(n >= 0 && flag != nullptr, "pdg_nonfinite: bad args");
-  if (hipMemsetAsync(flag, 0, sizeof(int), (hipStream_t)stream) != hipSuccess) {
-    set_error("pdg_nonfinite: memset failed");
-    return PDG_ERR_HIP;
-  }
-  if (n == 0) return PDG_OK;
-  long blocks = (n + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, (long)n, flag);
-  PDG_CHECK_LAUNCH("pdg_nonfinite");
-  return PDG_OK;
-}
-
 // The step's non-finite test and the zero-mean-stress skip in one launch, with no memset: flags[2] is
 // double-buffered by call parity (as Adam's step count): every block ORs into flags[parity], block 0
 // clears flags[parity ^ 1] for the next call (which runs after this one on the stream).  *zero_flag (a

@@ -46,7 +46,6 @@ SIGNATURES: dict[str, list] = {
     "pdg_ln_finalize2": [P, P, I, c_double, P, P, P],
     "pdg_node_pq_rw_fin": [I, P, P, I, c_double, P, P, P, P, P, P, P, P, P],
     "pdg_ln_partials_sum": [P, I, P, P],
-    "pdg_ln_bwd_rescale": [P, P, P],
     "pdg_node_pq": [I, P, P, P, P, P, P, P, P, P, P],
     "pdg_node_pq_rw": [I, P, P, P, P, P, P, P, P, P, P],
     "pdg_edge_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
@@ -101,7 +100,6 @@ SIGNATURES: dict[str, list] = {
     "pdg_div_fwd": [I, P, P, P, P, P, P, I, P, P, P],
     "pdg_div_bwd": [I, P, I, P, P, P, P, P, P, I, I, P, P],
     "pdg_transpose": [I, I, I, P, P, P],
-    "pdg_nonfinite": [P, c_int64, P, P],
     "pdg_nonfinite2": [P, c_int64, P, P, I, P],
     "pdg_loss_reduce": [I, P, P, c_float, c_float, P, P, P],
     "pdg_collate": [P, I, ctypes.c_long, P],
