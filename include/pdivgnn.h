@@ -320,8 +320,9 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
  * slab map is fixed and the slabs accumulate, reduced once by pdg_wgrad_reduce).
  *   pdg_edge_bwd_w2:  gz1m/gz1e/gC as pdg_edge_bwd; slabs (zeroed before the first call)
  *                     += gz2m^T a1m + gz2e^T a1e and the b2 column sums; gz2m/gz2e are not
- *                     materialised.  ge_next == NULL: message branch only, gC = gz1m.  gC may
- *                     be NULL (not written; pdg_edge_gout_wc2 forms it).
+ *                     materialised.  ge_next == NULL: message branch only, gC = gz1m (gC may
+ *                     then be the gz1m pointer itself: written once).  gC may be NULL (not
+ *                     written; pdg_edge_gout_wc2 forms it).
  *   pdg_edge_gout_wc: ge_out = [ge_next +] WcT gC; slabs += gC^T e and the b1 column sums.
  *                     a2ln != NULL: also the column sums of the backward of the LayerNorm that
  *                     produced e (input a2ln, statistics st_ln, upstream gradient ge_out), as

@@ -311,7 +311,10 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   // no memory operation below is conditional (rows past the block's end are clamped on load and
   // dropped by the buffer range check on store), so the compiler can count the loads in flight: a
   // skipped store or load on some path made it wait for all of them (vmcnt(0)) in the stage
-  const __amdgpu_buffer_rsrc_t out_m = rows_rsrc(gz1m, r0, r1), out_c = rows_rsrc(gC, r0, r1);
+  // without the edge update gC = gz1m: a caller passing gC == gz1m gets it written once (an empty range
+  // drops the second store)
+  const __amdgpu_buffer_rsrc_t out_m = rows_rsrc(gz1m, r0, r1);
+  const __amdgpu_buffer_rsrc_t out_c = rows_rsrc(EU || gC != gz1m ? gC : nullptr, r0, r1);
   const __amdgpu_buffer_rsrc_t out_e = rows_rsrc(EU ? gz1e : gz1m, r0, r1);
   dn[0] = dst[clamp_row(first + rg, r1)];   // E > 0: an empty block (first = r1 = E) reads row E - 1
   dn[1] = dst[clamp_row(first + R16 + rg, r1)];
@@ -1715,6 +1718,7 @@ static int edge_bwd_w2_launch(int n_edges, const int* dst, const float* gaggr, c
   PDG_CHECK_ARG(!rc || (src && P && Q && PDG_ALIGNED(C) && PDG_ALIGNED(P) && PDG_ALIGNED(Q)),
                 "pdg_edge_bwd_w2_rc: src / C / P / Q missing or misaligned");
   const bool eu = ge_next != nullptr;
+  PDG_CHECK_ARG(!eu || gC != gz1m, "pdg_edge_bwd_w2: gC may alias gz1m only without the edge update");
   PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && (rc || a1e) && gz1e && st_e && (lb_e || pairs_e) &&
                         PDG_ALIGNED(a2e) && (rc || PDG_ALIGNED(a1e)) && PDG_ALIGNED(gz1e)),
                 "pdg_edge_bwd_w2: edge-update arguments missing or misaligned");

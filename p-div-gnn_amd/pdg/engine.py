@@ -546,6 +546,8 @@ class EPDEngine:
             assert E == 0 or eu == (ge_next is not None)
             gz2n, gz1n, gP, gQ = (self._empty(N, L) for _ in range(4))
             gC = gC_fused if fused else self._empty(E, L)   # fused: consumed within the step
+            if fused and not eu and not gz1_in_gout:
+                gC = gz1m   # message branch only: gC = gz1m, written once (pdg_edge_bwd_w2)
             gz2m = None if fused else self._empty(E, L)
             gz2e = self._empty(E, L) if (eu and not fused) else None
             ge_out = ge_bufs[t % 2]
