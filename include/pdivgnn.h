@@ -209,16 +209,24 @@ int pdg_mlp2_bwd(int rows, const float* gy_rows, const int* gidx, const float* a
 
 /* pdg_decoder_bwd in the block-cooperative layout (the Wd1^T product in bf16x6). With partials != NULL
  * it also forms pdg_ln_colsum's column partials / (S1, S2) pairs of gx for the LayerNorm with output
- * statistics ln_st over ln_a2 (one partial per block: *nparts = nblocks), as pdg_gemm_sum2_coop. */
+ * statistics ln_st over ln_a2 (one partial per block: *nparts = nblocks), as pdg_gemm_sum2_coop.
+ * narrow_partials != NULL: also node_decoder.2's weight / bias gradient (models.py:316-321 backward,
+ * pdg_wgrad_narrow(rows, a1d, gy, 3, ...)'s block partials, nblocks of them) for
+ * pdg_wgrad_narrow_finalize(narrow_partials, nblocks, 3, 1, ...): one pass over a1d / gy fewer. */
 int pdg_decoder_bwd_coop(int rows, const float* gy, const float* a1d, const float* Wd2, const float* Wd1T,
                          float* gz1d, float* gx, const float* ln_a2, const pdg_ln_stat* ln_st, double* partials,
-                         const float* ln_g, double* pairs, int accumulate, int nblocks, void* stream);
+                         const float* ln_g, double* pairs, int accumulate, double* narrow_partials, int nblocks,
+                         void* stream);
 
 /* pdg_mlp2_bwd (gidx = NULL) in the block-cooperative layout: the W2^T product in bf16x6 with W2^T
- * stationary in registers, whole-row access (the node encoder's backward). */
+ * stationary in registers, whole-row access (the node encoder's backward).  x_narrow != NULL (rows x 6,
+ * the encoder input): also the first layer's weight / bias gradient from gz1, as the block partials of
+ * pdg_wgrad_narrow(rows, gz1, x_narrow, 6, ...) in narrow_partials (nblocks of them, for
+ * pdg_wgrad_narrow_finalize(narrow_partials, nblocks, 6, 0, ...)); gz1 may then be NULL (not stored). */
 int pdg_mlp2_bwd_coop(int rows, const float* gy, const float* a2, const float* a1, const pdg_ln_stat* st,
                       const pdg_ln_bwd* lb, const float* ln_g, const float* W2T, float* gz2, float* gz1,
-                      const double* lb_pairs, int lb_npairs, int nblocks, void* stream);
+                      const double* lb_pairs, int lb_npairs, const float* x_narrow, double* narrow_partials,
+                      int nblocks, void* stream);
 
 /* Fused node_net backward of one step (the work of pdg_mlp2_bwd + pdg_gemm_dual with
  * res0 = NULL, res1 = gy): gz2 = LN_bwd(gy) * [a2n > 0]; gz1 = (Wn2^T gz2) * [a1n > 0];
@@ -422,6 +430,10 @@ int pdg_wgrad_pairs(int nseg, const float* const* a0_ptrs, const float* const* a
 int pdg_wgrad_narrow(int rows, const float* wide, const float* narrow, int k_narrow, int transpose,
                      double* partials, float* grad_W, float* grad_b_wide, float* grad_b_narrow,
                      void* stream);
+/* The finalize step of pdg_wgrad_narrow alone (grad_W / grad_b_* += the reduced block partials, in
+ * pdg_wgrad_narrow's order), for partials formed inside pdg_mlp2_bwd_coop / pdg_decoder_bwd_coop. */
+int pdg_wgrad_narrow_finalize(const double* partials, int nparts, int k_narrow, int transpose, float* grad_W,
+                              float* grad_b_wide, float* grad_b_narrow, void* stream);
 
 /* ---------------------------------------------------------------- losses */
 

@@ -1516,6 +1516,35 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd2_kernel(
   }
 }
 
+// ============================================================================ narrow weight gradients
+// The block partial of a narrow weight gradient T[c][i] = sum_rows wide[c] narrow[i] (c < 128, i < K) in
+// wgrad_narrow_kernel's layout [T (128 K) | wide sums (128) | narrow sums (K)], reduced by
+// pdg_wgrad_narrow_finalize.  Thread (rg, cg) holds the fp64 sums of columns 4cg .. 4cg + 3 over the rows
+// it visited (t[4 K + 4 + K]: products, wide sums, narrow sums — the narrow sums counted by the cg = 0
+// threads only); the 16 row groups are added in order through LDS (`red`: 16 x tot doubles).
+template <int K>
+__device__ __forceinline__ void narrow_emit(const double (&t)[4 * K + 4 + K], double* red, double* __restrict__ out) {
+  constexpr int tot = L * K + L + K;
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  __syncthreads();   // the caller's LDS is free
+  double* mine = red + rg * tot;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) mine[(4 * cg + c) * K + i] = t[c * K + i];
+    mine[L * K + 4 * cg + c] = t[4 * K + c];
+  }
+  if (cg == 0)
+#pragma unroll
+    for (int i = 0; i < K; ++i) mine[L * K + L + i] = t[4 * K + 4 + i];
+  __syncthreads();
+  for (int e = threadIdx.x; e < tot; e += blockDim.x) {
+    double v = 0;
+    for (int g = 0; g < EBW_THREADS / 32; ++g) v += red[g * tot + e];
+    out[(size_t)blockIdx.x * tot + e] = v;
+  }
+}
+
 // ============================================================================ encoder backward
 // pdg_mlp2_bwd in the cooperative layout (the node encoder's backward, models.py:264-275 for the
 // 6-input encoder): gz2 = LN_bwd(gy) [a2 > 0] (whole rows -> HBM and a bf16x6 image),
@@ -1525,7 +1554,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void mlp2_bwd_coop_kernel(
     int N, const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ a1,
     const pdg_ln_stat* __restrict__ stp, const pdg_ln_bwd* __restrict__ lbp, const double* __restrict__ lb_pairs,
     int lb_npairs, const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ gz2_out,
-    float* __restrict__ gz1_out) {
+    float* __restrict__ gz1_out, const float* __restrict__ xn, double* __restrict__ npart) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img2 = sm;                                    // gz2
   unsigned char* msk = sm + EBW_IMG;                           // [a1 > 0]
@@ -1540,14 +1569,25 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void mlp2_bwd_coop_kernel(
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const pdg_ln_bwd lb = lnb_resolve(lbp, lb_pairs, lb_npairs, stp);
   const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+  // xn != NULL: the first layer's weight gradient from the gz1 rows of the epilogue (wgrad_narrow_kernel<6>'s
+  // products and order per row, wide = gz1, narrow = xn = the encoder input), gz1 itself not needed
+  constexpr int NK = 6, NT = 4 * NK + 4 + NK;
+  double nt[NT];
+#pragma unroll
+  for (int p = 0; p < NT; ++p) nt[p] = 0;
   f32x4 pg[2], pa2[2], pa1[2];
+  float px[2][NK], xv[2][NK];
   auto issue = [&](int base) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
+      const int rr = clamp_row(base + rg + 16 * u, r1);
+      const size_t rc = (size_t)rr * L + 4 * cg;
       pg[u] = *reinterpret_cast<const f32x4*>(gy + rc);
       pa2[u] = *reinterpret_cast<const f32x4*>(a2 + rc);
       pa1[u] = *reinterpret_cast<const f32x4*>(a1 + rc);
+      if (xn)
+#pragma unroll
+        for (int i = 0; i < NK; ++i) px[u][i] = xn[(size_t)rr * NK + i];
     }
   };
   if (r0 < r1) issue(r0);
@@ -1561,6 +1601,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void mlp2_bwd_coop_kernel(
       if (ok) stnt4(gz2_out + (size_t)(base + r) * L + 4 * cg, z2);
       img_store4(img2, r, cg, z2);
       *reinterpret_cast<unsigned*>(msk + r * MSK_STRIDE + 4 * cg) = relu_mask4(pa1[u]);
+#pragma unroll
+      for (int i = 0; i < NK; ++i) xv[u][i] = px[u][i];
     }
     __syncthreads();   // gz2 image and the a1 mask complete
     if (base + X6_ROWS < r1) issue(base + X6_ROWS);
@@ -1580,10 +1622,23 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void mlp2_bwd_coop_kernel(
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r = rg + 16 * u;
-      if (base + r < r1)
-        stnt4(gz1_out + (size_t)(base + r) * L + 4 * cg, *reinterpret_cast<const f32x4*>(t_z + r * OT_STRIDE + 4 * cg));
+      if (base + r < r1) {
+        const f32x4 z1 = *reinterpret_cast<const f32x4*>(t_z + r * OT_STRIDE + 4 * cg);
+        if (gz1_out) stnt4(gz1_out + (size_t)(base + r) * L + 4 * cg, z1);
+        if (xn) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+#pragma unroll
+            for (int i = 0; i < NK; ++i) nt[c * NK + i] += (double)(z1[c] * xv[u][i]);
+            nt[4 * NK + c] += (double)z1[c];
+          }
+#pragma unroll
+          for (int i = 0; i < NK; ++i) nt[4 * NK + 4 + i] += (double)xv[u][i];
+        }
+      }
     }
   }
+  if (xn) narrow_emit<NK>(nt, reinterpret_cast<double*>(sm), npart);
 }
 
 // ============================================================================ decoder backward
@@ -1597,10 +1652,16 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void decoder_bwd_coop_kernel(
     int N, const float* __restrict__ gy, const float* __restrict__ a1d, const float* __restrict__ Wd2,
     const float* __restrict__ Wd1T, float* __restrict__ gz1d, float* __restrict__ gx,
     const float* __restrict__ ln_a2, const pdg_ln_stat* __restrict__ ln_st, double* __restrict__ part,
-    const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate) {
+    const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate, double* __restrict__ npart) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img = sm;
   float* t_o = reinterpret_cast<float*>(sm + EBW_IMG);
+  // npart != NULL: node_decoder.2's weight gradient from the staged rows (wgrad_narrow_kernel<3>'s products
+  // per row, wide = a1d, narrow = gy)
+  constexpr int NK = 3, NT = 4 * NK + 4 + NK;
+  double nt[NT];
+#pragma unroll
+  for (int p = 0; p < NT; ++p) nt[p] = 0;
   LNStat stln;
   if (COLS) stln = *reinterpret_cast<const LNStat*>(ln_st);
   const int l = lane_id(), w = wave_id();
@@ -1643,6 +1704,16 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void decoder_bwd_coop_kernel(
       if (ok) stnt4(gz1d + (size_t)(base + r) * L + 4 * cg, z);
       img_store4(img, r, cg, z);
       av[u] = COLS ? pa2[u] : zero;
+      if (npart && ok) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+#pragma unroll
+          for (int i = 0; i < NK; ++i) nt[c * NK + i] += (double)(pa1[u][c] * pg[u][i]);
+          nt[4 * NK + c] += (double)pa1[u][c];
+        }
+#pragma unroll
+        for (int i = 0; i < NK; ++i) nt[4 * NK + 4 + i] += (double)pg[u][i];
+      }
     }
     __syncthreads();   // image complete
     if (base + X6_ROWS < r1) issue(base + X6_ROWS);
@@ -1695,6 +1766,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void decoder_bwd_coop_kernel(
     __syncthreads();
     lnb_emit(row, ln_g, part, accumulate, pairs, row + 2 * L);
   }
+  if (npart) narrow_emit<NK>(nt, reinterpret_cast<double*>(sm), npart);
 }
 
 // ============================================================================ C ABI
@@ -2073,42 +2145,51 @@ extern "C" int pdg_node_bwd_coop(int n_nodes, const float* gy, const float* a2n,
   return PDG_OK;
 }
 
+// LDS of a narrow weight gradient's block reduction (narrow_emit): 16 row groups x tot doubles
+static constexpr size_t narrow_lds(int K) { return (size_t)(EBW_THREADS / 32) * (L * K + L + K) * sizeof(double); }
+
 extern "C" int pdg_mlp2_bwd_coop(int rows, const float* gy, const float* a2, const float* a1, const pdg_ln_stat* st,
                                  const pdg_ln_bwd* lb, const float* ln_g, const float* W2T, float* gz2, float* gz1,
-                                 const double* lb_pairs, int lb_npairs, int nblocks, void* stream) {
+                                 const double* lb_pairs, int lb_npairs, const float* x_narrow, double* narrow_partials,
+                                 int nblocks, void* stream) {
   PDG_CHECK_ARG(rows > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_mlp2_bwd_coop: bad sizes");
-  PDG_CHECK_ARG(gy && a2 && a1 && st && (lb || lb_pairs) && ln_g && W2T && gz2 && gz1,
+  PDG_CHECK_ARG(gy && a2 && a1 && st && (lb || lb_pairs) && ln_g && W2T && gz2 && (gz1 || x_narrow),
                 "pdg_mlp2_bwd_coop: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2) && PDG_ALIGNED(a1) && PDG_ALIGNED(W2T) && PDG_ALIGNED(gz2) &&
-                    PDG_ALIGNED(gz1) && PDG_ALIGNED(ln_g),
+                    (!gz1 || PDG_ALIGNED(gz1)) && PDG_ALIGNED(ln_g),
                 "pdg_mlp2_bwd_coop: misaligned pointer");
-  const size_t shm = EBW_IMG + EBW_MASK + (size_t)EFC_TILE * sizeof(float);
+  PDG_CHECK_ARG(!x_narrow == !narrow_partials, "pdg_mlp2_bwd_coop: x_narrow and narrow_partials go together");
+  size_t shm = EBW_IMG + EBW_MASK + (size_t)EFC_TILE * sizeof(float);
+  if (x_narrow && narrow_lds(6) > shm) shm = narrow_lds(6);
   hipLaunchKernelGGL(mlp2_bwd_coop_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, rows, gy, a2,
-                     a1, st, lb, lb_pairs, lb_npairs, ln_g, W2T, gz2, gz1);
+                     a1, st, lb, lb_pairs, lb_npairs, ln_g, W2T, gz2, gz1, x_narrow, narrow_partials);
   PDG_CHECK_LAUNCH("pdg_mlp2_bwd_coop");
   return PDG_OK;
 }
 
 extern "C" int pdg_decoder_bwd_coop(int rows, const float* gy, const float* a1d, const float* Wd2, const float* Wd1T,
                                     float* gz1d, float* gx, const float* ln_a2, const pdg_ln_stat* ln_st,
-                                    double* partials, const float* ln_g, double* pairs, int accumulate, int nblocks,
-                                    void* stream) {
+                                    double* partials, const float* ln_g, double* pairs, int accumulate,
+                                    double* narrow_partials, int nblocks, void* stream) {
   PDG_CHECK_ARG(rows > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_decoder_bwd_coop: bad sizes");
   PDG_CHECK_ARG(gy && a1d && Wd2 && Wd1T && gz1d && gx, "pdg_decoder_bwd_coop: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(a1d) && PDG_ALIGNED(Wd2) && PDG_ALIGNED(Wd1T) && PDG_ALIGNED(gz1d) && PDG_ALIGNED(gx),
                 "pdg_decoder_bwd_coop: misaligned pointer");
   const size_t tile = (size_t)EFC_TILE * sizeof(float);
   const size_t cols = ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
+  size_t shm = EBW_IMG + tile;
+  if (partials && cols > shm) shm = cols;
+  if (narrow_partials && narrow_lds(3) > shm) shm = narrow_lds(3);
   if (partials) {
     PDG_CHECK_ARG(ln_a2 && ln_st && PDG_ALIGNED(ln_a2) && (!pairs || ln_g),
                   "pdg_decoder_bwd_coop: column partials need an aligned ln_a2, ln_st (and ln_g for pairs)");
-    const size_t shm = EBW_IMG + tile > cols ? EBW_IMG + tile : cols;
     hipLaunchKernelGGL(decoder_bwd_coop_kernel<true>, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream,
-                       rows, gy, a1d, Wd2, Wd1T, gz1d, gx, ln_a2, ln_st, partials, ln_g, pairs, accumulate);
+                       rows, gy, a1d, Wd2, Wd1T, gz1d, gx, ln_a2, ln_st, partials, ln_g, pairs, accumulate,
+                       narrow_partials);
   } else {
-    hipLaunchKernelGGL(decoder_bwd_coop_kernel<false>, dim3(nblocks), dim3(EBW_THREADS), EBW_IMG + tile,
-                       (hipStream_t)stream, rows, gy, a1d, Wd2, Wd1T, gz1d, gx, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, 0);
+    hipLaunchKernelGGL(decoder_bwd_coop_kernel<false>, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream,
+                       rows, gy, a1d, Wd2, Wd1T, gz1d, gx, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                       narrow_partials);
   }
   PDG_CHECK_LAUNCH("pdg_decoder_bwd_coop");
   return PDG_OK;

@@ -321,6 +321,19 @@ extern "C" int pdg_wgrad_narrow(int rows, const float* wide, const float* narrow
   return PDG_OK;
 }
 
+// The finalize of pdg_wgrad_narrow alone, for block partials formed inside another kernel
+// (pdg_mlp2_bwd_coop / pdg_decoder_bwd_coop with narrow_partials).
+extern "C" int pdg_wgrad_narrow_finalize(const double* partials, int nparts, int k_narrow, int transpose,
+                                         float* grad_W, float* grad_b_wide, float* grad_b_narrow, void* stream) {
+  PDG_CHECK_ARG(nparts > 0 && nparts <= MAX_BLOCKS && partials && grad_W, "pdg_wgrad_narrow_finalize: bad arguments");
+  PDG_CHECK_ARG(k_narrow == 1 || k_narrow == 3 || k_narrow == 6, "pdg_wgrad_narrow_finalize: k_narrow must be 1, 3 or 6");
+  const int tot = L * k_narrow + L + k_narrow;
+  hipLaunchKernelGGL(wgrad_narrow_finalize_kernel, dim3(tot), dim3(256), 0, (hipStream_t)stream, partials, nparts,
+                     k_narrow, transpose, grad_W, grad_b_wide, grad_b_narrow);
+  PDG_CHECK_LAUNCH("pdg_wgrad_narrow_finalize");
+  return PDG_OK;
+}
+
 // ============================================================================ segmented, LDS-staged wgrad
 // One launch per weight and backward: the row segments of every message-passing
 // step (and both edge_net evaluations) form one virtual K = sum(rows) reduction.

@@ -146,8 +146,11 @@ def kernel_variants(overrides: dict | None = None) -> dict:
 class _StatBuf:
     """A device array of pdg_ln_stat (or pdg_ln_bwd) structs."""
 
-    def __init__(self, n: int, nbytes: int, device) -> None:
-        self.buf = torch.zeros(max(n, 1) * nbytes, dtype=torch.uint8, device=device)
+    def __init__(self, n: int, nbytes: int, device, zero: bool = True) -> None:
+        # zero=False: every entry is written (pdg_ln_finalize / the producers' fused finalize) before
+        # it is read, so no fill launch
+        alloc = torch.zeros if zero else torch.empty
+        self.buf = alloc(max(n, 1) * nbytes, dtype=torch.uint8, device=device)
         self.nbytes = nbytes
 
     def __getitem__(self, i: int) -> int:
@@ -269,7 +272,8 @@ class EPDEngine:
             raise ValueError("exact (sync) data parallelism needs edges on every rank's shard")
         np_ = ctypes.byref(self._nparts)
         ctx = FwdCtx(plan=plan, steps=steps, scale_output=scale_output)
-        ctx.stats = _StatBuf(2 + 3 * steps, LN_STAT_BYTES, self.device)
+        # without edges the edge LayerNorms' entries are never finalized (zeros keep them finite)
+        ctx.stats = _StatBuf(2 + 3 * steps, LN_STAT_BYTES, self.device, zero=E == 0)
         st = ctx.stats
         x_in = self._empty(N, 6)
         e_in = self._empty(E)
@@ -515,15 +519,18 @@ class EPDEngine:
         gz1d, gx = self._empty(N, L), self._empty(N, L)
         dl = ctx.per_step[S - 1]
         if self.nbwd_coop:   # + the column sums of the last node LayerNorm (upstream gradient: gx)
+            # + node_decoder.2's weight / bias gradient from the same a1d / gy rows (block partials)
             self._t("decoder_bwd", lib.pdg_decoder_bwd_coop, N, _p(gy), _p(ctx.a1d), _p(P["node_decoder.2.weight"]),
                     _p(T["Wd1T"]), _p(gz1d), _p(gx), _p(dl["a2n"]), st[dl["i_n"]], _p(ACC_N), _p(g_node),
-                    _p(PN(S - 1)), 1, self._nslabs_e, s)
+                    _p(PN(S - 1)), 1, _p(self._part_narrow), self._nslabs_e, s)
             self._nparts.value = self._nslabs_e
+            lib.pdg_wgrad_narrow_finalize(_p(self._part_narrow), self._nslabs_e, 3, 1, _p(G["node_decoder.2.weight"]),
+                                          None, _p(G["node_decoder.2.bias"]), s)
         else:
             lib.pdg_decoder_bwd(N, _p(gy), _p(ctx.a1d), _p(P["node_decoder.2.weight"]), _p(T["Wd1T"]), _p(gz1d),
                                 _p(gx), s)
-        lib.pdg_wgrad_narrow(N, _p(ctx.a1d), _p(gy), 3, 1, _p(self._part_narrow), _p(G["node_decoder.2.weight"]),
-                             None, _p(G["node_decoder.2.bias"]), s)
+            lib.pdg_wgrad_narrow(N, _p(ctx.a1d), _p(gy), 3, 1, _p(self._part_narrow), _p(G["node_decoder.2.weight"]),
+                                 None, _p(G["node_decoder.2.bias"]), s)
         segs["d1"].append((gz1d, ctx.x_S, N))
 
         ge_next = None              # d loss / d e_S: the last edge update has no consumer
@@ -638,17 +645,22 @@ class EPDEngine:
             gx_next, gx_t = gx_t, gx_next
             ge_next = ge_out
         # encoders
-        gz2, gz1 = self._empty(N, L), self._empty(N, L)
+        gz2 = self._empty(N, L)
+        gz1 = None if self.nbwd_coop else self._empty(N, L)
         pn, nn = src(P_NENC, n_node)
-        if self.nbwd_coop:   # the node encoder's backward, bf16x6 (pdg_mlp2_bwd_coop)
+        if self.nbwd_coop:   # the node encoder's backward, bf16x6 (pdg_mlp2_bwd_coop), + its first layer's
+            # weight / bias gradient from gz1 and the encoder input (block partials; gz1 is not stored)
             self._t("node_enc_bwd", lib.pdg_mlp2_bwd_coop, N, _p(gx_next), _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], None,
-                    _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), pn, nn, self._nslabs_e, s)
+                    _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), None, pn, nn, _p(ctx.x_in),
+                    _p(self._part_narrow), self._nslabs_e, s)
+            lib.pdg_wgrad_narrow_finalize(_p(self._part_narrow), self._nslabs_e, 6, 0, _p(G["node_encoder.0.weight"]),
+                                          _p(G["node_encoder.0.bias"]), None, s)
         else:
             lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], None,
                              _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), pn, nn, s)
+            lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow),
+                                 _p(G["node_encoder.0.weight"]), _p(G["node_encoder.0.bias"]), None, s)
         segs["ne2"].append((gz2, ctx.a1_ne, N))
-        lib.pdg_wgrad_narrow(N, _p(gz1), _p(ctx.x_in), 6, 0, _p(self._part_narrow), _p(G["node_encoder.0.weight"]),
-                             _p(G["node_encoder.0.bias"]), None, s)
         if E:
             pp, n_e = edge_ln_pairs(P_EENC, ge_next, ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"])
             pe, ne = src(pp, n_e if not fused else n_edge)

@@ -80,8 +80,9 @@ SIGNATURES: dict[str, list] = {
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_node_bwd_coop": [I] + [P] * 14 + [I, I, P],
-    "pdg_mlp2_bwd_coop": [I] + [P] * 10 + [I, I, P],
-    "pdg_decoder_bwd_coop": [I] + [P] * 11 + [I, I, P],
+    "pdg_mlp2_bwd_coop": [I] + [P] * 10 + [I, P, P, I, P],
+    "pdg_decoder_bwd_coop": [I] + [P] * 11 + [I, P, I, P],
+    "pdg_wgrad_narrow_finalize": [P, I, I, I, P, P, P, P],
     "pdg_segsum_finish": [I, P, P, P, P, P, P, P, P],
     "pdg_wgrad_slabs_per_cu": [],
     "pdg_wgrad_pairs": [I, P, P, P, P, I, P, P, I, P],

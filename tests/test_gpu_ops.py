@@ -1032,10 +1032,25 @@ def test_mlp2_bwd_coop_vs_mlp2_bwd(env, N, nb):
     assert lib.pdg_mlp2_bwd(N, gy.data_ptr(), None, a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None, g.data_ptr(),
                             W2T.data_ptr(), o0[0].data_ptr(), o0[1].data_ptr(), pairs.data_ptr(), 2, s) == 0
     assert lib.pdg_mlp2_bwd_coop(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None, g.data_ptr(),
-                                 W2T.data_ptr(), o1[0].data_ptr(), o1[1].data_ptr(), pairs.data_ptr(), 2, nb, s) == 0
+                                 W2T.data_ptr(), o1[0].data_ptr(), o1[1].data_ptr(), pairs.data_ptr(), 2, None, None,
+                                 nb, s) == 0
     assert torch.equal(o0[0], o1[0])                       # gz2
     z1 = torch.where(a1 > 0, o0[0].double() @ W2T.double().T, torch.zeros(N, L, dtype=torch.float64, device="cuda"))
     assert rel(o1[1], z1) < TOL and rel(o0[1], z1) < TOL
+    # + the encoder's first-layer gradient (wide = gz1, narrow = the 6-wide input), gz1 not stored: the same
+    # gz2, and the finalized dW0 (128 x 6) / db0 against fp64 sums over the kernel's own gz1
+    xn = rnd(N, 6)
+    npart = torch.full((nb * (6 * L + L + 6),), float("nan"), dtype=torch.float64, device="cuda")
+    gz2b = torch.full((N, L), float("nan"), device="cuda")
+    assert lib.pdg_mlp2_bwd_coop(N, gy.data_ptr(), a2.data_ptr(), a1.data_ptr(), st.data_ptr(), None, g.data_ptr(),
+                                 W2T.data_ptr(), gz2b.data_ptr(), None, pairs.data_ptr(), 2, xn.data_ptr(),
+                                 npart.data_ptr(), nb, s) == 0
+    assert torch.equal(o0[0], gz2b)
+    gW, gb = torch.full((L, 6), 0.5, device="cuda"), torch.full((L,), -0.25, device="cuda")   # += semantics
+    assert lib.pdg_wgrad_narrow_finalize(npart.data_ptr(), nb, 6, 0, gW.data_ptr(), gb.data_ptr(), None, s) == 0
+    z1k = o1[1].double()
+    assert rel(gW.double() - 0.5, z1k.T @ xn.double()) < 1e-6
+    assert rel(gb.double() + 0.25, z1k.sum(0)) < 1e-6
 
 
 @pytest.mark.parametrize("N,nb", [(1, 1), (7, 37), (1031, 37), (40328, 256)])
@@ -1061,6 +1076,7 @@ def test_decoder_bwd_coop_vs_decoder_bwd(env, N, nb):
     assert lib.pdg_decoder_bwd(N, gy.data_ptr(), a1.data_ptr(), Wd2.data_ptr(), W1T.data_ptr(), z0.data_ptr(),
                                x0.data_ptr(), s) == 0
     ref = z0.double() @ W1T.double().T
+    npart = torch.full((nb * (3 * L + L + 3),), float("nan"), dtype=torch.float64, device="cuda")
     for cols in (False, True):
         z1, x1 = (torch.full((N, L), float("nan"), device="cuda") for _ in range(2))
         part = torch.zeros(nb * 256, dtype=torch.float64, device="cuda")
@@ -1068,10 +1084,16 @@ def test_decoder_bwd_coop_vs_decoder_bwd(env, N, nb):
         assert lib.pdg_decoder_bwd_coop(N, gy.data_ptr(), a1.data_ptr(), Wd2.data_ptr(), W1T.data_ptr(),
                                         z1.data_ptr(), x1.data_ptr(), a2.data_ptr() if cols else None,
                                         st.data_ptr() if cols else None, part.data_ptr() if cols else None,
-                                        g.data_ptr() if cols else None, pairs.data_ptr() if cols else None, 0, nb,
-                                        s) == 0
+                                        g.data_ptr() if cols else None, pairs.data_ptr() if cols else None, 0,
+                                        npart.data_ptr() if cols else None, nb, s) == 0
         assert torch.equal(z0, z1)
         assert rel(x1, ref) < TOL and rel(x0, ref) < TOL
+        if cols:   # node_decoder.2's weight / bias gradient (wide = a1d, narrow = gy, stored transposed 3 x 128)
+            gW, gb = torch.full((3, L), 0.5, device="cuda"), torch.full((3,), -0.25, device="cuda")
+            assert lib.pdg_wgrad_narrow_finalize(npart.data_ptr(), nb, 3, 1, gW.data_ptr(), None, gb.data_ptr(),
+                                                 s) == 0
+            assert rel(gW.double() - 0.5, gy.double().T @ a1.double()) < 1e-6
+            assert rel(gb.double() + 0.25, gy.double().sum(0)) < 1e-6
         if cols:
             got = part.view(nb, 256).sum(0).cpu()
             gyv = x1.double().cpu()
