@@ -59,12 +59,9 @@ PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd
              "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_x6_kernel", "node_net_pair_kernel", "node_net_kernel"),
              "pq_scatter_bwd": "pq_scatter_bwd_kernel",
              "wgrad_W2": "wgrad_x6_kernel",
-             # the edge-update instantiations (template <EU, RC> / <RES, C2>: the recompute_a1 / gout_gz1
-             # variants are the <true, true> ones)
-             "edge_bwd_w2": ("void edge_bwd_w2_kernel<true, false>", "void edge_bwd_w2_kernel<true, true>",
-                             "void edge_bwd_w2_kernel<true>"),
-             "edge_gout": ("void edge_gout_wc_kernel<true, false>", "void edge_gout_wc_kernel<true, true>",
-                           "void edge_gout_wc_kernel<true>"),
+             # the edge-update instantiations
+             "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
+             "edge_gout": "void edge_gout_wc_kernel<true>",
              "node_bwd": "node_bwd_coop_kernel", "node_pq": "void node_pq_x6_kernel<true>",
              "gemm_sum2": "void gemm_sum2_coop_kernel<true>", "wgrad_pairs": "void wgrad_x6_pair2_kernel"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
@@ -236,8 +233,7 @@ def cpu_baseline(cfg, samples, full_graphs: int, reps: int = 5, one_thread: bool
 
 
 # ---------------------------------------------------------------------------------- roofline
-def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, seg: bool = False,
-                rc: bool = False) -> dict:
+def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, seg: bool = False) -> dict:
     """Algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops with the peak of their
     instruction type, and the bytes the kernel must read/write (inputs once, outputs once, int32
     indices).  An fp32-accurate 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA,
@@ -245,19 +241,16 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
     g = 2 * L * L
     return {
         # W_c product (fp32 MFMA) + 2 W2 products (bf16x6) per edge; reads a2e_prev, e_prev, 4 gathered
-        # P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e (rc: C instead of both);
+        # P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e;
         # seg: also the N message sums rows, and a2m only when training
         "edge_fwd": ([(E * g, PEAK_FP32_MFMA), (E * 2 * g * X6, PEAK_BF16_MFMA)],
-                     E * ((9 if infer else (10 if rc else 11)) * 4 * L + 8) - (E * 4 * L if (seg and infer) else 0)
+                     E * ((9 if infer else 11) * 4 * L + 8) - (E * 4 * L if (seg and infer) else 0)
                      + (8 * L * N if seg else 0)),
         # fused (pdg_edge_bwd_w2): 2 W2^T products + 2 weight-gradient products per edge (bf16x6);
         # reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gz1e, gC; one slab
         # read+write per block.  unfused (pdg_edge_bwd): W2^T x2 (bf16x6) + Wc^T (fp32); writes
         # gz2m, gz1m, gz2e, gz1e, gC, ge_out
-        # rc (pdg_edge_bwd_w2_rc): reads C instead of a1m, a1e, gathers the 4 P/Q rows (counted as reads)
-        # and src
-        "edge_bwd": (([(E * 4 * g * X6, PEAK_BF16_MFMA)],
-                      E * ((12 if rc else 9) * 4 * L + (8 if rc else 4)) + 2 * nslab_bytes) if fused
+        "edge_bwd": (([(E * 4 * g * X6, PEAK_BF16_MFMA)], E * (9 * 4 * L + 4) + 2 * nslab_bytes) if fused
                      else ([(E * 2 * g * X6, PEAK_BF16_MFMA), (E * g, PEAK_FP32_MFMA)], E * (12 * 4 * L + 4))),
         # fused Wc path (pdg_edge_gout_wc): Wc^T product + weight-gradient product (bf16x6); reads gC,
         # e, ge_next and the LayerNorm input of e (column sums), writes ge_out; one slab read+write
@@ -503,8 +496,7 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
     # the fused message sums run in inference only unless PDG_SEG_SUMS_TRAIN=1 (engine.py:253)
     seg = getattr(eng, "seg_sums", False) if infer else getattr(eng, "seg_sums_train", False)
-    rc = (not infer and E > 0 and eng.recompute_a1 and fused and eng.coop_fwd and not eng.seg_sums_train)
-    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg, rc)
+    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg)
     pmc_path, pmc_reason = pmc_file() if with_pmc else (None, "not collected for this config")
     pmc = load_pmc(fused, pmc_path)
     sq_path, sq_reason = sq_file() if with_pmc else (None, "not collected for this config")

@@ -155,6 +155,14 @@ int pdg_decoder_fwd(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, co
                     const float* ln_b, const float* x_res, float* x_out, const float* Wd1,
                     const float* bd1, float* a1d, const float* Wd2, const float* bd2,
                     const float* stats8, int scale_output, float* y, void* stream);
+/* pdg_decoder_fwd with the last node LayerNorm's statistics folded in: every block reduces the
+ * (sum, sumsq) partials of pdg_node_net in pdg_ln_finalize's order (bit-identical) and block 0
+ * stores them to st_out for the backward, replacing a separate pdg_ln_finalize launch (as
+ * pdg_node_pq_rw_fin does for the earlier steps). */
+int pdg_decoder_fwd_fin(int n_nodes, const float* a2_prev, const double* partials, int nparts, double count,
+                        pdg_ln_stat* st_out, const float* ln_g, const float* ln_b, const float* x_res,
+                        float* x_out, const float* Wd1, const float* bd1, float* a1d, const float* Wd2,
+                        const float* bd2, const float* stats8, int scale_output, float* y, void* stream);
 
 /* torch.any(x != 0) into *flag (int, device). models.py:294 */
 int pdg_any_nonzero(const float* x, int64_t n, int* flag, void* stream);
@@ -288,15 +296,6 @@ int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, 
                       const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                       const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                       double* part_e, int with_edge_update, int nblocks, void* stream);
-/* pdg_edge_fwd_coop for training with a backward that recomputes the first layers
- * (pdg_edge_bwd_w2_rc): instead of a1m and a1e it stores c_out = Wc e + b1 (E x 128, b1 added), from
- * which a1m = relu((c_out + P[dst]) + Q[src]) and a1e = relu((c_out + P[src]) + Q[dst]) follow bit for
- * bit (models.py:219-222, :233-238 with W1 = [Wa | Wb | Wc]); one E-row array written instead of two. */
-int pdg_edge_fwd_coop_c(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                        const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
-                        const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
-                        const float* b2, float* c_out, float* a2m, float* a2e, double* part_m, double* part_e,
-                        int with_edge_update, int nblocks, void* stream);
 /* pdg_edge_fwd_coop that also forms the aggregation's message sums (models.py:215-217) from its
  * a2m tiles, replacing pdg_segment_sum's re-read of a2m: sums[v] (fp64, N x 128) = sum of a2m over
  * v's incoming edges, raw (the message LayerNorm's statistics come out of this launch); rows of
@@ -329,8 +328,7 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
  *   pdg_edge_bwd_w2:  gz1m/gz1e/gC as pdg_edge_bwd; slabs (zeroed before the first call)
  *                     += gz2m^T a1m + gz2e^T a1e and the b2 column sums; gz2m/gz2e are not
  *                     materialised.  ge_next == NULL: message branch only, gC = gz1m (gC may
- *                     then be the gz1m pointer itself: written once).  gC may be NULL (not
- *                     written; pdg_edge_gout_wc2 forms it).
+ *                     then be the gz1m pointer itself: written once).
  *   pdg_edge_gout_wc: ge_out = [ge_next +] WcT gC; slabs += gC^T e and the b1 column sums.
  *                     a2ln != NULL: also the column sums of the backward of the LayerNorm that
  *                     produced e (input a2ln, statistics st_ln, upstream gradient ge_out), as
@@ -342,16 +340,6 @@ int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float
                     const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
                     float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
                     const double* pairs_e, int npairs_e, void* stream);
-/* pdg_edge_bwd_w2 reading, instead of a1m / a1e, the C rows of pdg_edge_fwd_coop_c and the step's P / Q
- * (N x 128, the pdg_node_pq_rw outputs the forward gathered), recomputing a1m / a1e bit for bit: the
- * same outputs as pdg_edge_bwd_w2 on the stored a1 arrays, with one E-row array read instead of two
- * (the four P / Q rows per edge are gathered, mostly from the caches). */
-int pdg_edge_bwd_w2_rc(int n_edges, const int* dst, const int* src, const float* gaggr, const float* ge_next,
-                       const float* a2m, const float* C, const float* P, const float* Q, const float* a2e,
-                       const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
-                       const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m, float* gz1e,
-                       float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
-                       const double* pairs_e, int npairs_e, void* stream);
 /* Edge encoder backward (models.py:268-274), fused: gz2 = LN_bwd(gy) [a2 > 0], slabs (zeroed
  * before, pdg_wgrad_reduce layout) += gz2^T a1 and the b2 sums, gz1 = (W2T gz2) [a1 > 0], and per
  * block narrow_sums[b] = (sum gz1 e_in, sum gz1) as 2 x 128 doubles; a1 = relu(w0 e_in + b0) is
@@ -367,13 +355,6 @@ int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* 
                      const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
                      const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,
                      int accumulate, void* stream);
-/* pdg_edge_gout_wc with gC = gz1m + gz1e formed on load (the fp32 add pdg_edge_bwd_w2 would store as
- * gC; gz1e == NULL: gC = gz1m), so pdg_edge_bwd_w2 runs with gC == NULL and writes one E-row stream
- * fewer.  Same outputs bit for bit. */
-int pdg_edge_gout_wc2(int n_edges, const float* gz1m, const float* gz1e, const float* e,
-                      const float* ge_next, const float* WcT, float* ge_out, float* slabs, int nslabs,
-                      const float* a2ln, const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g,
-                      double* pairs, int accumulate, void* stream);
 
 /* Mesh graph on the device (pdg_graph.hip): FaceToEdge of a triangle
  * mesh (convert_utils.py:47-60), edge lengths (datasets.py:182-188) and, when `periodic`,

@@ -243,14 +243,9 @@ __device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const 
 // made the compiler's loop-carried count collapse to vmcnt(0) in the stage, a wait for both sets.
 // gz1m / gz1e / gC are bitwise those of the 32-row kernel; dW2 sums the same products in another
 // order (message and edge-update rows of a round interleave per 16 rows instead of per 32).
-//
-// RC (pdg_edge_bwd_w2_rc): a1m / a1e are not read but recomputed from the edge forward's C = Wc e + b1
-// rows and the step's P / Q gathered at dst / src, a1m = relu((C + P[dst]) + Q[src]) and a1e =
-// relu((C + P[src]) + Q[dst]) with the forward's operations, bit for bit (pdg_edge_fwd_coop_c stores C
-// instead of the two a1 arrays).  C rides in the two-deep row sets; the four gathered rows of round
-// n + 1 are issued at round n's stage, ahead of round n + 2's rows (vmcnt counts in issue order), from
-// indices loaded one round earlier.
-template <bool EU, bool RC>
+// (A form recomputing a1m / a1e from the forward's C = Wc e + b1 and the step's gathered P / Q rows,
+// one E-row array read and written fewer, measured slower and was removed: DESIGN §4 round 3.)
+template <bool EU>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
     const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
@@ -258,8 +253,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     const pdg_ln_bwd* __restrict__ lbm_p, const pdg_ln_bwd* __restrict__ lbe_p, const float* __restrict__ lg,
     const float* __restrict__ W2T, float* __restrict__ gz1m, float* __restrict__ gz1e, float* __restrict__ gC,
     float* __restrict__ slabs, int E, const double* __restrict__ pm, int npm, const double* __restrict__ pe,
-    int npe, const int* __restrict__ src, const float* __restrict__ Cr, const float* __restrict__ Pn,
-    const float* __restrict__ Qn) {
+    int npe) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   constexpr int NIMG = EU ? 4 : 2, NMSK = EU ? 2 : 1;
   constexpr int BUF = NIMG * IMG16 + NMSK * MSK16;           // one round's images + masks
@@ -278,35 +272,19 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
   f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  // two register sets of prefetched rows (round parity), and the dst id each set gathers next;
-  // RC: pa1 holds the C row, pa1e is unused, and the P / Q rows of the next round to stage are
-  // gathered into gq[] from the ids in nd / ns
+  // two register sets of prefetched rows (round parity), and the dst id each set gathers next
   f32x4 pg[2], pa2[2], pa1[2], pge[2], pa2e[2], pa1e[2];
-  f32x4 gq[4];   // RC: P[dst], Q[src], P[src], Q[dst]
-  int dn[2], nd = 0, ns = 0;
+  int dn[2];
   auto issue = [&](int s, int base) {
     const size_t rc = (size_t)clamp_row(base + rg, r1) * L + 4 * cg;
     pg[s] = *reinterpret_cast<const f32x4*>(gaggr + (size_t)dn[s] * L + 4 * cg);
     pa2[s] = *reinterpret_cast<const f32x4*>(a2m + rc);
-    pa1[s] = *reinterpret_cast<const f32x4*>((RC ? Cr : a1m) + rc);
+    pa1[s] = *reinterpret_cast<const f32x4*>(a1m + rc);
     if (EU) {
       pge[s] = *reinterpret_cast<const f32x4*>(ge_next + rc);
       pa2e[s] = *reinterpret_cast<const f32x4*>(a2e + rc);
-      if (!RC) pa1e[s] = *reinterpret_cast<const f32x4*>(a1e + rc);
+      pa1e[s] = *reinterpret_cast<const f32x4*>(a1e + rc);
     }
-  };
-  auto gather = [&]() {   // RC: the P / Q rows of the row whose ids are nd / ns
-    gq[0] = *reinterpret_cast<const f32x4*>(Pn + (size_t)nd * L + 4 * cg);
-    gq[1] = *reinterpret_cast<const f32x4*>(Qn + (size_t)ns * L + 4 * cg);
-    if (EU) {
-      gq[2] = *reinterpret_cast<const f32x4*>(Pn + (size_t)ns * L + 4 * cg);
-      gq[3] = *reinterpret_cast<const f32x4*>(Qn + (size_t)nd * L + 4 * cg);
-    }
-  };
-  auto ids = [&](int base) {   // RC: dst / src of the thread's row of the round at `base`
-    const int rr = clamp_row(base + rg, r1);
-    nd = dst[rr];
-    ns = src[rr];
   };
   // no memory operation below is conditional (rows past the block's end are clamped on load and
   // dropped by the buffer range check on store), so the compiler can count the loads in flight: a
@@ -318,12 +296,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   const __amdgpu_buffer_rsrc_t out_e = rows_rsrc(EU ? gz1e : gz1m, r0, r1);
   dn[0] = dst[clamp_row(first + rg, r1)];   // E > 0: an empty block (first = r1 = E) reads row E - 1
   dn[1] = dst[clamp_row(first + R16 + rg, r1)];
-  if (RC) {   // round 0's gathered rows first, then round 1's ids
-    ids(first);
-    gather();
-    ids(first + R16);
-    __builtin_amdgcn_sched_barrier(0);
-  }
   // each set's loads strictly before the next set's (sched_barrier), in the order the loop re-issues
   // them: the loop waits for one set by count, and an interleaved prologue lowers that count
   issue(0, first);
@@ -347,16 +319,9 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     {
       const bool ok = base + rg < r1;
       const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 a1mv = pa1[s], a1ev = pa1e[s];
-      if (RC) {   // edge_fwd_coop_kernel's first layers from C (stored with b1 added) and the gathers
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a1mv[j] = fmaxf((pa1[s][j] + gq[0][j]) + gq[1][j], 0.f);
-          if (EU) a1ev[j] = fmaxf((pa1[s][j] + gq[2][j]) + gq[3][j], 0.f);
-        }
-      }
+      const f32x4 a1mv = pa1[s], a1ev = pa1e[s];
       // a row past r1 has gz2 = 0, which zeroes its products whatever its (finite, clamped-row) a1:
-      // no select on a1 (with one, the compiler moved the RC gathers into a branch at their use)
+      // no select on a1
       const f32x4 zm = ok ? ln_relu_bwd4(pg[s], pa2[s], stm, lbm, g4) : zero;
       const f32x4 am = a1mv;
       bsum += zm;
@@ -371,13 +336,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
         img_store4<T16>(img_ae, rg, cg, ae);
         *reinterpret_cast<unsigned*>(msk_e + rg * MSK_STRIDE + 4 * cg) = relu_mask4(ae);
       }
-    }
-    // ---- RC: the next round's gathered rows, then the ids of the round after it (both ahead of the
-    // row loads below, which the next stage must not wait for)
-    if (RC) {   // the next round's rows, then the ids of the round after it (this half of the next unit)
-      gather();
-      ids(base + stride);
-      __builtin_amdgcn_sched_barrier(0);
     }
     // ---- the set is free: its rows of the round after next (the same half of the next unit), then
     // the dst ids of the one after that
@@ -423,11 +381,9 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
 }
 
 // ============================================================================ Wc path
-// C2 (pdg_edge_gout_wc2): gC is formed here as gz1m + gz1e (the two arrays pdg_edge_bwd_w2 writes
-// anyway, the same fp32 add it would store as gC), so the edge backward writes no gC stream.
-template <bool RES, bool C2 = false>
+template <bool RES>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
-    const float* __restrict__ gC, const float* __restrict__ gC2, const float* __restrict__ e,
+    const float* __restrict__ gC, const float* __restrict__ e,
     const float* __restrict__ ge_next,
     const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs,
     const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, double* __restrict__ part, int E,
@@ -454,13 +410,12 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
   // LayerNorm column sums of this thread's columns 4cg .. 4cg+3 (ln_colsum_kernel, pdg_bwd.hip)
   double cs_g[4] = {0, 0, 0, 0}, cs_x[4] = {0, 0, 0, 0};
   // prefetched rows of the next round, all whole-row (a second slot measured no faster)
-  f32x4 pc[2], pc2[2], pe[2], pres[2], pa2[2];
+  f32x4 pc[2], pe[2], pres[2], pa2[2];
   auto issue = [&](int base) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
       pc[u] = *reinterpret_cast<const f32x4*>(gC + rc);
-      if (C2) pc2[u] = *reinterpret_cast<const f32x4*>(gC2 + rc);
       pe[u] = *reinterpret_cast<const f32x4*>(e + rc);
       if (RES) pres[u] = *reinterpret_cast<const f32x4*>(ge_next + rc);
       if (ln) pa2[u] = *reinterpret_cast<const f32x4*>(a2ln + rc);   // LayerNorm input of e
@@ -475,7 +430,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
       const int r = rg + 16 * u;
       const bool ok = base + r < r1;
       const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 c = ok ? (C2 ? pc[u] + pc2[u] : pc[u]) : zero;
+      const f32x4 c = ok ? pc[u] : zero;
       bsum += c;
       img_store4(img_c, r, cg, c);
       img_store4(img_e, r, cg, ok ? pe[u] : zero);
@@ -747,7 +702,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     const float* __restrict__ Q, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ a1m, float* __restrict__ a2m,
     float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m, double* __restrict__ part_e,
-    double* __restrict__ sums, double* __restrict__ seg_part, int* __restrict__ seg_info, int store_c) {
+    double* __restrict__ sums, double* __restrict__ seg_part, int* __restrict__ seg_info) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img_m = sm;                                   // a1m
   unsigned char* img_x = sm + EBW_IMG;                         // a1e (EU)
@@ -946,17 +901,15 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
       const int r = 16 * nb + (l & 15);
-      f32x4 am, ae, cv;
+      f32x4 am, ae;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float c = d[nb][j] + b1o[j];
-        cv[j] = c;
         am[j] = fmaxf((c + gpd[nb][j]) + gqs[nb][j], 0.f);
         if (EU) ae[j] = fmaxf((c + gps[nb][j]) + gqd[nb][j], 0.f);
       }
       img_store4(img_m, r, 4 * w + (l >> 4), am);
-      // store_c: the a1m output receives C = Wc e + b1 instead (pdg_edge_fwd_coop_c)
-      if (a1m) *reinterpret_cast<f32x4*>(t_m + r * OT_STRIDE + oc) = store_c ? cv : am;
+      if (a1m) *reinterpret_cast<f32x4*>(t_m + r * OT_STRIDE + oc) = am;
       if (EU) {
         img_store4(img_x, r, 4 * w + (l >> 4), ae);
         if (a1e) *reinterpret_cast<f32x4*>(t_x + r * OT_STRIDE + oc) = ae;
@@ -1770,77 +1723,44 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void decoder_bwd_coop_kernel(
 }
 
 // ============================================================================ C ABI
-static int edge_bwd_w2_launch(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
-                              const float* a2m, const float* a1m, const float* a2e, const float* a1e,
-                              const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
-                              const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
-                              float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
-                              const double* pairs_e, int npairs_e, const int* src, const float* C, const float* P,
-                              const float* Q, void* stream) {
-  const bool rc = C != nullptr;
-  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_w2: n_edges must be > 0");
-  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_bwd_w2: bad slabs");
-  PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_bwd_w2: the XCD-interleaved build needs 256 blocks");
-  // gC may be NULL: not written (pdg_edge_gout_wc2 forms it from gz1m + gz1e)
-  PDG_CHECK_ARG(dst && gaggr && a2m && (rc || a1m) && st_m && (lb_m || pairs_m) && ln_g && W2T && gz1m,
-                "pdg_edge_bwd_w2: null argument");
-  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && (rc || PDG_ALIGNED(a1m)) && PDG_ALIGNED(ln_g) &&
-                    PDG_ALIGNED(W2T) && PDG_ALIGNED(gz1m) && PDG_ALIGNED(gC) && PDG_ALIGNED(slabs),
-                "pdg_edge_bwd_w2: misaligned pointer");
-  PDG_CHECK_ARG(!rc || (src && P && Q && PDG_ALIGNED(C) && PDG_ALIGNED(P) && PDG_ALIGNED(Q)),
-                "pdg_edge_bwd_w2_rc: src / C / P / Q missing or misaligned");
-  const bool eu = ge_next != nullptr;
-  PDG_CHECK_ARG(!eu || gC != gz1m, "pdg_edge_bwd_w2: gC may alias gz1m only without the edge update");
-  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && (rc || a1e) && gz1e && st_e && (lb_e || pairs_e) &&
-                        PDG_ALIGNED(a2e) && (rc || PDG_ALIGNED(a1e)) && PDG_ALIGNED(gz1e)),
-                "pdg_edge_bwd_w2: edge-update arguments missing or misaligned");
-  // 16-row rounds, two rounds of loads in flight (edge_bwd_w2_kernel): two buffers of images + masks
-  const size_t shm = eu ? 2 * (4 * IMG16 + 2 * MSK16) : 2 * (2 * IMG16 + MSK16);
-  hipStream_t s = (hipStream_t)stream;
-#define PDG_EBW2(U, R)                                                                                              \
-  hipLaunchKernelGGL((edge_bwd_w2_kernel<U, R>), dim3(nslabs), dim3(EBW_THREADS), shm, s, dst, gaggr, ge_next, a2m, \
-                     a1m, a2e, a1e, st_m, U ? st_e : st_m, lb_m, U ? lb_e : lb_m, ln_g, W2T, gz1m, gz1e, gC, slabs,  \
-                     n_edges, pairs_m, npairs_m, U ? pairs_e : pairs_m, U ? npairs_e : npairs_m, src, C, P, Q)
-  if (eu) {
-    if (rc) PDG_EBW2(true, true); else PDG_EBW2(true, false);
-  } else {
-    if (rc) PDG_EBW2(false, true); else PDG_EBW2(false, false);
-  }
-#undef PDG_EBW2
-  PDG_CHECK_LAUNCH("pdg_edge_bwd_w2");
-  return PDG_OK;
-}
-
 extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                                const float* a2m, const float* a1m, const float* a2e, const float* a1e,
                                const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
                                const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
                                float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
                                const double* pairs_e, int npairs_e, void* stream) {
-  return edge_bwd_w2_launch(n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, gz1m,
-                            gz1e, gC, slabs, nslabs, pairs_m, npairs_m, pairs_e, npairs_e, nullptr, nullptr, nullptr,
-                            nullptr, stream);
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_w2: n_edges must be > 0");
+  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_bwd_w2: bad slabs");
+  PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_bwd_w2: the XCD-interleaved build needs 256 blocks");
+  PDG_CHECK_ARG(dst && gaggr && a2m && a1m && st_m && (lb_m || pairs_m) && ln_g && W2T && gz1m && gC,
+                "pdg_edge_bwd_w2: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(ln_g) &&
+                    PDG_ALIGNED(W2T) && PDG_ALIGNED(gz1m) && PDG_ALIGNED(gC) && PDG_ALIGNED(slabs),
+                "pdg_edge_bwd_w2: misaligned pointer");
+  const bool eu = ge_next != nullptr;
+  PDG_CHECK_ARG(!eu || gC != gz1m, "pdg_edge_bwd_w2: gC may alias gz1m only without the edge update");
+  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && gz1e && st_e && (lb_e || pairs_e) &&
+                        PDG_ALIGNED(a2e) && PDG_ALIGNED(a1e) && PDG_ALIGNED(gz1e)),
+                "pdg_edge_bwd_w2: edge-update arguments missing or misaligned");
+  // 16-row rounds, two rounds of loads in flight (edge_bwd_w2_kernel): two buffers of images + masks
+  const size_t shm = eu ? 2 * (4 * IMG16 + 2 * MSK16) : 2 * (2 * IMG16 + MSK16);
+  hipStream_t s = (hipStream_t)stream;
+  if (eu)
+    hipLaunchKernelGGL(edge_bwd_w2_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, s, dst, gaggr, ge_next, a2m,
+                       a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, gz1m, gz1e, gC, slabs, n_edges, pairs_m,
+                       npairs_m, pairs_e, npairs_e);
+  else
+    hipLaunchKernelGGL(edge_bwd_w2_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, s, dst, gaggr, ge_next, a2m,
+                       a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, gz1m, gz1e, gC, slabs, n_edges, pairs_m,
+                       npairs_m, pairs_m, npairs_m);
+  PDG_CHECK_LAUNCH("pdg_edge_bwd_w2");
+  return PDG_OK;
 }
 
-extern "C" int pdg_edge_bwd_w2_rc(int n_edges, const int* dst, const int* src, const float* gaggr,
-                                  const float* ge_next, const float* a2m, const float* C, const float* P,
-                                  const float* Q, const float* a2e, const pdg_ln_stat* st_m, const pdg_ln_stat* st_e,
-                                  const pdg_ln_bwd* lb_m, const pdg_ln_bwd* lb_e, const float* ln_g,
-                                  const float* W2T, float* gz1m, float* gz1e, float* gC, float* slabs, int nslabs,
-                                  const double* pairs_m, int npairs_m, const double* pairs_e, int npairs_e,
-                                  void* stream) {
-  PDG_CHECK_ARG(C != nullptr, "pdg_edge_bwd_w2_rc: C is required");
-  return edge_bwd_w2_launch(n_edges, dst, gaggr, ge_next, a2m, nullptr, a2e, nullptr, st_m, st_e, lb_m, lb_e, ln_g,
-                            W2T, gz1m, gz1e, gC, slabs, nslabs, pairs_m, npairs_m, pairs_e, npairs_e, src, C, P, Q,
-                            stream);
-}
-
-static int edge_gout_wc_launch(int n_edges, const float* gC, const float* gC2, const float* e, const float* ge_next,
-                               const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
-                               const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,
-                               int accumulate, void* stream) {
+extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
+                                float* ge_out, float* slabs, int nslabs, const float* a2ln, const pdg_ln_stat* st_ln,
+                                double* ln_partials, const float* ln_g, double* pairs, int accumulate, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_gout_wc: n_edges must be > 0");
-  PDG_CHECK_ARG(!gC2 || PDG_ALIGNED(gC2), "pdg_edge_gout_wc2: misaligned gz1e");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_gout_wc: bad slabs");
   PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_gout_wc: the XCD-interleaved build needs 256 blocks");
   PDG_CHECK_ARG(gC && e && WcT && ge_out, "pdg_edge_gout_wc: null argument");
@@ -1852,32 +1772,14 @@ static int edge_gout_wc_launch(int n_edges, const float* gC, const float* gC2, c
   PDG_CHECK_ARG(!pairs || (a2ln && ln_g), "pdg_edge_gout_wc: pairs need a2ln and ln_g");
   // LDS: the two images, then (LayerNorm column sums) the row groups' sums + one row + its scratch
   const size_t shm = 2 * EBW_IMG + ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
-#define PDG_GOUT(R, C)                                                                                            \
-  hipLaunchKernelGGL((edge_gout_wc_kernel<R, C>), dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, gC2, \
-                     e, ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate)
-  if (ge_next) {
-    if (gC2) PDG_GOUT(true, true); else PDG_GOUT(true, false);
-  } else {
-    if (gC2) PDG_GOUT(false, true); else PDG_GOUT(false, false);
-  }
-#undef PDG_GOUT
+  if (ge_next)
+    hipLaunchKernelGGL(edge_gout_wc_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
+                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
+  else
+    hipLaunchKernelGGL(edge_gout_wc_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
+                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
   PDG_CHECK_LAUNCH("pdg_edge_gout_wc");
   return PDG_OK;
-}
-
-extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
-                                float* ge_out, float* slabs, int nslabs, const float* a2ln, const pdg_ln_stat* st_ln,
-                                double* ln_partials, const float* ln_g, double* pairs, int accumulate, void* stream) {
-  return edge_gout_wc_launch(n_edges, gC, nullptr, e, ge_next, WcT, ge_out, slabs, nslabs, a2ln, st_ln, ln_partials,
-                             ln_g, pairs, accumulate, stream);
-}
-
-extern "C" int pdg_edge_gout_wc2(int n_edges, const float* gz1m, const float* gz1e, const float* e,
-                                 const float* ge_next, const float* WcT, float* ge_out, float* slabs, int nslabs,
-                                 const float* a2ln, const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g,
-                                 double* pairs, int accumulate, void* stream) {
-  return edge_gout_wc_launch(n_edges, gz1m, gz1e, e, ge_next, WcT, ge_out, slabs, nslabs, a2ln, st_ln, ln_partials,
-                             ln_g, pairs, accumulate, stream);
 }
 
 extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, const float* e_in, const float* w0,
@@ -1913,7 +1815,7 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
                                 const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                                 const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                                 double* part_e, int with_edge_update, double* sums, double* seg_part, int* seg_info,
-                                int nblocks, int store_c, void* stream);
+                                int nblocks, void* stream);
 
 // deferred a2 stores in the cooperative edge forward (edge_fwd_coop_kernel's D)
 // (default: bitwise the same outputs; with X below 216 -> 210.5 us per config-2 call, the step -0.05 ms, in
@@ -1932,19 +1834,8 @@ extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln
                                  const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                                  double* part_e, int with_edge_update, int nblocks, void* stream) {
   return edge_fwd_coop_launch(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m,
-                              a2m, a1e, a2e, part_m, part_e, with_edge_update, nullptr, nullptr, nullptr, nblocks, 0,
+                              a2m, a1e, a2e, part_m, part_e, with_edge_update, nullptr, nullptr, nullptr, nblocks,
                               stream);
-}
-
-extern "C" int pdg_edge_fwd_coop_c(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                                   const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
-                                   const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
-                                   const float* b2, float* c_out, float* a2m, float* a2e, double* part_m,
-                                   double* part_e, int with_edge_update, int nblocks, void* stream) {
-  PDG_CHECK_ARG(c_out != nullptr && a2m != nullptr, "pdg_edge_fwd_coop_c: c_out and a2m are required");
-  return edge_fwd_coop_launch(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, c_out,
-                              a2m, nullptr, a2e, part_m, part_e, with_edge_update, nullptr, nullptr, nullptr, nblocks,
-                              1, stream);
 }
 
 extern "C" int pdg_edge_fwd_coop_seg(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
@@ -1954,7 +1845,7 @@ extern "C" int pdg_edge_fwd_coop_seg(int n_edges, const float* a2_prev, const pd
                                      double* part_m, double* part_e, int with_edge_update, double* sums,
                                      double* seg_part, int* seg_info, int nblocks, void* stream) {
   return edge_fwd_coop_launch(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m,
-                              a2m, a1e, a2e, part_m, part_e, with_edge_update, sums, seg_part, seg_info, nblocks, 0,
+                              a2m, a1e, a2e, part_m, part_e, with_edge_update, sums, seg_part, seg_info, nblocks,
                               stream);
 }
 
@@ -1963,7 +1854,7 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
                                 const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                                 const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                                 double* part_e, int with_edge_update, double* sums, double* seg_part, int* seg_info,
-                                int nblocks, int store_c, void* stream) {
+                                int nblocks, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd_coop: n_edges must be > 0");
   PDG_CHECK_ARG(nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_fwd_coop: bad nblocks");
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
@@ -1988,7 +1879,7 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
   hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER, X>), \
                      dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
                      ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e,  \
-                     sums, seg_part, seg_info, store_c)
+                     sums, seg_part, seg_info)
 #define PDG_EFC(R, U, S)                           \
   do {                                             \
     if (!(S) && PDG_EFC_XCD && xcd) {              \

@@ -768,13 +768,21 @@ __global__ __launch_bounds__(384, 3) void decoder_kernel(int N, const float* __r
                                                           const float* __restrict__ Wd2,
                                                           const float* __restrict__ bd2,
                                                           const float* __restrict__ st8, int scale,
-                                                          float* __restrict__ y) {
+                                                          float* __restrict__ y, const double* __restrict__ part,
+                                                          int nparts, double count, pdg_ln_stat* __restrict__ st_out) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* w2l = lds + WBLK;   // Wd2 (3 x 128)
+  __shared__ LNStat st_sh;
+  __shared__ double red_fin[2 * 384 / 64];
+  if (part) {   // the last node LayerNorm's statistics folded in (pdg_decoder_fwd_fin; pdg_ln_finalize's order)
+    ln_stat_from_partials(part, nparts, count, &st_sh, red_fin);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_sh;
+  }
   load_wblock(lds, Wd1, L, 0);
   for (int i = threadIdx.x; i < 3 * L; i += blockDim.x) w2l[i] = Wd2[i];
   __syncthreads();
-  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const LNStat st = part ? st_sh : *reinterpret_cast<const LNStat*>(stp);
   const int l = lane_id(), q = l >> 4;
   PDG_TILE_LOOP(N) {
     const int row = tile * TILE + (l & 15);
@@ -818,21 +826,42 @@ __global__ __launch_bounds__(384, 3) void decoder_kernel(int N, const float* __r
   }
 }
 
-extern "C" int pdg_decoder_fwd(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                               const float* ln_b, const float* x_res, float* x_out, const float* Wd1,
-                               const float* bd1, float* a1d, const float* Wd2, const float* bd2,
-                               const float* stats8, int scale_output, float* y, void* stream) {
+static int decoder_fwd_launch(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                              const float* ln_b, const float* x_res, float* x_out, const float* Wd1, const float* bd1,
+                              float* a1d, const float* Wd2, const float* bd2, const float* stats8, int scale_output,
+                              float* y, const double* partials, int nparts, double count, pdg_ln_stat* st_out,
+                              void* stream) {
   PDG_CHECK_ARG(n_nodes > 0, "pdg_decoder_fwd: n_nodes must be > 0");
   PDG_CHECK_ARG(x_res != nullptr, "pdg_decoder_fwd: x_res is NULL");
   PDG_CHECK_ARG(!scale_output || stats8 != nullptr, "pdg_decoder_fwd: stats8 is NULL");
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(x_res) && PDG_ALIGNED(x_out) && PDG_ALIGNED(a1d) &&
                     PDG_ALIGNED(Wd1) && PDG_ALIGNED(Wd2),
                 "pdg_decoder_fwd: misaligned pointer");
+  PDG_CHECK_ARG(partials ? (nparts > 0 && count > 0 && st_out != nullptr) : st != nullptr,
+                "pdg_decoder_fwd: statistics arguments");
   const int grid = persistent_grid(n_nodes, 6, 2);
   hipLaunchKernelGGL(decoder_kernel, dim3(grid), dim3(384), (WBLK + 3 * L) * sizeof(float), (hipStream_t)stream,
-                     n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, Wd1, bd1, a1d, Wd2, bd2, stats8, scale_output, y);
+                     n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, Wd1, bd1, a1d, Wd2, bd2, stats8, scale_output, y,
+                     partials, nparts, count, st_out);
   PDG_CHECK_LAUNCH("pdg_decoder_fwd");
   return PDG_OK;
+}
+
+extern "C" int pdg_decoder_fwd(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                               const float* ln_b, const float* x_res, float* x_out, const float* Wd1,
+                               const float* bd1, float* a1d, const float* Wd2, const float* bd2,
+                               const float* stats8, int scale_output, float* y, void* stream) {
+  return decoder_fwd_launch(n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, Wd1, bd1, a1d, Wd2, bd2, stats8,
+                            scale_output, y, nullptr, 0, 0.0, nullptr, stream);
+}
+
+extern "C" int pdg_decoder_fwd_fin(int n_nodes, const float* a2_prev, const double* partials, int nparts, double count,
+                                   pdg_ln_stat* st_out, const float* ln_g, const float* ln_b, const float* x_res,
+                                   float* x_out, const float* Wd1, const float* bd1, float* a1d, const float* Wd2,
+                                   const float* bd2, const float* stats8, int scale_output, float* y, void* stream) {
+  PDG_CHECK_ARG(partials != nullptr, "pdg_decoder_fwd_fin: partials are required");
+  return decoder_fwd_launch(n_nodes, a2_prev, nullptr, ln_g, ln_b, x_res, x_out, Wd1, bd1, a1d, Wd2, bd2, stats8,
+                            scale_output, y, partials, nparts, count, st_out, stream);
 }
 
 // ============================================================================ any-nonzero guard

@@ -93,15 +93,6 @@ VARIANTS = {
     "pair_blocks_per_cu": ("PDG_PAIR_BLOCKS_PER_CU", 1),
     # pdg_edge_enc_fwd blocks per CU (104 VGPRs, 41 KB LDS per 8-wave block)
     "enc_blocks_per_cu": ("PDG_ENC_BLOCKS_PER_CU", 2),
-    # training with the fused cooperative kernels: the edge forward stores C = Wc e + b1 instead of a1m
-    # and a1e (pdg_edge_fwd_coop_c) and the edge backward recomputes both bit for bit from C and the
-    # step's P / Q (pdg_edge_bwd_w2_rc): one E-row array written and one read instead of two each.
-    # Bitwise the same; off: 8.85-8.91 vs 8.78 ms per config-2 step (same box; edge_bwd 214 vs 201 us,
-    # the four P / Q row gathers cost more than the a1 row they replace, edge_fwd unchanged)
-    "recompute_a1": ("PDG_RECOMPUTE_A1", False),
-    # the Wc pass reads gz1m + gz1e and forms gC on load (pdg_edge_gout_wc2), so the edge backward writes
-    # no gC stream (bitwise the same)
-    "gout_gz1": ("PDG_GOUT_GZ1", False),
 }
 
 
@@ -203,7 +194,6 @@ class EPDEngine:
         # kernel variants (VARIANTS above; tests and A/B tools flip these attributes)
         self.fused_edge_wgrad = var["fused_edge_wgrad"]
         self.pq_first = var["pq_first"]
-        self.gout_gz1 = var["gout_gz1"]
         self.coop_fwd = var["coop_fwd"]
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
@@ -211,7 +201,6 @@ class EPDEngine:
         self.seg_sums_train = self.coop_fwd and var["seg_sums_train"]
         self.gsum2_coop = var["gsum2_coop"]
         self.nbwd_coop = var["nbwd_coop"]
-        self.recompute_a1 = var["recompute_a1"]
         self._enc_blocks = min(var["enc_blocks_per_cu"] *
                                torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
         self._seg_part = torch.empty(2 * self._nslabs_e * L, dtype=torch.float64, device=self.device)
@@ -321,17 +310,11 @@ class EPDEngine:
         a2n_prev, stn_prev, gn_prev, bn_prev = a2_ne, st[0], P["node_encoder.4.weight"], P["node_encoder.4.bias"]
         a2e_prev, ste_prev, ge_prev, be_prev = a2_ee, st[1], P["edge_encoder.4.weight"], P["edge_encoder.4.bias"]
         x_prev = e_prev = None
-        # the backward recomputes a1m / a1e from C and this step's P / Q (pdg_edge_bwd_w2_rc): P and Q
-        # are then kept per step
-        rc = (need_grad and bool(E) and self.recompute_a1 and self.fused_edge_wgrad and self.coop_fwd
-              and not self.seg_sums_train)
         Pm, Qm = self._empty(N, L), self._empty(N, L)
         # pend_n: deferred node LayerNorm statistics (nparts of the partials in pend_buf)
         for t in range(steps):
             i_m, i_e, i_n = 2 + 3 * t, 3 + 3 * t, 4 + 3 * t
             x_t = self._empty(N, L)
-            if rc and t > 0:
-                Pm, Qm = self._empty(N, L), self._empty(N, L)
             if pend_n is not None:    # the previous step's node statistics, reduced inside node_pq
                 self._t("node_pq", lib.pdg_node_pq_rw_fin, N, _p(a2n_prev), pend_buf.data_ptr(), pend_n,
                         float(N * L), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_t), _p(W1), _p(Pm),
@@ -346,17 +329,10 @@ class EPDEngine:
             seg = bool(E) and (self.seg_sums_train if need_grad else self.seg_sums)
             a2m = self._empty(E, L) if (need_grad or not seg) else None   # seg: a backward-only output
             sums = torch.empty(N, L, dtype=torch.float64, device=self.device) if seg else None
-            a1m = self._empty(E, L) if (need_grad and not rc) else None   # layer-1 outputs: backward only
+            a1m = self._empty(E, L) if need_grad else None   # layer-1 outputs: backward only
             a2e = self._empty(E, L) if eu else None
-            a1e = self._empty(E, L) if (eu and need_grad and not rc) else None
-            cst = self._empty(E, L) if rc else None                         # rc: C = Wc e + b1 instead
-            if rc:
-                self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop_c, E, _p(a2e_prev), ste_prev,
-                        _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm),
-                        _p(W1), _p(b1), _p(W2), _p(b2), _p(cst), _p(a2m), _p(a2e), _p(self._part_a),
-                        _p(self._part_b), int(eu), self._nslabs_e, s)
-                self._nparts.value = self._nslabs_e
-            elif seg:
+            a1e = self._empty(E, L) if (eu and need_grad) else None
+            if seg:
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop_seg, E, _p(a2e_prev),
                         ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm),
                         _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e),
@@ -406,14 +382,14 @@ class EPDEngine:
                 xs = torch.zeros(N, L, dtype=torch.float32, device=self.device) if need_grad else None
             self._t("node_net", lib.pdg_node_net, N, _p(aggr), _p(x_t), _p(Wn1), _p(bn1), _p(Wn2), _p(bn2), _p(a1n),
                     _p(a2n), _p(self._part_a), np_, s)
-            if t < steps - 1 and self.sync is None:
-                pend_n, pend_buf = self._nparts.value, self._part_a   # finalised by the next step's node_pq
+            if self.sync is None:
+                # finalised by the next step's node_pq, or by the decoder after the last step
+                pend_n, pend_buf = self._nparts.value, self._part_a
             else:
                 self._finalize(self._part_a, N * L, st[i_n], s)
             if need_grad:
                 ctx.per_step.append(dict(x=x_t, e=e_t, a1m=a1m, a2m=a2m, a1e=a1e, a2e=a2e, aggr=aggr, xs=xs,
-                                         a1n=a1n, a2n=a2n, i_m=i_m, i_e=i_e, i_n=i_n, eu=eu, C=cst,
-                                         P=Pm if rc else None, Q=Qm if rc else None))
+                                         a1n=a1n, a2n=a2n, i_m=i_m, i_e=i_e, i_n=i_n, eu=eu))
             a2n_prev, stn_prev, gn_prev, bn_prev = a2n, st[i_n], gn, bnn
             a2e_prev, ste_prev, ge_prev, be_prev = a2e, st[i_e], ge, be
             x_prev, e_prev = x_t, e_t
@@ -421,10 +397,16 @@ class EPDEngine:
         x_S, a1d, y = self._empty(N, L), self._empty(N, L), self._empty(N, 3)
         if x_prev is None:
             raise ValueError("message_passing_steps must be >= 1")
-        lib.pdg_decoder_fwd(N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_S),
-                            _p(P["node_decoder.0.weight"]), _p(P["node_decoder.0.bias"]), _p(a1d),
-                            _p(P["node_decoder.2.weight"]), _p(P["node_decoder.2.bias"]), _p(stats8),
-                            int(scale_output), _p(y), s)
+        if pend_n is not None:   # the last node LayerNorm's statistics reduced inside the decoder
+            lib.pdg_decoder_fwd_fin(N, _p(a2n_prev), pend_buf.data_ptr(), pend_n, float(N * L), stn_prev,
+                                    _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_S), _p(P["node_decoder.0.weight"]),
+                                    _p(P["node_decoder.0.bias"]), _p(a1d), _p(P["node_decoder.2.weight"]),
+                                    _p(P["node_decoder.2.bias"]), _p(stats8), int(scale_output), _p(y), s)
+        else:
+            lib.pdg_decoder_fwd(N, _p(a2n_prev), stn_prev, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_S),
+                                _p(P["node_decoder.0.weight"]), _p(P["node_decoder.0.bias"]), _p(a1d),
+                                _p(P["node_decoder.2.weight"]), _p(P["node_decoder.2.bias"]), _p(stats8),
+                                int(scale_output), _p(y), s)
         if need_grad:
             ctx.x_S, ctx.a1d = x_S, a1d
         return y, ctx
@@ -537,8 +519,7 @@ class EPDEngine:
         gaggr, gx_part, gx_t = (self._empty(N, L) for _ in range(3))
         gz1m, gz1e = self._empty(E, L), self._empty(E, L)
         ge_bufs = [self._empty(E, L), self._empty(E, L)]
-        gz1_in_gout = fused and self.gout_gz1   # gC formed by pdg_edge_gout_wc2 from gz1m + gz1e
-        gC_fused = self._empty(E, L) if (fused and not gz1_in_gout) else None
+        gC_fused = self._empty(E, L) if fused else None
         gx_next = gx
         # node LayerNorm of the last step (upstream gradient: the decoder's); for the earlier steps
         # the previous iteration's pdg_gemm_sum2_rw produces these partials
@@ -553,7 +534,7 @@ class EPDEngine:
             assert E == 0 or eu == (ge_next is not None)
             gz2n, gz1n, gP, gQ = (self._empty(N, L) for _ in range(4))
             gC = gC_fused if fused else self._empty(E, L)   # fused: consumed within the step
-            if fused and not eu and not gz1_in_gout:
+            if fused and not eu:
                 gC = gz1m   # message branch only: gC = gz1m, written once (pdg_edge_bwd_w2)
             gz2m = None if fused else self._empty(E, L)
             gz2e = self._empty(E, L) if (eu and not fused) else None
@@ -580,13 +561,7 @@ class EPDEngine:
                 if eu:   # edge-update LayerNorm: gy = ge_next (per edge)
                     pp, n_e = edge_ln_pairs(PE(t), ge_next, d["a2e"], st[d["i_e"]], ACC_E, g_edge)
                     pe, ne = src(pp, n_e if not fused else n_edge)
-                if fused and d["C"] is not None:   # a1m / a1e recomputed from C and the step's P / Q
-                    self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2_rc, E, _p(plan.dst),
-                            _p(plan.src), _p(gaggr), _p(ge_next), _p(d["a2m"]), _p(d["C"]), _p(d["P"]), _p(d["Q"]),
-                            _p(d["a2e"]), st[d["i_m"]], st[d["i_e"]] if eu else None, None, None, _p(g_edge),
-                            _p(T["W2T"]), _p(gz1m), _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe,
-                            ne, s)
-                elif fused:
+                if fused:
                     self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
@@ -601,10 +576,7 @@ class EPDEngine:
                         a2ln, st_ln, accb, gl, pp = ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"], P_EENC
                     tail = (_p(d["e"]), _p(ge_next), _p(T["WcT"]), _p(ge_out), _p(slabs_wc), nse, _p(a2ln), st_ln,
                             _p(accb), _p(gl), _p(pp), 1, s)
-                    if gz1_in_gout:
-                        gout_fn, gout_args = lib.pdg_edge_gout_wc2, (E, _p(gz1m), _p(gz1e if eu else None)) + tail
-                    else:
-                        gout_fn, gout_args = lib.pdg_edge_gout_wc, (E, _p(gC)) + tail
+                    gout_fn, gout_args = lib.pdg_edge_gout_wc, (E, _p(gC)) + tail
                     if not self.pq_first:
                         self._t("edge_gout", gout_fn, *gout_args)
                     n_edge = nse

@@ -55,6 +55,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_mlp2_fwd": [I, P, P, P, P, P, P, P],
     "pdg_node_net": [I, P, P, P, P, P, P, P, P, P, P, P],
     "pdg_decoder_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
+    "pdg_decoder_fwd_fin": [I, P, P, I, c_double, P] + [P] * 10 + [I, P, P],
     "pdg_any_nonzero": [P, c_int64, P, P],
     "pdg_decoder_bwd": [I, P, P, P, P, P, P, P],
     "pdg_ln_colsum": [I, P, P, P, P, P, P, P, P, I, P],
@@ -75,7 +76,6 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_edge_fwd_coop_seg": [I] + [P] * 20 + [I, P, P, P, I, P],
-    "pdg_edge_fwd_coop_c": [I] + [P] * 19 + [I, I, P],
     "pdg_segsum_fixup": [I, P, P, P, P],
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
@@ -89,9 +89,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_edge_enc_bwd": [I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P],
     "pdg_enc_narrow_reduce": [P, I, P, P, P],
     "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P, I, P],
-    "pdg_edge_bwd_w2_rc": [I] + [P] * 19 + [I, P, I, P, I, P],
     "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P, P, I, P],
-    "pdg_edge_gout_wc2": [I, P, P, P, P, P, P, P, I, P, P, P, P, P, I, P],
     "pdg_mesh_graph": [I, P, I, I, P, I, P, P, P, ctypes.c_long, P, P, ctypes.c_long, P],
     "pdg_mesh_graph_scratch_bytes": [I, I],
     "pdg_wgrad_segments": [I, P, P, P, P, I, P],

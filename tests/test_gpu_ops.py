@@ -560,6 +560,42 @@ def test_node_pq_rw_fin_equals_finalize_then_pq_rw(env, N, nparts, res):
         assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("N,nparts,scale", [(7, 1, 1), (1031, 37, 0), (40328, 256, 1), (5000, 700, 0)])
+def test_decoder_fwd_fin_equals_finalize_then_decoder(env, N, nparts, scale):
+    """pdg_decoder_fwd_fin (the last node LayerNorm's statistics reduced inside the decoder) is bitwise
+    pdg_ln_finalize + pdg_decoder_fwd: x_S, a1d, y and the stored pdg_ln_stat."""
+    lib, sh, _ = env
+    s = sh()
+    a2 = torch.relu(rnd(N, L))
+    xr = rnd(N, L)
+    g, b = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
+    Wd1, bd1 = lin(L, L)
+    Wd2, bd2 = lin(3, L)
+    st8 = torch.tensor([0.1, 1.2, -0.3, 2.0, 0.25, 3.5, 0.05, 0.7], device="cuda")
+    edges = torch.linspace(0, N, nparts + 1).round().long().tolist()
+    a64 = a2.double()
+    part = torch.stack([torch.stack([a64[i:j].sum(), a64[i:j].square().sum()])
+                        for i, j in zip(edges[:-1], edges[1:])]).reshape(-1).cuda()
+    st_ref = finalize(lib, s, part, nparts, N * L)
+    outs = []
+    xs, a1, y = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda"), torch.empty(N, 3, device="cuda")
+    assert lib.pdg_decoder_fwd(N, a2.data_ptr(), st_ref.data_ptr(), g.data_ptr(), b.data_ptr(), xr.data_ptr(),
+                               xs.data_ptr(), Wd1.data_ptr(), bd1.data_ptr(), a1.data_ptr(), Wd2.data_ptr(),
+                               bd2.data_ptr(), st8.data_ptr(), scale, y.data_ptr(), s) == 0
+    outs.append((xs, a1, y))
+    st_fin = torch.full((40,), 0xAB, dtype=torch.uint8, device="cuda")
+    xs, a1, y = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda"), torch.empty(N, 3, device="cuda")
+    assert lib.pdg_decoder_fwd_fin(N, a2.data_ptr(), part.data_ptr(), nparts, float(N * L), st_fin.data_ptr(),
+                                   g.data_ptr(), b.data_ptr(), xr.data_ptr(), xs.data_ptr(), Wd1.data_ptr(),
+                                   bd1.data_ptr(), a1.data_ptr(), Wd2.data_ptr(), bd2.data_ptr(), st8.data_ptr(),
+                                   scale, y.data_ptr(), s) == 0
+    outs.append((xs, a1, y))
+    torch.cuda.synchronize()
+    assert torch.equal(st_ref, st_fin)
+    for u, v in zip(*outs):
+        assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("E", [77, 5000])
 def test_edge_enc_bwd_vs_autograd(env, E):
     """pdg_edge_enc_bwd (edge encoder backward in one pass, layer-1 output recomputed from the scalar
@@ -695,86 +731,6 @@ def test_edge_fwd_coop_matches_edge_fwd(env, E, eu, res):
     assert rel(pm1, pm0) < 1e-6
     if eu:
         assert rel(pe1, pe0) < 1e-6
-
-
-@pytest.mark.parametrize("E,eu", [(4099, 1), (4099, 0), (77, 1), (60001, 1)])
-def test_edge_c_recompute_matches_stored_a1(env, E, eu):
-    """pdg_edge_fwd_coop_c + pdg_edge_bwd_w2_rc (C = Wc e + b1 stored, a1m / a1e recomputed in the
-    backward from C and the P / Q gathered at dst / src) against pdg_edge_fwd_coop + pdg_edge_bwd_w2
-    (a1m / a1e stored): every forward output but a1 bitwise, a1m == relu((C + P[dst]) + Q[src]) and
-    a1e == relu((C + P[src]) + Q[dst]) bitwise, and every backward output (gz1m, gz1e, gC, the dW2
-    slabs) bitwise.  (77: fewer rows than blocks x 16, empty blocks; 60001: many rounds per block.)"""
-    lib, sh, _ = env
-    s = sh()
-    N = max(300, E // 6)
-    g = torch.Generator().manual_seed(E + eu)
-    src = torch.randint(0, N, (E,), generator=g).int().cuda()
-    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values.int().cuda()
-    a2p, eres = torch.relu(rnd(E, L)), rnd(E, L)
-    Pn, Qn = rnd(N, L), rnd(N, L)
-    W1, b1 = lin(L, 3 * L)
-    W2, b2 = lin(L, L)
-    lg, lbv = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
-    part = torch.empty(4096, dtype=torch.float64, device="cuda")
-    n = ctypes.c_int(0)
-    tmp = torch.empty(E, L, device="cuda")
-    lib.pdg_mlp2_fwd(E, a2p.data_ptr(), W2.data_ptr(), b2.data_ptr(), tmp.data_ptr(), part.data_ptr(),
-                     ctypes.byref(n), s)
-    st = finalize(lib, s, part, n.value, E * L)
-    nb = 37
-    fw = {}
-    for mode in ("a1", "c"):
-        o = {k: torch.full((E, L), float("nan"), device="cuda") for k in ("e", "a1m", "a2m", "a1e", "a2e", "c")}
-        pm = torch.zeros(4096, dtype=torch.float64, device="cuda")
-        pe = torch.zeros(4096, dtype=torch.float64, device="cuda")
-        head = (E, a2p.data_ptr(), st.data_ptr(), lg.data_ptr(), lbv.data_ptr(), eres.data_ptr(), o["e"].data_ptr(),
-                src.data_ptr(), dst.data_ptr(), Pn.data_ptr(), Qn.data_ptr(), W1.data_ptr(), b1.data_ptr(),
-                W2.data_ptr(), b2.data_ptr())
-        if mode == "a1":
-            lib.pdg_edge_fwd_coop(*head, o["a1m"].data_ptr(), o["a2m"].data_ptr(), o["a1e"].data_ptr() if eu else None,
-                                  o["a2e"].data_ptr() if eu else None, pm.data_ptr(), pe.data_ptr() if eu else None,
-                                  eu, nb, s)
-        else:
-            lib.pdg_edge_fwd_coop_c(*head, o["c"].data_ptr(), o["a2m"].data_ptr(), o["a2e"].data_ptr() if eu else None,
-                                    pm.data_ptr(), pe.data_ptr() if eu else None, eu, nb, s)
-        fw[mode] = (o, pm[: 2 * nb].clone(), pe[: 2 * nb].clone())
-    (oa, pma, pea), (oc, pmc, pec) = fw["a1"], fw["c"]
-    for k in ("e", "a2m") + (("a2e",) if eu else ()):
-        assert torch.equal(oa[k], oc[k]), k
-    assert torch.equal(pma, pmc) and torch.equal(pea, pec)
-    d, sr = dst.long(), src.long()
-    assert torch.equal(torch.relu((oc["c"] + Pn[d]) + Qn[sr]), oa["a1m"])
-    if eu:
-        assert torch.equal(torch.relu((oc["c"] + Pn[sr]) + Qn[d]), oa["a1e"])
-    # backward on the same upstream gradients and statistics
-    gaggr, ge_next = rnd(N, L), rnd(E, L)
-    W2T = W2.t().contiguous()
-    stm = finalize(lib, s, part, n.value, E * L)
-    lb = torch.zeros(2, 24, dtype=torch.uint8, device="cuda")
-    lb[:, :8] = torch.tensor([0.01, -0.02], dtype=torch.float32).view(torch.uint8).cuda()
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    bw = {}
-    for mode in ("a1", "c"):
-        r = {k: torch.full((E, L), 7.0, device="cuda") for k in ("gz1m", "gz1e", "gC")}
-        slabs = torch.zeros(cus, L * L + L, device="cuda")
-        common_tail = (stm.data_ptr(), stm.data_ptr() if eu else None, lb.data_ptr(), lb.data_ptr() + 24 if eu else None,
-                       lg.data_ptr(), W2T.data_ptr(), r["gz1m"].data_ptr(), r["gz1e"].data_ptr() if eu else None,
-                       r["gC"].data_ptr(), slabs.data_ptr(), cus, None, 0, None, 0, s)
-        if mode == "a1":
-            lib.pdg_edge_bwd_w2(E, dst.data_ptr(), gaggr.data_ptr(), ge_next.data_ptr() if eu else None,
-                                oa["a2m"].data_ptr(), oa["a1m"].data_ptr(), oa["a2e"].data_ptr() if eu else None,
-                                oa["a1e"].data_ptr() if eu else None, *common_tail)
-        else:
-            lib.pdg_edge_bwd_w2_rc(E, dst.data_ptr(), src.data_ptr(), gaggr.data_ptr(),
-                                   ge_next.data_ptr() if eu else None, oc["a2m"].data_ptr(), oc["c"].data_ptr(),
-                                   Pn.data_ptr(), Qn.data_ptr(), oc["a2e"].data_ptr() if eu else None, *common_tail)
-        torch.cuda.synchronize()
-        bw[mode] = (r, slabs)
-    (ra, sa), (rc_, sc) = bw["a1"], bw["c"]
-    for k in ("gz1m", "gC") + (("gz1e",) if eu else ()):
-        assert torch.equal(ra[k], rc_[k]), k
-    assert torch.equal(sa, sc)
-    assert bool(torch.isfinite(ra["gC"]).all())
 
 
 def _seg_graph(kind, g):
