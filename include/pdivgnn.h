@@ -325,8 +325,10 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
  * backward).  Weights stationary in registers, 32-row operand images in LDS; one block per
  * slab, `nslabs` blocks (the same value for every call of a backward pass: the block ->
  * slab map is fixed and the slabs accumulate, reduced once by pdg_wgrad_reduce).
- *   pdg_edge_bwd_w2:  gz1m/gz1e/gC as pdg_edge_bwd; slabs (zeroed before the first call)
- *                     += gz2m^T a1m + gz2e^T a1e and the b2 column sums; gz2m/gz2e are not
+ *   pdg_edge_bwd_w2:  gz1m/gz1e/gC as pdg_edge_bwd; slabs += gz2m^T a1m + gz2e^T a1e and the
+ *                     b2 column sums (slab_init != 0: slabs = ..., the first call of a backward,
+ *                     so the slabs need no zero fill; the same for pdg_edge_gout_wc and
+ *                     pdg_edge_enc_bwd); gz2m/gz2e are not
  *                     materialised.  ge_next == NULL: message branch only, gC = gz1m (gC may
  *                     then be the gz1m pointer itself: written once).
  *   pdg_edge_gout_wc: ge_out = [ge_next +] WcT gC; slabs += gC^T e and the b1 column sums.
@@ -339,7 +341,7 @@ int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float
                     const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
                     const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
                     float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
-                    const double* pairs_e, int npairs_e, void* stream);
+                    const double* pairs_e, int npairs_e, int slab_init, void* stream);
 /* Edge encoder backward (models.py:268-274), fused: gz2 = LN_bwd(gy) [a2 > 0], slabs (zeroed
  * before, pdg_wgrad_reduce layout) += gz2^T a1 and the b2 sums, gz1 = (W2T gz2) [a1 > 0], and per
  * block narrow_sums[b] = (sum gz1 e_in, sum gz1) as 2 x 128 doubles; a1 = relu(w0 e_in + b0) is
@@ -348,13 +350,13 @@ int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float
 int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, const float* e_in, const float* w0,
                      const float* b0, const pdg_ln_stat* st, const pdg_ln_bwd* lb, const double* lb_pairs,
                      int lb_npairs, const float* ln_g, const float* W2T, float* slabs, double* narrow_sums,
-                     int nslabs, void* stream);
+                     int nslabs, int slab_init, void* stream);
 /* grad_w0 += sum_b narrow_sums[b][0:128], grad_b0 += sum_b narrow_sums[b][128:256] (block order). */
 int pdg_enc_narrow_reduce(const double* narrow_sums, int nslabs, float* grad_w0, float* grad_b0, void* stream);
 int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next,
                      const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
                      const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,
-                     int accumulate, void* stream);
+                     int accumulate, int slab_init, void* stream);
 
 /* Mesh graph on the device (pdg_graph.hip): FaceToEdge of a triangle
  * mesh (convert_utils.py:47-60), edge lengths (datasets.py:182-188) and, when `periodic`,
@@ -415,6 +417,19 @@ int pdg_wgrad_narrow(int rows, const float* wide, const float* narrow, int k_nar
  * pdg_wgrad_narrow's order), for partials formed inside pdg_mlp2_bwd_coop / pdg_decoder_bwd_coop. */
 int pdg_wgrad_narrow_finalize(const double* partials, int nparts, int k_narrow, int transpose, float* grad_W,
                               float* grad_b_wide, float* grad_b_narrow, void* stream);
+/* Every end-of-backward reduction in one launch: n_reduce slab reductions as pdg_wgrad_reduce_batch
+ * (<= 16), n_ln LayerNorm groups as pdg_ln_param_grads (<= 4), n_narrow (<= 2) narrow finalizes as
+ * pdg_wgrad_narrow_finalize, and (enc_sums != NULL) the edge encoder's first-layer sums as
+ * pdg_enc_narrow_reduce.  Bitwise the separate launches' gradients except the encoder sums, which add
+ * their rows in another fixed order.  New in this build (the reference's autograd accumulates the
+ * parameter gradients in place, gnn_train.py:160-161). */
+int pdg_bwd_epilogue(int n_reduce, const float* const* slabs, const int* nslabs, float* const* grad_W,
+                     const int* ld, const int* col0, float* const* grad_b, int n_ln, const double* const* ln_acc,
+                     const int* ln_rows, float* const* ln_grad_g, float* const* ln_grad_b, int n_narrow,
+                     const double* const* narrow_partials, const int* narrow_nparts, const int* narrow_k,
+                     const int* narrow_transpose, float* const* narrow_gW, float* const* narrow_gb_wide,
+                     float* const* narrow_gb_narrow, const double* enc_sums, int enc_nslabs, float* enc_grad_w0,
+                     float* enc_grad_b0, void* stream);
 
 /* ---------------------------------------------------------------- losses */
 
@@ -425,6 +440,10 @@ int pdg_nmse_fwd(int n_graphs, const int* ptr, const float* gt, const float* pre
 /* g_pred[n][c] (+)= scale * (-2/3) (gt-pred)/den_c. */
 int pdg_nmse_bwd(int n_graphs, const int* ptr, int n_nodes, const float* gt, const float* pred,
                  const float* den, const float* scale, int accumulate, float* g_pred, void* stream);
+/* pdg_nmse_fwd + pdg_nmse_bwd in one launch (bitwise the two): each graph's block also writes its
+ * gradient rows from the denominators it just formed. */
+int pdg_nmse_fwd_bwd(int n_graphs, const int* ptr, const float* gt, const float* pred, float* loss, float* den,
+                     const float* scale, int accumulate, float* g_pred, void* stream);
 
 /* Divergence penalty (gnn_train.py:60-92) with the operator in CSR over global rows and
  * graph-local columns (col < n_i: x-derivative, else y-derivative), ptr = node offsets:

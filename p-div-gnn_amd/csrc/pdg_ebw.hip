@@ -197,7 +197,7 @@ __device__ __forceinline__ void row_schedule(bool xi, int M, int& r0, int& r1, i
 // thread (cg, rg) holds column sums of columns 4cg .. 4cg+3 over its rows; reduced over
 // the 16 row groups in order through LDS (`red`, 8 KB, the images being dead).
 __device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const f32x16 (&acc)[2], const f32x4& bsum,
-                                                float* red) {
+                                                float* red, int init) {
   const int l = lane_id(), w = wave_id(), h = l >> 5, c = l & 31;
   const int ob = 32 * (w & 3), ib = 64 * (w >> 2);
   // every load before any store: vmcnt counts loads and stores together in issue order, so a
@@ -209,7 +209,7 @@ __device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const 
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h, i = ib + 32 * b + c;
-      old[b][r] = slab[o * L + i];
+      old[b][r] = init ? 0.f : slab[o * L + i];   // init: the first call of a backward writes (no fill)
     }
 #pragma unroll
   for (int b = 0; b < 2; ++b)
@@ -225,7 +225,7 @@ __device__ __forceinline__ void slab_accumulate(float* __restrict__ slab, const 
     float s = 0.f;
 #pragma unroll
     for (int g = 0; g < 16; ++g) s += red[g * L + threadIdx.x];
-    slab[L * L + threadIdx.x] += s;
+    slab[L * L + threadIdx.x] = (init ? 0.f : slab[L * L + threadIdx.x]) + s;
   }
 }
 
@@ -253,7 +253,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     const pdg_ln_bwd* __restrict__ lbm_p, const pdg_ln_bwd* __restrict__ lbe_p, const float* __restrict__ lg,
     const float* __restrict__ W2T, float* __restrict__ gz1m, float* __restrict__ gz1e, float* __restrict__ gC,
     float* __restrict__ slabs, int E, const double* __restrict__ pm, int npm, const double* __restrict__ pe,
-    int npe) {
+    int npe, int slab_init) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   constexpr int NIMG = EU ? 4 : 2, NMSK = EU ? 2 : 1;
   constexpr int BUF = NIMG * IMG16 + NMSK * MSK16;           // one round's images + masks
@@ -377,7 +377,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     round(1, base + R16);
   }
   __syncthreads();   // the last rounds' image reads precede the LDS reuse below
-  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
 }
 
 // ============================================================================ Wc path
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
     const float* __restrict__ ge_next,
     const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs,
     const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, double* __restrict__ part, int E,
-    const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate) {
+    const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate, int slab_init) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img_c = sm;                                         // gC
   unsigned char* img_e = sm + EBW_IMG;                               // e
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
     }
   }
   __syncthreads();   // the last round's tile reads precede the LDS reuse below
-  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
   if (ln) {
     // block partial = the 16 row groups' column sums, reduced in order through LDS
     double* red = reinterpret_cast<double*>(sm + 2 * EBW_IMG);
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd_kernel(
     const float* __restrict__ w0, const float* __restrict__ b0, const pdg_ln_stat* __restrict__ st_p,
     const pdg_ln_bwd* __restrict__ lb_p, const double* __restrict__ pairs, int npairs,
     const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ slabs,
-    double* __restrict__ nsums, int E) {
+    double* __restrict__ nsums, int E, int slab_init) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img_g = sm;                                   // gz2
   unsigned char* img_a = sm + EBW_IMG;                         // a1
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd_kernel(
   };
   round(r0);
   for (int base = r0 + X6_ROWS; base < r1; base += X6_ROWS) round(base);
-  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
   // the 16 lanes holding the same features (different rows): fixed xor butterfly
 #pragma unroll
   for (int off = 1; off < 16; off <<= 1)
@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd2_kernel(
     const float* __restrict__ w0, const float* __restrict__ b0, const pdg_ln_stat* __restrict__ st_p,
     const pdg_ln_bwd* __restrict__ lb_p, const double* __restrict__ pairs, int npairs,
     const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ slabs,
-    double* __restrict__ nsums, int E) {
+    double* __restrict__ nsums, int E, int slab_init) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;    // the thread's staged row: rg (0..15)
@@ -1452,7 +1452,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd2_kernel(
     round(1, base + R16);
   }
   __syncthreads();   // the last rounds' image reads precede the LDS reuse below
-  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm));
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
 #pragma unroll
   for (int off = 1; off < 16; off <<= 1)
 #pragma unroll
@@ -1728,7 +1728,7 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
                                const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
                                const pdg_ln_bwd* lb_e, const float* ln_g, const float* W2T, float* gz1m,
                                float* gz1e, float* gC, float* slabs, int nslabs, const double* pairs_m, int npairs_m,
-                               const double* pairs_e, int npairs_e, void* stream) {
+                               const double* pairs_e, int npairs_e, int slab_init, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_w2: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_bwd_w2: bad slabs");
   PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_bwd_w2: the XCD-interleaved build needs 256 blocks");
@@ -1748,18 +1748,19 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
   if (eu)
     hipLaunchKernelGGL(edge_bwd_w2_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, s, dst, gaggr, ge_next, a2m,
                        a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, gz1m, gz1e, gC, slabs, n_edges, pairs_m,
-                       npairs_m, pairs_e, npairs_e);
+                       npairs_m, pairs_e, npairs_e, slab_init);
   else
     hipLaunchKernelGGL(edge_bwd_w2_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, s, dst, gaggr, ge_next, a2m,
                        a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, gz1m, gz1e, gC, slabs, n_edges, pairs_m,
-                       npairs_m, pairs_m, npairs_m);
+                       npairs_m, pairs_m, npairs_m, slab_init);
   PDG_CHECK_LAUNCH("pdg_edge_bwd_w2");
   return PDG_OK;
 }
 
 extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
                                 float* ge_out, float* slabs, int nslabs, const float* a2ln, const pdg_ln_stat* st_ln,
-                                double* ln_partials, const float* ln_g, double* pairs, int accumulate, void* stream) {
+                                double* ln_partials, const float* ln_g, double* pairs, int accumulate, int slab_init,
+                                void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_gout_wc: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_gout_wc: bad slabs");
   PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_gout_wc: the XCD-interleaved build needs 256 blocks");
@@ -1774,10 +1775,12 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
   const size_t shm = 2 * EBW_IMG + ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
   if (ge_next)
     hipLaunchKernelGGL(edge_gout_wc_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
+                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate,
+                       slab_init);
   else
     hipLaunchKernelGGL(edge_gout_wc_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate);
+                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate,
+                       slab_init);
   PDG_CHECK_LAUNCH("pdg_edge_gout_wc");
   return PDG_OK;
 }
@@ -1785,7 +1788,7 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
 extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, const float* e_in, const float* w0,
                                 const float* b0, const pdg_ln_stat* st, const pdg_ln_bwd* lb, const double* lb_pairs,
                                 int lb_npairs, const float* ln_g, const float* W2T, float* slabs, double* narrow_sums,
-                                int nslabs, void* stream) {
+                                int nslabs, int slab_init, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_enc_bwd: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs && narrow_sums, "pdg_edge_enc_bwd: bad slabs");
   PDG_CHECK_ARG(gy && a2 && e_in && w0 && b0 && st && (lb || lb_pairs) && ln_g && W2T,
@@ -1796,7 +1799,7 @@ extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, c
   const size_t shm = PDG_EEB_2DEEP ? 2 * EEB2_BUF : 2 * EBW_IMG + EBW_MASK + X6_ROWS * sizeof(float);
   hipLaunchKernelGGL(PDG_EEB_2DEEP ? edge_enc_bwd2_kernel : edge_enc_bwd_kernel, dim3(nslabs), dim3(EBW_THREADS), shm,
                      (hipStream_t)stream, gy, a2, e_in, w0, b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs,
-                     narrow_sums, n_edges);
+                     narrow_sums, n_edges, slab_init);
   PDG_CHECK_LAUNCH("pdg_edge_enc_bwd");
   return PDG_OK;
 }

@@ -49,7 +49,8 @@ constexpr int NF_U = 4;
 
 __global__ __launch_bounds__(1024) void nmse_fwd_kernel(const int* __restrict__ ptr, const float* __restrict__ gt,
                                                         const float* __restrict__ pred, float* __restrict__ loss,
-                                                        float* __restrict__ den_out) {
+                                                        float* __restrict__ den_out, const float* __restrict__ scale,
+                                                        int accumulate, float* __restrict__ gp) {
   __shared__ double red[6 * 16];
   const int g = blockIdx.x;
   const int n0 = ptr[g], n1 = ptr[g + 1];
@@ -103,13 +104,34 @@ __global__ __launch_bounds__(1024) void nmse_fwd_kernel(const int* __restrict__ 
     if (threadIdx.x == 0) den_out[g * 3 + c] = den;
   }
   if (threadIdx.x == 0) loss[g] = (ratio[0] + ratio[1] + ratio[2]) / 3.0f;
+  if (gp == nullptr) return;
+  // pdg_nmse_fwd_bwd: the graph's gradient rows with nmse_bwd_kernel's arithmetic (bitwise), den from the
+  // block's own sums
+  const float sc = scale[0];
+  for (int e = 3 * n0 + threadIdx.x; e < 3 * n1; e += T) {
+    const int c = e % 3;
+    const float den = (float)sd[3 + c];
+    const float d = gt[e] - pred[e];
+    const float v = sc * ((-2.0f * d) / den) / 3.0f;
+    gp[e] = accumulate ? gp[e] + v : v;
+  }
 }
 
 extern "C" int pdg_nmse_fwd(int n_graphs, const int* ptr, const float* gt, const float* pred, float* loss,
                             float* den, void* stream) {
   PDG_CHECK_ARG(n_graphs > 0, "pdg_nmse_fwd: n_graphs must be > 0");
-  hipLaunchKernelGGL(nmse_fwd_kernel, dim3(n_graphs), dim3(1024), 0, (hipStream_t)stream, ptr, gt, pred, loss, den);
+  hipLaunchKernelGGL(nmse_fwd_kernel, dim3(n_graphs), dim3(1024), 0, (hipStream_t)stream, ptr, gt, pred, loss, den,
+                     nullptr, 0, nullptr);
   PDG_CHECK_LAUNCH("pdg_nmse_fwd");
+  return PDG_OK;
+}
+
+extern "C" int pdg_nmse_fwd_bwd(int n_graphs, const int* ptr, const float* gt, const float* pred, float* loss,
+                                float* den, const float* scale, int accumulate, float* g_pred, void* stream) {
+  PDG_CHECK_ARG(n_graphs > 0 && scale && g_pred, "pdg_nmse_fwd_bwd: bad arguments");
+  hipLaunchKernelGGL(nmse_fwd_kernel, dim3(n_graphs), dim3(1024), 0, (hipStream_t)stream, ptr, gt, pred, loss, den,
+                     scale, accumulate, g_pred);
+  PDG_CHECK_LAUNCH("pdg_nmse_fwd_bwd");
   return PDG_OK;
 }
 

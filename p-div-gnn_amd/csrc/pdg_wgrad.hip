@@ -334,6 +334,194 @@ extern "C" int pdg_wgrad_narrow_finalize(const double* partials, int nparts, int
   return PDG_OK;
 }
 
+// ============================================================================ backward epilogue
+// Every end-of-backward reduction in one launch (pdg_bwd_epilogue): the deferred slab reductions
+// (pdg_wgrad_reduce_batch), the LayerNorm parameter gradients (pdg_ln_param_grads), up to two narrow
+// weight-gradient finalizes (pdg_wgrad_narrow_finalize) and the edge encoder's first-layer sums
+// (pdg_enc_narrow_reduce).  Blocks are dealt to the parts by index; each part's block does what the
+// separate kernel's block did, in the same order (bitwise the same gradients; the encoder sums use
+// 256 threads in place of 512 and add their rows in another fixed order).  Four launches fewer per step.
+constexpr int EPI_NARROW_MAX = 2;
+struct EpilogueJobs {
+  WgradReduceJobs wr;
+  int n_wr;
+  const double* ln_acc[4];
+  int ln_rows[4];
+  float* ln_g[4];
+  float* ln_b[4];
+  int n_ln;
+  const double* np[EPI_NARROW_MAX];
+  int np_n[EPI_NARROW_MAX], np_k[EPI_NARROW_MAX], np_t[EPI_NARROW_MAX];
+  float* np_W[EPI_NARROW_MAX];
+  float* np_bw[EPI_NARROW_MAX];
+  float* np_bn[EPI_NARROW_MAX];
+  int n_np;
+  const double* enc;   // edge encoder narrow sums (nslabs x 256), or NULL
+  int enc_n;
+  float* enc_w0;
+  float* enc_b0;
+};
+
+__global__ __launch_bounds__(256) void bwd_epilogue_kernel(EpilogueJobs J) {
+  __shared__ double dred[256];
+  __shared__ float fred[8][33];
+  int b = blockIdx.x;
+  constexpr int WR_X = (SLAB + 31) / 32;
+  if (b < J.n_wr * WR_X) {   // a slab reduction block (wgrad_reduce_batch_kernel)
+    const int j = b / WR_X, bx = b % WR_X;
+    const float* __restrict__ slabs = J.wr.slabs[j];
+    const int n = J.wr.nslabs[j];
+    const int el = threadIdx.x & 31, g = threadIdx.x >> 5;
+    const int e = bx * 32 + el;
+    float acc = 0.f;
+    if (e < SLAB) {
+      for (int b0 = g; b0 < n; b0 += 64) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = b0 + 8 * u < n ? slabs[(size_t)(b0 + 8 * u) * SLAB + e] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+      }
+    }
+    fred[g][el] = acc;
+    __syncthreads();
+    if (g == 0 && e < SLAB) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += fred[k][el];
+      if (e < L * L) {
+        const int o = e / L, i = e % L;
+        J.wr.gW[j][(size_t)o * J.wr.ld[j] + J.wr.col0[j] + i] += s;
+      } else if (J.wr.gb[j]) {
+        J.wr.gb[j][e - L * L] += s;
+      }
+    }
+    return;
+  }
+  b -= J.n_wr * WR_X;
+  if (b < J.n_ln * 256) {   // a LayerNorm parameter column (ln_param_grads_kernel)
+    const int grp = b / 256, col = b % 256;
+    double s = 0;
+    for (int r = threadIdx.x; r < J.ln_rows[grp]; r += blockDim.x) s += J.ln_acc[grp][(size_t)r * 256 + col];
+    dred[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = blockDim.x >> 1; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) dred[threadIdx.x] += dred[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      float* g = col < 128 ? J.ln_b[grp] : J.ln_g[grp];
+      if (g) g[col & 127] += (float)dred[0];
+    }
+    return;
+  }
+  b -= J.n_ln * 256;
+  for (int q = 0; q < J.n_np; ++q) {   // a narrow weight-gradient element (wgrad_narrow_finalize_kernel)
+    const int K = J.np_k[q], tot = L * K + L + K;
+    if (b >= tot) {
+      b -= tot;
+      continue;
+    }
+    double s = 0;
+    for (int r = threadIdx.x; r < J.np_n[q]; r += blockDim.x) s += J.np[q][(size_t)r * tot + b];
+    dred[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = blockDim.x >> 1; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) dred[threadIdx.x] += dred[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    s = dred[0];
+    if (b < L * K) {
+      const int c = b / K, i = b % K;
+      if (J.np_t[q]) J.np_W[q][i * L + c] += (float)s;
+      else J.np_W[q][c * K + i] += (float)s;
+    } else if (b < L * K + L) {
+      if (J.np_bw[q]) J.np_bw[q][b - L * K] += (float)s;
+    } else {
+      if (J.np_bn[q]) J.np_bn[q][b - L * K - L] += (float)s;
+    }
+    return;
+  }
+  if (J.enc && b < 2) {   // the edge encoder's w0 (b = 0) / b0 (b = 1) sums (enc_narrow_reduce_kernel's job)
+    const int col = threadIdx.x & (L - 1), grp = threadIdx.x >> 7, e = L * b + col;
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    int r = grp;
+    for (; r + 6 < J.enc_n; r += 8) {
+      s0 += J.enc[(size_t)r * 2 * L + e];
+      s1 += J.enc[(size_t)(r + 2) * 2 * L + e];
+      s2 += J.enc[(size_t)(r + 4) * 2 * L + e];
+      s3 += J.enc[(size_t)(r + 6) * 2 * L + e];
+    }
+    for (; r < J.enc_n; r += 2) s0 += J.enc[(size_t)r * 2 * L + e];
+    dred[threadIdx.x] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (grp == 0) {
+      const double t = dred[col] + dred[L + col];
+      if (b == 0) J.enc_w0[col] += (float)t;
+      else J.enc_b0[col] += (float)t;
+    }
+  }
+}
+
+extern "C" int pdg_bwd_epilogue(int n_reduce, const float* const* slabs, const int* nslabs, float* const* grad_W,
+                                const int* ld, const int* col0, float* const* grad_b, int n_ln, const double* const* ln_acc,
+                                const int* ln_rows, float* const* ln_grad_g, float* const* ln_grad_b, int n_narrow,
+                                const double* const* narrow_partials, const int* narrow_nparts, const int* narrow_k,
+                                const int* narrow_transpose, float* const* narrow_gW, float* const* narrow_gb_wide,
+                                float* const* narrow_gb_narrow, const double* enc_sums, int enc_nslabs,
+                                float* enc_grad_w0, float* enc_grad_b0, void* stream) {
+  PDG_CHECK_ARG(n_reduce >= 0 && n_reduce <= WRB_MAX && n_ln >= 0 && n_ln <= 4 && n_narrow >= 0 &&
+                    n_narrow <= EPI_NARROW_MAX,
+                "pdg_bwd_epilogue: bad job counts");
+  EpilogueJobs J{};
+  J.n_wr = n_reduce;
+  for (int i = 0; i < n_reduce; ++i) {
+    PDG_CHECK_ARG(slabs[i] && grad_W[i] && nslabs[i] > 0 && nslabs[i] <= MAX_BLOCKS && ld[i] >= L &&
+                      col0[i] >= 0 && col0[i] + L <= ld[i],
+                  "pdg_bwd_epilogue: bad reduction job %d", i);
+    J.wr.slabs[i] = slabs[i];
+    J.wr.gW[i] = grad_W[i];
+    J.wr.gb[i] = grad_b[i];
+    J.wr.nslabs[i] = nslabs[i];
+    J.wr.ld[i] = ld[i];
+    J.wr.col0[i] = col0[i];
+  }
+  J.n_ln = n_ln;
+  for (int i = 0; i < n_ln; ++i) {
+    PDG_CHECK_ARG(ln_acc[i] && ln_rows[i] > 0 && ln_rows[i] <= MAX_BLOCKS, "pdg_bwd_epilogue: bad LayerNorm group %d", i);
+    J.ln_acc[i] = ln_acc[i];
+    J.ln_rows[i] = ln_rows[i];
+    J.ln_g[i] = ln_grad_g[i];
+    J.ln_b[i] = ln_grad_b[i];
+  }
+  J.n_np = n_narrow;
+  long nb = (long)n_reduce * ((SLAB + 31) / 32) + (long)n_ln * 256;
+  for (int i = 0; i < n_narrow; ++i) {
+    PDG_CHECK_ARG(narrow_partials[i] && narrow_nparts[i] > 0 && narrow_nparts[i] <= MAX_BLOCKS && narrow_gW[i] &&
+                      (narrow_k[i] == 1 || narrow_k[i] == 3 || narrow_k[i] == 6),
+                  "pdg_bwd_epilogue: bad narrow job %d", i);
+    J.np[i] = narrow_partials[i];
+    J.np_n[i] = narrow_nparts[i];
+    J.np_k[i] = narrow_k[i];
+    J.np_t[i] = narrow_transpose[i];
+    J.np_W[i] = narrow_gW[i];
+    J.np_bw[i] = narrow_gb_wide[i];
+    J.np_bn[i] = narrow_gb_narrow[i];
+    nb += L * narrow_k[i] + L + narrow_k[i];
+  }
+  PDG_CHECK_ARG(!enc_sums || (enc_nslabs > 0 && enc_grad_w0 && enc_grad_b0), "pdg_bwd_epilogue: bad encoder sums");
+  J.enc = enc_sums;
+  J.enc_n = enc_nslabs;
+  J.enc_w0 = enc_grad_w0;
+  J.enc_b0 = enc_grad_b0;
+  if (enc_sums) nb += 2;
+  if (nb == 0) return PDG_OK;
+  hipLaunchKernelGGL(bwd_epilogue_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, J);
+  PDG_CHECK_LAUNCH("pdg_bwd_epilogue");
+  return PDG_OK;
+}
+
 // ============================================================================ segmented, LDS-staged wgrad
 // One launch per weight and backward: the row segments of every message-passing
 // step (and both edge_net evaluations) form one virtual K = sum(rows) reduction.

@@ -184,6 +184,10 @@ class EPDEngine:
         self._ln_acc = torch.zeros(4, self._acc_rows * 256, **f64)
         self._sync_pairs = torch.zeros(8, 2, **f64)
         self._part_narrow = torch.empty(self.max_blocks * (L * 6 + L + 6), **f64)
+        # block partials of the two narrow gradients formed inside the encoder / decoder backward, held until
+        # the backward's epilogue (apart from _part_narrow, the scratch of pdg_wgrad_narrow)
+        self._part_narrow_d = torch.empty(self.max_blocks * (L * 3 + L + 3), **f64)
+        self._part_narrow_ne = torch.empty(self.max_blocks * (L * 6 + L + 6), **f64)
         self._nparts = ctypes.c_int(0)
         # one weight-gradient slab per block of pdg_wgrad_segments: three blocks per CU
         self._nslabs = lib.pdg_wgrad_slabs_per_cu() * torch.cuda.get_device_properties(self.device).multi_processor_count
@@ -456,17 +460,20 @@ class EPDEngine:
         # per-block rows into the group accumulator and writes per-block (S1, S2) pairs; the consumer
         # kernel reduces the pairs (include/pdivgnn.h, pdg_ln_colsum)
         if fused:
-            # one zero fill per backward for the three fused weight-gradient slab sets (W2, Wc, the edge
-            # encoder's W2) and the LayerNorm column-sum accumulators: four fill launches became one
+            # the three fused weight-gradient slab sets (W2, Wc, the edge encoder's W2) are written by the
+            # first call of the backward (slab_init) and need no fill; the LayerNorm column-sum
+            # accumulators are zeroed (one fill launch)
             nse = self._nslabs_e
-            nsl, nacc = nse * (L * L + L), self._ln_acc.numel()
-            zb = torch.zeros(3 * nsl + 2 * nacc, dtype=torch.float32, device=self.device)
-            slabs_w2, slabs_wc, slabs_ee = (zb[i * nsl:(i + 1) * nsl].view(nse, L * L + L) for i in range(3))
-            acc = zb[3 * nsl:].view(torch.float64).view(self._ln_acc.shape)
+            # (an edgeless batch runs no edge kernel: zeros, so the edge weights get zero gradients)
+            sl = (torch.empty if E else torch.zeros)(3, nse, L * L + L, dtype=torch.float32, device=self.device)
+            slabs_w2, slabs_wc, slabs_ee = sl[0], sl[1], sl[2]
+            acc = torch.zeros(self._ln_acc.shape, dtype=torch.float64, device=self.device)
         else:
             acc = self._ln_acc
             acc.zero_()
-        reds = []   # deferred slab reductions (one pdg_wgrad_reduce_batch launch at the end)
+        reds = []   # deferred slab reductions (in the one pdg_bwd_epilogue launch at the end)
+        epi_narrow = []   # narrow weight-gradient finalizes for pdg_bwd_epilogue
+        epi_enc = None    # the edge encoder's first-layer sums for pdg_bwd_epilogue
         ACC_N, ACC_E, ACC_NE, ACC_EE = (acc[i] for i in range(4))
         S = ctx.steps
         pairs = torch.empty(3 * S + 2, self.max_blocks * 2, dtype=torch.float64, device=self.device)
@@ -504,10 +511,10 @@ class EPDEngine:
             # + node_decoder.2's weight / bias gradient from the same a1d / gy rows (block partials)
             self._t("decoder_bwd", lib.pdg_decoder_bwd_coop, N, _p(gy), _p(ctx.a1d), _p(P["node_decoder.2.weight"]),
                     _p(T["Wd1T"]), _p(gz1d), _p(gx), _p(dl["a2n"]), st[dl["i_n"]], _p(ACC_N), _p(g_node),
-                    _p(PN(S - 1)), 1, _p(self._part_narrow), self._nslabs_e, s)
+                    _p(PN(S - 1)), 1, _p(self._part_narrow_d), self._nslabs_e, s)
             self._nparts.value = self._nslabs_e
-            lib.pdg_wgrad_narrow_finalize(_p(self._part_narrow), self._nslabs_e, 3, 1, _p(G["node_decoder.2.weight"]),
-                                          None, _p(G["node_decoder.2.bias"]), s)
+            epi_narrow.append((self._part_narrow_d, self._nslabs_e, 3, 1, G["node_decoder.2.weight"], None,
+                               G["node_decoder.2.bias"]))
         else:
             lib.pdg_decoder_bwd(N, _p(gy), _p(ctx.a1d), _p(P["node_decoder.2.weight"]), _p(T["Wd1T"]), _p(gz1d),
                                 _p(gx), s)
@@ -565,7 +572,7 @@ class EPDEngine:
                     self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
-                            _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, s)
+                            _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, int(t == S - 1), s)
                 if fused:
                     # + the column sums / pairs of the LayerNorm that produced e_t (LN_e of step t-1, or the
                     # edge encoder's)
@@ -575,7 +582,7 @@ class EPDEngine:
                     else:
                         a2ln, st_ln, accb, gl, pp = ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"], P_EENC
                     tail = (_p(d["e"]), _p(ge_next), _p(T["WcT"]), _p(ge_out), _p(slabs_wc), nse, _p(a2ln), st_ln,
-                            _p(accb), _p(gl), _p(pp), 1, s)
+                            _p(accb), _p(gl), _p(pp), 1, int(t == S - 1), s)
                     gout_fn, gout_args = lib.pdg_edge_gout_wc, (E, _p(gC)) + tail
                     if not self.pq_first:
                         self._t("edge_gout", gout_fn, *gout_args)
@@ -624,9 +631,9 @@ class EPDEngine:
             # weight / bias gradient from gz1 and the encoder input (block partials; gz1 is not stored)
             self._t("node_enc_bwd", lib.pdg_mlp2_bwd_coop, N, _p(gx_next), _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], None,
                     _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), None, pn, nn, _p(ctx.x_in),
-                    _p(self._part_narrow), self._nslabs_e, s)
-            lib.pdg_wgrad_narrow_finalize(_p(self._part_narrow), self._nslabs_e, 6, 0, _p(G["node_encoder.0.weight"]),
-                                          _p(G["node_encoder.0.bias"]), None, s)
+                    _p(self._part_narrow_ne), self._nslabs_e, s)
+            epi_narrow.append((self._part_narrow_ne, self._nslabs_e, 6, 0, G["node_encoder.0.weight"],
+                               G["node_encoder.0.bias"], None))
         else:
             lib.pdg_mlp2_bwd(N, _p(gx_next), None, _p(ctx.a2_ne), _p(ctx.a1_ne), st[0], None,
                              _p(P["node_encoder.4.weight"]), _p(T["Wne2T"]), _p(gz2), _p(gz1), pn, nn, s)
@@ -640,10 +647,9 @@ class EPDEngine:
                 nsum = torch.empty(nse, 2 * L, dtype=torch.float64, device=self.device)
                 self._t("edge_enc_bwd", lib.pdg_edge_enc_bwd, E, _p(ge_next), _p(ctx.a2_ee), _p(ctx.e_in),
                         _p(P["edge_encoder.0.weight"]), _p(P["edge_encoder.0.bias"]), st[1], None, pe, ne,
-                        _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(slabs_ee), _p(nsum), nse, s)
+                        _p(P["edge_encoder.4.weight"]), _p(T["Wee2T"]), _p(slabs_ee), _p(nsum), nse, 1, s)
                 reds.append((slabs_ee, nse, G["edge_encoder.2.weight"], L, 0, G["edge_encoder.2.bias"]))
-                lib.pdg_enc_narrow_reduce(_p(nsum), nse, _p(G["edge_encoder.0.weight"]),
-                                          _p(G["edge_encoder.0.bias"]), s)
+                epi_enc = (nsum, nse, G["edge_encoder.0.weight"], G["edge_encoder.0.bias"])
             else:
                 gz2e_, gz1e_ = self._empty(E, L), self._empty(E, L)
                 lib.pdg_mlp2_bwd(E, _p(ge_next), None, _p(ctx.a2_ee), _p(ctx.a1_ee), st[1], None,
@@ -651,12 +657,6 @@ class EPDEngine:
                 segs["ee2"].append((gz2e_, ctx.a1_ee, E))
                 lib.pdg_wgrad_narrow(E, _p(gz1e_), _p(ctx.e_in), 1, 0, _p(self._part_narrow),
                                      _p(G["edge_encoder.0.weight"]), _p(G["edge_encoder.0.bias"]), None, s)
-        # LayerNorm weight / bias gradients: one launch over the four accumulators
-        names = ("processor.node_net.4", "processor.edge_net.4", "node_encoder.4", "edge_encoder.4")
-        lib.pdg_ln_param_grads(4, (ctypes.c_void_p * 4)(*[_p(acc[i]) for i in range(4)]),
-                               (ctypes.c_int * 4)(*([self._acc_rows] * 4)),
-                               (ctypes.c_void_p * 4)(*[_p(G[n + ".weight"]) for n in names]),
-                               (ctypes.c_void_p * 4)(*[_p(G[n + ".bias"]) for n in names]), s)
         # deferred weight gradients: one segmented pass + slab reduction per shared weight block
         red = [
             ("W2", "processor.edge_net.2.weight", L, 0, "processor.edge_net.2.bias"),
@@ -745,11 +745,29 @@ class EPDEngine:
             reds.append((slabs_w2, nse, G["processor.edge_net.2.weight"], L, 0, G["processor.edge_net.2.bias"]))
             reds.append((slabs_wc, nse, G["processor.edge_net.0.weight"], 3 * L, 2 * L,
                          G["processor.edge_net.0.bias"]))
-        # every deferred slab reduction in one launch
-        for c0 in range(0, len(reds), 16):
+        # every end-of-backward reduction in one launch (pdg_bwd_epilogue): the deferred slab reductions,
+        # the LayerNorm weight / bias gradients of the four accumulator groups, the narrow weight gradients
+        # and the edge encoder's first layer (more than 16 slab sets: the rest in pdg_wgrad_reduce_batch)
+        VP, IA = ctypes.c_void_p, ctypes.c_int
+        for c0 in range(16, len(reds), 16):
             jb = reds[c0:c0 + 16]
             n = len(jb)
-            VP, IA = ctypes.c_void_p * n, ctypes.c_int * n
-            lib.pdg_wgrad_reduce_batch(n, VP(*[_p(j[0]) for j in jb]), IA(*[j[1] for j in jb]),
-                                       VP(*[_p(j[2]) for j in jb]), IA(*[j[3] for j in jb]),
-                                       IA(*[j[4] for j in jb]), VP(*[_p(j[5]) for j in jb]), s)
+            lib.pdg_wgrad_reduce_batch(n, (VP * n)(*[_p(j[0]) for j in jb]), (IA * n)(*[j[1] for j in jb]),
+                                       (VP * n)(*[_p(j[2]) for j in jb]), (IA * n)(*[j[3] for j in jb]),
+                                       (IA * n)(*[j[4] for j in jb]), (VP * n)(*[_p(j[5]) for j in jb]), s)
+        jb = reds[:16]
+        n = len(jb)
+        names = ("processor.node_net.4", "processor.edge_net.4", "node_encoder.4", "edge_encoder.4")
+        m = len(epi_narrow)
+        lib.pdg_bwd_epilogue(n, (VP * n)(*[_p(j[0]) for j in jb]), (IA * n)(*[j[1] for j in jb]),
+                             (VP * n)(*[_p(j[2]) for j in jb]), (IA * n)(*[j[3] for j in jb]),
+                             (IA * n)(*[j[4] for j in jb]), (VP * n)(*[_p(j[5]) for j in jb]),
+                             4, (VP * 4)(*[_p(acc[i]) for i in range(4)]), (IA * 4)(*([self._acc_rows] * 4)),
+                             (VP * 4)(*[_p(G[k + ".weight"]) for k in names]),
+                             (VP * 4)(*[_p(G[k + ".bias"]) for k in names]),
+                             m, (VP * m)(*[_p(j[0]) for j in epi_narrow]), (IA * m)(*[j[1] for j in epi_narrow]),
+                             (IA * m)(*[j[2] for j in epi_narrow]), (IA * m)(*[j[3] for j in epi_narrow]),
+                             (VP * m)(*[_p(j[4]) for j in epi_narrow]), (VP * m)(*[_p(j[5]) for j in epi_narrow]),
+                             (VP * m)(*[_p(j[6]) for j in epi_narrow]),
+                             _p(epi_enc[0]) if epi_enc else None, epi_enc[1] if epi_enc else 0,
+                             _p(epi_enc[2]) if epi_enc else None, _p(epi_enc[3]) if epi_enc else None, s)

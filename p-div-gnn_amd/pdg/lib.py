@@ -83,19 +83,21 @@ SIGNATURES: dict[str, list] = {
     "pdg_mlp2_bwd_coop": [I] + [P] * 10 + [I, P, P, I, P],
     "pdg_decoder_bwd_coop": [I] + [P] * 11 + [I, P, I, P],
     "pdg_wgrad_narrow_finalize": [P, I, I, I, P, P, P, P],
+    "pdg_bwd_epilogue": [I, P, P, P, P, P, P, I, P, P, P, P, I, P, P, P, P, P, P, P, P, I, P, P, P],
     "pdg_segsum_finish": [I, P, P, P, P, P, P, P, P],
     "pdg_wgrad_slabs_per_cu": [],
     "pdg_wgrad_pairs": [I, P, P, P, P, I, P, P, I, P],
-    "pdg_edge_enc_bwd": [I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P],
+    "pdg_edge_enc_bwd": [I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, I, P],
     "pdg_enc_narrow_reduce": [P, I, P, P, P],
-    "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P, I, P],
-    "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P, P, I, P],
+    "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P, I, I, P],
+    "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P, P, I, I, P],
     "pdg_mesh_graph": [I, P, I, I, P, I, P, P, P, ctypes.c_long, P, P, ctypes.c_long, P],
     "pdg_mesh_graph_scratch_bytes": [I, I],
     "pdg_wgrad_segments": [I, P, P, P, P, I, P],
     "pdg_wgrad_narrow": [I, P, P, I, I, P, P, P, P, P],
     "pdg_nmse_fwd": [I, P, P, P, P, P, P],
     "pdg_nmse_bwd": [I, P, I, P, P, P, P, I, P, P],
+    "pdg_nmse_fwd_bwd": [I, P, P, P, P, P, P, I, P, P],
     "pdg_div_fwd": [I, P, P, P, P, P, P, I, P, P, P],
     "pdg_div_bwd": [I, P, I, P, P, P, P, P, P, I, I, P, P],
     "pdg_transpose": [I, I, I, P, P, P],

@@ -232,11 +232,11 @@ class Trainer:
                                      m.message_passing_steps, True, False, True)
         gt = self._gt(batch)
         loss_g, den = torch.empty(B, **f32), torch.empty(B, 3, **f32)
-        lib.pdg_nmse_fwd(B, plan.ptr.data_ptr(), gt.data_ptr(), y.data_ptr(), loss_g.data_ptr(), den.data_ptr(), s)
         scale = self._const(1.0 / Bn)
         gy = torch.empty(N, 3, **f32)
-        lib.pdg_nmse_bwd(B, plan.ptr.data_ptr(), N, gt.data_ptr(), y.data_ptr(), den.data_ptr(), scale.data_ptr(), 0,
-                         gy.data_ptr(), s)
+        # per-graph NMSE and its gradient in one launch (pdg_nmse_fwd_bwd, bitwise pdg_nmse_fwd + pdg_nmse_bwd)
+        lib.pdg_nmse_fwd_bwd(B, plan.ptr.data_ptr(), gt.data_ptr(), y.data_ptr(), loss_g.data_ptr(), den.data_ptr(),
+                             scale.data_ptr(), 0, gy.data_ptr(), s)
         # per-graph losses; _update reduces them (pdg_loss_reduce: sum / B_global [x penalty])
         out = {"B": B, "Bn": Bn, "loss_g": loss_g}
         if self.divergence:

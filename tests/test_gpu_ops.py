@@ -596,8 +596,9 @@ def test_decoder_fwd_fin_equals_finalize_then_decoder(env, N, nparts, scale):
         assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("slab_init", [0, 1])
 @pytest.mark.parametrize("E", [77, 5000])
-def test_edge_enc_bwd_vs_autograd(env, E):
+def test_edge_enc_bwd_vs_autograd(env, E, slab_init):
     """pdg_edge_enc_bwd (edge encoder backward in one pass, layer-1 output recomputed from the scalar
     input) against torch autograd of Lin(1->128) ReLU Lin(128->128) ReLU LN in fp64: all four
     weight / bias gradients; the encoder forward is run with a1 == NULL (not stored)."""
@@ -620,12 +621,13 @@ def test_edge_enc_bwd_vs_autograd(env, E):
     lib.pdg_ln_colsum(E, gy.data_ptr(), None, a2.data_ptr(), st.data_ptr(), acc.data_ptr(), ctypes.byref(n),
                       g.data_ptr(), pairs.data_ptr(), 1, s)
     ns = 37
-    slabs = torch.zeros(ns, L * L + L, device="cuda")
+    # slab_init: the slabs are written, not accumulated (their NaN contents must not leak)
+    slabs = torch.full((ns, L * L + L), float("nan"), device="cuda") if slab_init else torch.zeros(ns, L * L + L, device="cuda")
     nsum = torch.empty(ns, 2 * L, dtype=torch.float64, device="cuda")
     WT = W2.T.contiguous()
     lib.pdg_edge_enc_bwd(E, gy.data_ptr(), a2.data_ptr(), e_in.data_ptr(), W0.data_ptr(), b0.data_ptr(),
                          st.data_ptr(), None, pairs.data_ptr(), n.value, g.data_ptr(), WT.data_ptr(),
-                         slabs.data_ptr(), nsum.data_ptr(), ns, s)
+                         slabs.data_ptr(), nsum.data_ptr(), ns, slab_init, s)
     gW2, gb2 = torch.zeros(L, L, device="cuda"), torch.zeros(L, device="cuda")
     gW0, gb0 = torch.zeros(L, 1, device="cuda"), torch.zeros(L, device="cuda")
     lib.pdg_wgrad_reduce(slabs.data_ptr(), ns, gW2.data_ptr(), L, 0, gb2.data_ptr(), s)
@@ -1109,3 +1111,78 @@ def test_fence_free_timing_events_agree_with_torch_events(env):
     assert ours > 0 and ref > 0
     assert ours <= ref * 1.02 + 0.05, (ours, ref)
     assert abs(ours - ref) / ref < 0.1, (ours, ref)
+
+
+def test_bwd_epilogue_matches_separate_launches(env):
+    """pdg_bwd_epilogue (every end-of-backward reduction in one launch) against pdg_wgrad_reduce_batch +
+    pdg_ln_param_grads + pdg_wgrad_narrow_finalize x2 + pdg_enc_narrow_reduce on the same partials: the
+    slab, LayerNorm and narrow gradients bitwise (the same per-block order), the edge encoder's first
+    layer to fp64 rounding (its rows are added in another order); gradients accumulate (+=)."""
+    lib, sh, _ = env
+    s = sh()
+    VP, IA = ctypes.c_void_p, ctypes.c_int
+    f64 = dict(dtype=torch.float64, device="cuda")
+    nj, ns = 3, 37
+    slabs = [torch.randn(ns, L * L + L, device="cuda") for _ in range(nj)]
+    ld, col0 = [L, 3 * L, 3 * L], [0, 2 * L, 0]
+    acc = [torch.randn(51 * 256, **f64) for _ in range(4)]
+    rows = [51, 40, 51, 13]
+    npart = [torch.randn(29 * (3 * L + L + 3), **f64), torch.randn(17 * (6 * L + L + 6), **f64)]
+    nk = [(29, 3, 1), (17, 6, 0)]
+    enc = torch.randn(ns, 2 * L, **f64)
+
+    def grads():
+        return {"W": [torch.full((L, w), 0.25, device="cuda") for w in ld], "b": [torch.full((L,), -0.5, device="cuda") if j != 2 else None for j in range(nj)],
+                "lg": [torch.full((L,), 1.0, device="cuda") for _ in range(4)], "lb": [torch.full((L,), 2.0, device="cuda") for _ in range(4)],
+                "nW": [torch.full((3, L), 0.5, device="cuda"), torch.full((L, 6), 0.5, device="cuda")],
+                "nbw": [None, torch.full((L,), 0.1, device="cuda")], "nbn": [torch.full((3,), 0.2, device="cuda"), None],
+                "w0": torch.full((L,), 0.3, device="cuda"), "b0": torch.full((L,), 0.4, device="cuda")}
+
+    a, b = grads(), grads()
+    p = lambda t: None if t is None else t.data_ptr()
+    assert lib.pdg_wgrad_reduce_batch(nj, (VP * nj)(*[p(x) for x in slabs]), (IA * nj)(*[ns] * nj),
+                                      (VP * nj)(*[p(x) for x in a["W"]]), (IA * nj)(*ld), (IA * nj)(*col0),
+                                      (VP * nj)(*[p(x) for x in a["b"]]), s) == 0
+    assert lib.pdg_ln_param_grads(4, (VP * 4)(*[p(x) for x in acc]), (IA * 4)(*rows), (VP * 4)(*[p(x) for x in a["lg"]]),
+                                  (VP * 4)(*[p(x) for x in a["lb"]]), s) == 0
+    for q in range(2):
+        assert lib.pdg_wgrad_narrow_finalize(p(npart[q]), nk[q][0], nk[q][1], nk[q][2], p(a["nW"][q]), p(a["nbw"][q]),
+                                             p(a["nbn"][q]), s) == 0
+    assert lib.pdg_enc_narrow_reduce(p(enc), ns, p(a["w0"]), p(a["b0"]), s) == 0
+    assert lib.pdg_bwd_epilogue(nj, (VP * nj)(*[p(x) for x in slabs]), (IA * nj)(*[ns] * nj),
+                                (VP * nj)(*[p(x) for x in b["W"]]), (IA * nj)(*ld), (IA * nj)(*col0),
+                                (VP * nj)(*[p(x) for x in b["b"]]), 4, (VP * 4)(*[p(x) for x in acc]), (IA * 4)(*rows),
+                                (VP * 4)(*[p(x) for x in b["lg"]]), (VP * 4)(*[p(x) for x in b["lb"]]), 2,
+                                (VP * 2)(*[p(x) for x in npart]), (IA * 2)(*[t[0] for t in nk]),
+                                (IA * 2)(*[t[1] for t in nk]), (IA * 2)(*[t[2] for t in nk]),
+                                (VP * 2)(*[p(x) for x in b["nW"]]), (VP * 2)(*[p(x) for x in b["nbw"]]),
+                                (VP * 2)(*[p(x) for x in b["nbn"]]), p(enc), ns, p(b["w0"]), p(b["b0"]), s) == 0
+    torch.cuda.synchronize()
+    for k in ("W", "b", "lg", "lb", "nW", "nbw", "nbn"):
+        for x, y in zip(a[k], b[k]):
+            assert (x is None and y is None) or torch.equal(x, y), k
+    for k in ("w0", "b0"):
+        assert rel(b[k], a[k]) < 1e-6, k
+    assert not torch.equal(a["W"][0], torch.full((L, L), 0.25, device="cuda"))   # something was added
+
+
+@pytest.mark.parametrize("sizes,accumulate", [((5041,) * 8, 0), ((17, 2, 3000, 250), 1)])
+def test_nmse_fwd_bwd_equals_fwd_then_bwd(env, sizes, accumulate):
+    """pdg_nmse_fwd_bwd (per-graph NMSE and its gradient in one launch) is bitwise pdg_nmse_fwd + pdg_nmse_bwd:
+    losses, denominators and the gradient (written or accumulated); ragged graphs."""
+    lib, sh, _ = env
+    s = sh()
+    B, N = len(sizes), sum(sizes)
+    ptr = torch.tensor([0] + list(torch.tensor(sizes).cumsum(0)), dtype=torch.int32, device="cuda")
+    gt, pred = rnd(N, 3), rnd(N, 3)
+    scale = torch.tensor([0.125], device="cuda")
+    base = rnd(N, 3)
+    l0, d0, g0 = torch.empty(B, device="cuda"), torch.empty(B, 3, device="cuda"), base.clone()
+    assert lib.pdg_nmse_fwd(B, ptr.data_ptr(), gt.data_ptr(), pred.data_ptr(), l0.data_ptr(), d0.data_ptr(), s) == 0
+    assert lib.pdg_nmse_bwd(B, ptr.data_ptr(), N, gt.data_ptr(), pred.data_ptr(), d0.data_ptr(), scale.data_ptr(),
+                            accumulate, g0.data_ptr(), s) == 0
+    l1, d1, g1 = torch.empty(B, device="cuda"), torch.empty(B, 3, device="cuda"), base.clone()
+    assert lib.pdg_nmse_fwd_bwd(B, ptr.data_ptr(), gt.data_ptr(), pred.data_ptr(), l1.data_ptr(), d1.data_ptr(),
+                                scale.data_ptr(), accumulate, g1.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(l0, l1) and torch.equal(d0, d1) and torch.equal(g0, g1)

@@ -51,7 +51,7 @@ def main(a, b, E=60001, N=10007):
             rc = dll.pdg_edge_bwd_w2(E, P(dst), P(gaggr), P(ge) if eu else None, P(a2m), P(a1m), P(a2e), P(a1e),
                                      P(st), P(st) + LN_STAT_BYTES, P(lb), P(lb) + LN_BWD_BYTES, P(g), P(W2T),
                                      P(res["gz1m"]), P(res["gz1e"]), P(res["gC"]), P(slabs), cus, None, 0, None, 0,
-                                     stream_handle(dev))
+                                     0, stream_handle(dev))
             assert rc == 0, rc
             torch.cuda.synchronize()
             out[(name, eu)] = {k: v.clone() for k, v in res.items()} | {"slabs": slabs.clone()}
