@@ -46,12 +46,13 @@ if [ "$WHAT" = measure ]; then
   grep '^{' "$O/prof.log" | tail -1 > "$O/prof_bench_line.json"
   rm -f "$O"/prof/*kernel_trace.csv "$O"/*/*.db
   cp "$O/pmc_traffic.json" "$R/profiles/${ROUND:-r04}_pmc_traffic.json"
-  step bench 500 python bench.py || exit 1
-  grep '^{' "$O/bench.log" | tail -1 > "$O/bench_line.json"
-  # SQ counters of the same tree (MFMA busy, wave-cycle split), two passes with kernel traces
+  # SQ counters of the same tree (MFMA busy, wave-cycle split), two passes with kernel traces, before the
+  # bench line so that it carries the counter MFMA busy beside its flop-derived frac_mfma
   bash tools/sq_pass.sh "$TAG/sq" > "$O/sq_pass.log" 2>&1 || { tail -5 "$O/sq_pass.log"; exit 1; }
   cp "$R/gpurun_out/$TAG/sq/sq.txt" "$R/profiles/${ROUND:-r04}_sq.txt"
   cp "$R/gpurun_out/$TAG/sq/sq.json" "$R/profiles/${ROUND:-r04}_sq.json"
+  step bench 500 python bench.py || exit 1
+  grep '^{' "$O/bench.log" | tail -1 > "$O/bench_line.json"
   python -c "import json; d = json.load(open('$O/bench_line.json')); print(d['value'], d['ms_per_step'], d['tree'], d['traffic_tree_match'], d['roofline'])"
 fi
 echo "all done"
