@@ -330,7 +330,9 @@ int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* g
  *                     so the slabs need no zero fill; the same for pdg_edge_gout_wc and
  *                     pdg_edge_enc_bwd); gz2m/gz2e are not
  *                     materialised.  ge_next == NULL: message branch only, gC = gz1m (gC may
- *                     then be the gz1m pointer itself: written once).
+ *                     then be the gz1m pointer itself: written once).  gz1e may be NULL with
+ *                     the edge update: it is then not stored (pdg_pq_scatter_bwd with
+ *                     e_is_sum forms it from gC - gz1m).
  *   pdg_edge_gout_wc: ge_out = [ge_next +] WcT gC; slabs += gC^T e and the b1 column sums.
  *                     a2ln != NULL: also the column sums of the backward of the LayerNorm that
  *                     produced e (input a2ln, statistics st_ln, upstream gradient ge_out), as
@@ -376,9 +378,10 @@ int pdg_mesh_graph(int n_nodes, const float* points, int dim, int n_faces, const
 /* Backward of the P/Q gathers: gP[v] = sum_{dst-seg(v)} gz1m + sum_{src-seg(v)} gz1e,
  * gQ[v] = sum_{src-seg(v)} gz1m + sum_{dst-seg(v)} gz1e.  src-seg uses rowptr_src and
  * perm_src (positions of the dst-sorted edges grouped by src).  gz1e may be NULL (no
- * edge-update branch). */
+ * edge-update branch).  e_is_sum != 0: the gz1e argument holds gC = gz1m + gz1e instead and
+ * each row's gz1e is formed as gC - gz1m in fp32 (the edge backward then stores no gz1e). */
 int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int* rowptr_src,
-                       const int* perm_src, const float* gz1m, const float* gz1e,
+                       const int* perm_src, const float* gz1m, const float* gz1e, int e_is_sum,
                        float* gP, float* gQ, void* stream);
 
 /* Weight gradient of a 128x128 Linear: per-block partial of sum_k G[k]^T X[k] (+ a second

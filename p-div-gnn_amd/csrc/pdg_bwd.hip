@@ -633,6 +633,10 @@ constexpr int PQ_U = 8;   // rows of each half in flight per node (6: 3 % slower
 // 288 MB), 67.7 -> 62.2 us.  Loads past a segment's end re-read row / entry 0 and are not
 // accumulated, so every sum is formed row by row in segment order (destination rows, then source
 // rows) as a serial loop would.
+// SUMC: the second array holds gC = gz1m + gz1e (what pdg_edge_bwd_w2 writes for the Wc pass) and each
+// row's gz1e is formed as gC - gz1m (one fp32 subtraction: within one rounding of |gC| of the stored
+// gz1e), so the edge backward writes one E-row array fewer (gz1e is never materialised).
+template <bool SUMC>
 __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, int chunk, const int* __restrict__ rpd,
                                                              const int* __restrict__ rps,
                                                              const int* __restrict__ perm_s,
@@ -675,22 +679,30 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, int chunk, c
     for (int u = 0; u < PQ_U; ++u) {
       if (d0 + u >= d1) break;
       p += xm[u];
-      if (gz1e) q += xe[u];
+      if (gz1e) q += SUMC ? xe[u] - xm[u] : xe[u];
     }
     for (int k = d0 + PQ_U; k < d1; ++k) {   // destination segments longer than PQ_U
-      p += reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
-      if (gz1e) q += reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+      const f32x4 a = reinterpret_cast<const f32x4*>(gz1m + (size_t)k * L)[j];
+      p += a;
+      if (gz1e) {
+        const f32x4 b = reinterpret_cast<const f32x4*>(gz1e + (size_t)k * L)[j];
+        q += SUMC ? b - a : b;
+      }
     }
 #pragma unroll
     for (int u = 0; u < PQ_U; ++u) {
       if (s0 + u >= s1) break;
       q += ym[u];
-      if (gz1e) p += ye[u];
+      if (gz1e) p += SUMC ? ye[u] - ym[u] : ye[u];
     }
     for (int k = s0 + PQ_U; k < s1; ++k) {   // source segments longer than PQ_U
       const size_t kk = (size_t)perm_s[k] * L;
-      q += reinterpret_cast<const f32x4*>(gz1m + kk)[j];
-      if (gz1e) p += reinterpret_cast<const f32x4*>(gz1e + kk)[j];
+      const f32x4 a = reinterpret_cast<const f32x4*>(gz1m + kk)[j];
+      q += a;
+      if (gz1e) {
+        const f32x4 b = reinterpret_cast<const f32x4*>(gz1e + kk)[j];
+        p += SUMC ? b - a : b;
+      }
     }
     stg4(gP + (size_t)v * L + 4 * j, p);
     stg4(gQ + (size_t)v * L + 4 * j, q);
@@ -704,7 +716,8 @@ __global__ __launch_bounds__(256) void pq_scatter_bwd_kernel(int N, int chunk, c
 }
 
 extern "C" int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int* rowptr_src, const int* perm_src,
-                                  const float* gz1m, const float* gz1e, float* gP, float* gQ, void* stream) {
+                                  const float* gz1m, const float* gz1e, int e_is_sum, float* gP, float* gQ,
+                                  void* stream) {
   PDG_CHECK_ARG(n_nodes > 0, "pdg_pq_scatter_bwd: n_nodes must be > 0");
   PDG_CHECK_ARG(PDG_ALIGNED(gz1m) && (!gz1e || PDG_ALIGNED(gz1e)) && PDG_ALIGNED(gP) && PDG_ALIGNED(gQ),
                 "pdg_pq_scatter_bwd: misaligned pointer");
@@ -713,8 +726,9 @@ extern "C" int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int*
   const int grid = (int)(((want < cap ? want : cap) + 7) / 8 * 8);   // a multiple of 8 (node order)
   // 512-node chunks: contiguous per-XCD ranges (0) and 128 / 2,048 measured slower
   const int chunk = PQ_CHUNK > 0 ? PQ_CHUNK : (n_nodes + 7) / 8;
-  hipLaunchKernelGGL(pq_scatter_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, chunk, rowptr_dst,
-                     rowptr_src, perm_src, gz1m, gz1e, gP, gQ);
+  hipLaunchKernelGGL(e_is_sum && gz1e ? pq_scatter_bwd_kernel<true> : pq_scatter_bwd_kernel<false>, dim3(grid),
+                     dim3(256), 0, (hipStream_t)stream, n_nodes, chunk, rowptr_dst, rowptr_src, perm_src, gz1m, gz1e,
+                     gP, gQ);
   PDG_CHECK_LAUNCH("pdg_pq_scatter_bwd");
   return PDG_OK;
 }

@@ -293,6 +293,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   // drops the second store)
   const __amdgpu_buffer_rsrc_t out_m = rows_rsrc(gz1m, r0, r1);
   const __amdgpu_buffer_rsrc_t out_c = rows_rsrc(EU || gC != gz1m ? gC : nullptr, r0, r1);
+  // gz1e == nullptr (the edge update without a gz1e array): its stores dropped the same way
   const __amdgpu_buffer_rsrc_t out_e = rows_rsrc(EU ? gz1e : gz1m, r0, r1);
   dn[0] = dst[clamp_row(first + rg, r1)];   // E > 0: an empty block (first = r1 = E) reads row E - 1
   dn[1] = dst[clamp_row(first + R16 + rg, r1)];
@@ -1739,8 +1740,10 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
                 "pdg_edge_bwd_w2: misaligned pointer");
   const bool eu = ge_next != nullptr;
   PDG_CHECK_ARG(!eu || gC != gz1m, "pdg_edge_bwd_w2: gC may alias gz1m only without the edge update");
-  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && gz1e && st_e && (lb_e || pairs_e) &&
-                        PDG_ALIGNED(a2e) && PDG_ALIGNED(a1e) && PDG_ALIGNED(gz1e)),
+  // gz1e may be NULL with the edge update: not stored (an empty range drops its stores);
+  // pdg_pq_scatter_bwd(e_is_sum) then forms it from gC - gz1m
+  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && st_e && (lb_e || pairs_e) &&
+                        PDG_ALIGNED(a2e) && PDG_ALIGNED(a1e) && (!gz1e || PDG_ALIGNED(gz1e))),
                 "pdg_edge_bwd_w2: edge-update arguments missing or misaligned");
   // 16-row rounds, two rounds of loads in flight (edge_bwd_w2_kernel): two buffers of images + masks
   const size_t shm = eu ? 2 * (4 * IMG16 + 2 * MSK16) : 2 * (2 * IMG16 + MSK16);

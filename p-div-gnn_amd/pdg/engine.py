@@ -71,6 +71,9 @@ VARIANTS = {
     # P/Q gather backward before the Wc pass (gz1m / gz1e re-read while still in the Infinity Cache:
     # pq_scatter_bwd 63.6 -> 59.7 us and edge_gout_wc 145 -> 140 us per call, same box)
     "pq_first": ("PDG_PQ_FIRST", True),
+    # fused edge backward: gz1e not stored; the P/Q gather backward forms it per row as gC - gz1m (one fp32
+    # rounding of |gC|) from the gC rows the Wc pass reads anyway: one E-row array written fewer per step
+    "gz1e_from_gc": ("PDG_GZ1E_FROM_GC", True),
     # edge forward in the block-cooperative layout (pdg_edge_fwd_coop; 240 -> 230 us per call at config 2)
     # instead of pdg_edge_fwd
     "coop_fwd": ("PDG_EDGE_FWD_COOP", True),
@@ -198,6 +201,7 @@ class EPDEngine:
         # kernel variants (VARIANTS above; tests and A/B tools flip these attributes)
         self.fused_edge_wgrad = var["fused_edge_wgrad"]
         self.pq_first = var["pq_first"]
+        self.gz1e_from_gc = var["gz1e_from_gc"]
         self.coop_fwd = var["coop_fwd"]
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
@@ -524,7 +528,9 @@ class EPDEngine:
 
         ge_next = None              # d loss / d e_S: the last edge update has no consumer
         gaggr, gx_part, gx_t = (self._empty(N, L) for _ in range(3))
-        gz1m, gz1e = self._empty(E, L), self._empty(E, L)
+        e_sum = fused and self.gz1e_from_gc   # gz1e never stored: pdg_pq_scatter_bwd takes gC - gz1m
+        gz1m = self._empty(E, L)
+        gz1e = None if e_sum else self._empty(E, L)
         ge_bufs = [self._empty(E, L), self._empty(E, L)]
         gC_fused = self._empty(E, L) if fused else None
         gx_next = gx
@@ -573,6 +579,8 @@ class EPDEngine:
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
                             _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, int(t == S - 1), s)
+                # the edge-update rows of the P/Q gather backward: gz1e, or gC (= gz1m + gz1e) with e_is_sum
+                ge_rows, e_is_sum = (gC, 1) if (e_sum and eu) else (gz1e if eu else None, 0)
                 if fused:
                     # + the column sums / pairs of the LayerNorm that produced e_t (LN_e of step t-1, or the
                     # edge encoder's)
@@ -592,8 +600,9 @@ class EPDEngine:
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(T["WcT"]),
                             _p(gz2m), _p(gz1m), _p(gz2e), _p(gz1e if eu else None), _p(gC), _p(ge_out), pm, nm, pe, ne, s)
+                    ge_rows, e_is_sum = gz1e if eu else None, 0
                 self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
-                        _p(plan.perm_src), _p(gz1m), _p(gz1e if eu else None), _p(gP), _p(gQ), s)
+                        _p(plan.perm_src), _p(gz1m), _p(ge_rows), e_is_sum, _p(gP), _p(gQ), s)
                 if fused and self.pq_first:   # gz1m / gz1e read while still in the Infinity Cache
                     self._t("edge_gout", gout_fn, *gout_args)
             # gx_t, with the column sums / pairs of the LayerNorm whose output it is the gradient of:

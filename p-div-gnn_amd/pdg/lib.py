@@ -68,7 +68,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_gemm_sum2": [I, P, P, P, P, P, P, P],
     "pdg_gemm_sum2_rw": [I, P, P, P, P, P, P, P, P, P, P, P, P, I, P],
     "pdg_edge_bwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P],
-    "pdg_pq_scatter_bwd": [I, P, P, P, P, P, P, P, P],
+    "pdg_pq_scatter_bwd": [I, P, P, P, P, P, I, P, P, P],
     "pdg_wgrad_accum": [I, P, P, P, P, P, I, P],
     "pdg_wgrad_reduce": [P, I, P, I, I, P, P],
     "pdg_transpose128_batch": [I, P, P, P, P],

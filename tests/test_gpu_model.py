@@ -255,6 +255,31 @@ def test_fused_edge_weight_gradients_match_separate_passes(nmesh, ngraph, steps)
 
 
 @pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
+def test_gz1e_from_gc_matches_stored_gz1e(nmesh, ngraph, steps):
+    """The shipped edge backward stores no gz1e: pdg_pq_scatter_bwd forms it per row as gC - gz1m.
+    Against the form that stores gz1e, gP / gQ differ by one fp32 rounding of |gC| per row, so every
+    parameter gradient agrees to 1e-6 (the loss and output bitwise: the forward is untouched)."""
+    from gnn_local_stress import losses
+    from pdg import meshgen
+    samples = meshgen.make_dataset(ngraph, n=nmesh, hole_radius=(0.15, 0.3), seed=7)
+    batch = make_batch(samples)
+    stats = {k: float(v) for k, v in dataset_stats(batch).items()}
+    grads, losses_ = {}, {}
+    for e_sum in (True, False):
+        model = _model(steps, stats)
+        model._engine_for(batch.pos.device).gz1e_from_gc = e_sum
+        pred = model(batch, scale_output=False).local_stress
+        gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
+        total, _, _ = losses.batch_loss(pred, batch, gt, divergence=True, divergence_penalty=10.0)
+        total.backward()
+        losses_[e_sum] = float(total)
+        grads[e_sum] = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    assert losses_[True] == losses_[False]
+    for name, g in grads[True].items():
+        assert rel(g, grads[False][name]) < 1e-6, (name, rel(g, grads[False][name]))
+
+
+@pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
 def test_forward_variants_agree(nmesh, ngraph, steps):
     """The three edge-forward / aggregation variants of the engine: pdg_edge_fwd_coop_seg (message
     sums formed in the edge forward, message LayerNorm applied by node_net's loaders; default),

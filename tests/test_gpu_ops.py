@@ -192,10 +192,13 @@ def test_transpose_strided(env):
     assert torch.equal(out.cpu(), W[:, 2 * L:].T.contiguous().cpu())
 
 
+@pytest.mark.parametrize("e_is_sum", [0, 1])
 @pytest.mark.parametrize("N,E,isolated", [(300, 2500, 0), (300, 2500, 7), (5000, 30000, 3)])
-def test_pq_scatter_bwd(env, N, E, isolated):
+def test_pq_scatter_bwd(env, N, E, isolated, e_is_sum):
     """Heavy node (in-degree N/7 > the 8 rows kept in flight), random degrees, and `isolated`
-    trailing nodes with no edge at all (their row pointers equal E: nothing may be read there)."""
+    trailing nodes with no edge at all (their row pointers equal E: nothing may be read there).
+    e_is_sum: the second array is gC = gz1m + gz1e (fp32, as the edge backward writes it) and the
+    kernel forms gz1e = gC - gz1m per row; checked against the exact gz1e in fp64."""
     lib, sh, _ = env
     s = sh()
     src, dst, rp = _csr(N - isolated, E, seed=3)
@@ -208,8 +211,9 @@ def test_pq_scatter_bwd(env, N, E, isolated):
     gP, gQ = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
     # keep every device array referenced until the kernel has run (no temporaries)
     rp_d, rps_d, perm_d = rp.int().cuda(), rps.int().cuda(), perm_src.int().cuda()
-    lib.pdg_pq_scatter_bwd(N, rp_d.data_ptr(), rps_d.data_ptr(), perm_d.data_ptr(), gm.data_ptr(), ge.data_ptr(),
-                           gP.data_ptr(), gQ.data_ptr(), s)
+    g2 = gm + ge if e_is_sum else ge
+    lib.pdg_pq_scatter_bwd(N, rp_d.data_ptr(), rps_d.data_ptr(), perm_d.data_ptr(), gm.data_ptr(), g2.data_ptr(),
+                           e_is_sum, gP.data_ptr(), gQ.data_ptr(), s)
     z = lambda: torch.zeros(N, L, dtype=torch.float64)
     refP = z().index_add_(0, dst, gm.double().cpu()).index_add_(0, src, ge.double().cpu())
     refQ = z().index_add_(0, src, gm.double().cpu()).index_add_(0, dst, ge.double().cpu())
