@@ -57,7 +57,8 @@ TREE_GLOBS = ("p-div-gnn_amd/pdg/libpdivgnn_hip.so", "p-div-gnn_amd/csrc/*.hip",
 PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
              "edge_bwd": "void edge_bwd_kernel<true>",
              "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_x6_kernel", "node_net_pair_kernel", "node_net_kernel"),
-             "pq_scatter_bwd": "pq_scatter_bwd_kernel",
+             # the edge-update steps' instantiation (gz1e formed as gC - gz1m); the last step's is <false>
+             "pq_scatter_bwd": ("void pq_scatter_bwd_kernel<true>", "pq_scatter_bwd_kernel"),
              "wgrad_W2": "wgrad_x6_kernel",
              # the edge-update instantiations
              "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
@@ -233,7 +234,8 @@ def cpu_baseline(cfg, samples, full_graphs: int, reps: int = 5, one_thread: bool
 
 
 # ---------------------------------------------------------------------------------- roofline
-def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, seg: bool = False) -> dict:
+def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, seg: bool = False,
+                e_sum: bool = True) -> dict:
     """Algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops with the peak of their
     instruction type, and the bytes the kernel must read/write (inputs once, outputs once, int32
     indices).  An fp32-accurate 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA,
@@ -247,10 +249,11 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
                      E * ((9 if infer else 11) * 4 * L + 8) - (E * 4 * L if (seg and infer) else 0)
                      + (8 * L * N if seg else 0)),
         # fused (pdg_edge_bwd_w2): 2 W2^T products + 2 weight-gradient products per edge (bf16x6);
-        # reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gz1e, gC; one slab
-        # read+write per block.  unfused (pdg_edge_bwd): W2^T x2 (bf16x6) + Wc^T (fp32); writes
-        # gz2m, gz1m, gz2e, gz1e, gC, ge_out
-        "edge_bwd": (([(E * 4 * g * X6, PEAK_BF16_MFMA)], E * (9 * 4 * L + 4) + 2 * nslab_bytes) if fused
+        # reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gC (+ gz1e unless e_sum: the
+        # P/Q gather backward forms it from gC - gz1m); one slab read+write per block.  unfused
+        # (pdg_edge_bwd): W2^T x2 (bf16x6) + Wc^T (fp32); writes gz2m, gz1m, gz2e, gz1e, gC, ge_out
+        "edge_bwd": (([(E * 4 * g * X6, PEAK_BF16_MFMA)], E * ((8 if e_sum else 9) * 4 * L + 4) + 2 * nslab_bytes)
+                     if fused
                      else ([(E * 2 * g * X6, PEAK_BF16_MFMA), (E * g, PEAK_FP32_MFMA)], E * (12 * 4 * L + 4))),
         # fused Wc path (pdg_edge_gout_wc): Wc^T product + weight-gradient product (bf16x6); reads gC,
         # e, ge_next and the LayerNorm input of e (column sums), writes ge_out; one slab read+write
@@ -496,7 +499,7 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
     # the fused message sums run in inference only unless PDG_SEG_SUMS_TRAIN=1 (engine.py:253)
     seg = getattr(eng, "seg_sums", False) if infer else getattr(eng, "seg_sums_train", False)
-    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg)
+    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg, fused and getattr(eng, "gz1e_from_gc", False))
     pmc_path, pmc_reason = pmc_file() if with_pmc else (None, "not collected for this config")
     pmc = load_pmc(fused, pmc_path)
     sq_path, sq_reason = sq_file() if with_pmc else (None, "not collected for this config")
