@@ -44,8 +44,12 @@ __device__ __forceinline__ void block_sum_k(double (&x)[K], double* red) {
 
 // One block of 1024 threads per graph; the three channels in one pass over the graph's nodes
 // (loads of NF_U nodes issued together): a 256-thread block with one channel per pass and a
-// reduction per channel ran 31 us for 8 graphs of 5,041 nodes (latency-bound).
+// reduction per channel ran 31 us for 8 graphs of 5,041 nodes (latency-bound).  The first NF_C
+// loop iterations (NF_C NF_U 1024 = 8,192 nodes) keep their gt / pred values in registers, so for
+// such graphs the mean, the sums and the gradient rows take one round trip of loads instead of
+// three; larger graphs re-read the rest.  Same sums in the same order as the three-pass form.
 constexpr int NF_U = 4;
+constexpr int NF_C = 2;
 
 __global__ __launch_bounds__(1024) void nmse_fwd_kernel(const int* __restrict__ ptr, const float* __restrict__ gt,
                                                         const float* __restrict__ pred, float* __restrict__ loss,
@@ -56,8 +60,29 @@ __global__ __launch_bounds__(1024) void nmse_fwd_kernel(const int* __restrict__ 
   const int n0 = ptr[g], n1 = ptr[g + 1];
   const double n = (double)(n1 - n0);
   const int T = blockDim.x;
+  // node of iteration k, slot u: n0 + t + (k NF_U + u) T (the loops below step NF_U T per iteration)
+  float tc[NF_C][NF_U][3], pc[NF_C][NF_U][3];
+#pragma unroll
+  for (int k = 0; k < NF_C; ++k)
+#pragma unroll
+    for (int u = 0; u < NF_U; ++u)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int i = n0 + (int)threadIdx.x + (k * NF_U + u) * T;
+        const bool ok = i < n1;
+        tc[k][u][c] = ok ? gt[(size_t)i * 3 + c] : 0.f;
+        pc[k][u][c] = ok ? pred[(size_t)i * 3 + c] : 0.f;
+      }
+  const int rest = n0 + (int)threadIdx.x + NF_C * NF_U * T;   // the first iteration past the cached ones
   double m[3] = {0, 0, 0};
-  for (int i = n0 + threadIdx.x; i < n1; i += NF_U * T) {
+  // cached iterations past the graph's end add exact zeros (the loop form skips them: the same sums)
+#pragma unroll
+  for (int k = 0; k < NF_C; ++k)
+#pragma unroll
+    for (int u = 0; u < NF_U; ++u)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) m[c] += (double)tc[k][u][c];
+  for (int i = rest; i < n1; i += NF_U * T) {
     float t[NF_U][3];
 #pragma unroll
     for (int u = 0; u < NF_U; ++u)
@@ -73,7 +98,19 @@ __global__ __launch_bounds__(1024) void nmse_fwd_kernel(const int* __restrict__ 
 #pragma unroll
   for (int c = 0; c < 3; ++c) mean[c] = (float)(m[c] / n);   // gt.mean(axis=0)
   double sd[6] = {0, 0, 0, 0, 0, 0};   // se[3], sd[3]
-  for (int i = n0 + threadIdx.x; i < n1; i += NF_U * T) {
+#pragma unroll
+  for (int k = 0; k < NF_C; ++k)
+#pragma unroll
+    for (int u = 0; u < NF_U; ++u)
+      if (n0 + (int)threadIdx.x + (k * NF_U + u) * T < n1)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const float d = tc[k][u][c] - pc[k][u][c];
+          const float mm = tc[k][u][c] - mean[c];
+          sd[c] += (double)(d * d);
+          sd[3 + c] += (double)(mm * mm);
+        }
+  for (int i = rest; i < n1; i += NF_U * T) {
     float t[NF_U][3], p[NF_U][3];
 #pragma unroll
     for (int u = 0; u < NF_U; ++u)
@@ -108,13 +145,25 @@ __global__ __launch_bounds__(1024) void nmse_fwd_kernel(const int* __restrict__ 
   // pdg_nmse_fwd_bwd: the graph's gradient rows with nmse_bwd_kernel's arithmetic (bitwise), den from the
   // block's own sums
   const float sc = scale[0];
-  for (int e = 3 * n0 + threadIdx.x; e < 3 * n1; e += T) {
-    const int c = e % 3;
+  auto grad = [&](int i, int c, float t, float p) {
     const float den = (float)sd[3 + c];
-    const float d = gt[e] - pred[e];
+    const float d = t - p;
     const float v = sc * ((-2.0f * d) / den) / 3.0f;
+    const size_t e = (size_t)i * 3 + c;
     gp[e] = accumulate ? gp[e] + v : v;
-  }
+  };
+#pragma unroll
+  for (int k = 0; k < NF_C; ++k)
+#pragma unroll
+    for (int u = 0; u < NF_U; ++u) {
+      const int i = n0 + (int)threadIdx.x + (k * NF_U + u) * T;
+      if (i < n1)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) grad(i, c, tc[k][u][c], pc[k][u][c]);
+    }
+  for (int i = rest; i < n1; i += T)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) grad(i, c, gt[(size_t)i * 3 + c], pred[(size_t)i * 3 + c]);
 }
 
 extern "C" int pdg_nmse_fwd(int n_graphs, const int* ptr, const float* gt, const float* pred, float* loss,

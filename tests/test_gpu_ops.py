@@ -1170,10 +1170,11 @@ def test_bwd_epilogue_matches_separate_launches(env):
     assert not torch.equal(a["W"][0], torch.full((L, L), 0.25, device="cuda"))   # something was added
 
 
-@pytest.mark.parametrize("sizes,accumulate", [((5041,) * 8, 0), ((17, 2, 3000, 250), 1)])
+@pytest.mark.parametrize("sizes,accumulate", [((5041,) * 8, 0), ((17, 2, 3000, 250), 1), ((9000, 20000, 8192), 0)])
 def test_nmse_fwd_bwd_equals_fwd_then_bwd(env, sizes, accumulate):
     """pdg_nmse_fwd_bwd (per-graph NMSE and its gradient in one launch) is bitwise pdg_nmse_fwd + pdg_nmse_bwd:
-    losses, denominators and the gradient (written or accumulated); ragged graphs."""
+    losses, denominators and the gradient (written or accumulated); ragged graphs, and graphs past the
+    8,192 nodes whose values the kernel keeps in registers (the rest re-read).  Losses against fp64."""
     lib, sh, _ = env
     s = sh()
     B, N = len(sizes), sum(sizes)
@@ -1190,3 +1191,9 @@ def test_nmse_fwd_bwd_equals_fwd_then_bwd(env, sizes, accumulate):
                                 scale.data_ptr(), accumulate, g1.data_ptr(), s) == 0
     torch.cuda.synchronize()
     assert torch.equal(l0, l1) and torch.equal(d0, d1) and torch.equal(g0, g1)
+    gt64, pr64 = gt.double().cpu(), pred.double().cpu()
+    for b in range(B):
+        lo, hi = int(ptr[b]), int(ptr[b + 1])
+        t, p = gt64[lo:hi], pr64[lo:hi]
+        ref = (((t - p) ** 2).sum(0) / ((t - t.mean(0)) ** 2).sum(0)).mean()
+        assert abs(float(l1[b]) - float(ref)) <= 1e-5 * abs(float(ref)), (b, float(l1[b]), float(ref))
