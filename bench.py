@@ -372,7 +372,7 @@ def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None, pmc_source=None):
 
 
 # ---------------------------------------------------------------------------------- timing
-TIMED_KERNELS = ["edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2", "segment_sum", "node_net", "node_bwd", "edge_enc_fwd",
+TIMED_KERNELS = ["edge_fwd", "edge_bwd", "edge_gout", "wgrad_W2", "segment_sum", "node_net", "node_bwd", "edge_enc_fwd", "edge_enc_bwd",
                  "node_pq", "gemm_sum2", "pq_scatter_bwd", "sync_collective"]
 
 

@@ -309,20 +309,21 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   load_wslice(ws, W2T, w);
   const pdg_ln_bwd lbm = lnb_resolve(lbm_p, pm, npm, stm_p);
   const pdg_ln_bwd lbe = EU ? lnb_resolve(lbe_p, pe, npe, ste_p) : lbm;
-  auto round = [&](const int s, const int base) {
+  auto stage = [&](const int s, const int base) {
     unsigned char* img_gm = sm + s * BUF;                      // gz2m
     unsigned char* img_am = img_gm + IMG16;                    // a1m
     unsigned char* img_ge = img_gm + 2 * IMG16;                // gz2e (EU)
     unsigned char* img_ae = img_gm + 3 * IMG16;                // a1e (EU)
     unsigned char* msk_m = img_gm + NIMG * IMG16;              // [a1m > 0]
     unsigned char* msk_e = msk_m + MSK16;                      // [a1e > 0] (EU)
-    // ---- stage: gz2 (LN + relu backward), a1 and its relu mask into this round's images
+    // ---- gz2 (LN + relu backward), a1 and its relu mask into this round's images
     {
       const bool ok = base + rg < r1;
-      const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
       const f32x4 a1mv = pa1[s], a1ev = pa1e[s];
       // a row past r1 has gz2 = 0, which zeroes its products whatever its (finite, clamped-row) a1:
-      // no select on a1
+      // no select on a1.  (gz2 computed for every row and selected, branch-free as in pdg_edge_enc_bwd:
+      // 256 -> 226 VGPRs but 3-4 us slower per call, gpurun_out/r04s)
+      const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
       const f32x4 zm = ok ? ln_relu_bwd4(pg[s], pa2[s], stm, lbm, g4) : zero;
       const f32x4 am = a1mv;
       bsum += zm;
@@ -342,7 +343,14 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
     // the dst ids of the one after that
     issue(s, base + stride);
     dn[s] = dst[clamp_row(base + 2 * stride + rg, r1)];
-    __syncthreads();   // this round's images complete (the other buffer is the previous round's)
+  };
+  auto compute = [&](const int s, const int base) {
+    const unsigned char* img_gm = sm + s * BUF;
+    const unsigned char* img_am = img_gm + IMG16;
+    const unsigned char* img_ge = img_gm + 2 * IMG16;
+    const unsigned char* img_ae = img_gm + 3 * IMG16;
+    const unsigned char* msk_m = img_gm + NIMG * IMG16;
+    const unsigned char* msk_e = msk_m + MSK16;
     // ---- dW2 += gz2m^T a1m (+ gz2e^T a1e)
     wgrad_round<1, T16>(acc, img_gm, img_am);
     if (EU) wgrad_round<1, T16>(acc, img_ge, img_ae);
@@ -373,9 +381,16 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   };
   // both rounds of a 32-row step always run: a round past r1 stages zero rows (adding exact zeros to
   // the weight gradient) and stores nothing
+  // (the software-pipelined form of pdg_edge_enc_bwd, products of round k beside the stage of round k + 1,
+  // did not interleave here: the compiler kept the 72 products of a round together even with scheduling
+  // groups)
   for (int base = first; base < r1; base += stride) {
-    round(0, base);
-    round(1, base + R16);
+    stage(0, base);
+    __syncthreads();   // this round's images complete (the other buffer is the previous round's)
+    compute(0, base);
+    stage(1, base + R16);
+    __syncthreads();
+    compute(1, base + R16);
   }
   __syncthreads();   // the last rounds' image reads precede the LDS reuse below
   slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
@@ -1412,27 +1427,35 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd2_kernel(
   pin_vgpr(g4);
   pin_vgpr(w04);
   pin_vgpr(b04);
-  auto round = [&](const int s, const int base) {
+  auto stage = [&](const int s, const int base) {
     unsigned char* img_g = sm + s * EEB2_BUF;                  // gz2
     unsigned char* img_a = img_g + IMG16;                      // a1
     unsigned char* msk = img_g + 2 * IMG16;                    // [a1 > 0]
     float* ev = reinterpret_cast<float*>(msk + MSK16);         // the round's 16 inputs
-    {
-      const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bool ok = base + rg < r1;
-      const f32x4 zg = ok ? ln_relu_bwd4(pg[s], pa2[s], st, lb, g4) : zero;
-      bsum += zg;
-      img_store4<T16>(img_g, rg, cg, zg);
-      f32x4 a;
+    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool ok = base + rg < r1;
+    // computed for every row (a row past r1 is a clamped, finite row) and selected: a conditional
+    // call here became a branch, which splits the round into two scheduling regions
+    const f32x4 zr = ln_relu_bwd4(pg[s], pa2[s], st, lb, g4);
+    f32x4 zg;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] = fmaxf(fmaf(w04[j], pe[s], 0.f) + b04[j], 0.f);   // encoder_kernel's a1
-      a = ok ? a : zero;
-      img_store4<T16>(img_a, rg, cg, a);
-      *reinterpret_cast<unsigned*>(msk + rg * MSK_STRIDE + 4 * cg) = relu_mask4(a);
-      if (cg == 0) ev[rg] = ok ? pe[s] : 0.f;
-    }
+    for (int j = 0; j < 4; ++j) zg[j] = ok ? zr[j] : 0.f;
+    bsum += zg;
+    img_store4<T16>(img_g, rg, cg, zg);
+    f32x4 a;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = fmaxf(fmaf(w04[j], pe[s], 0.f) + b04[j], 0.f);   // encoder_kernel's a1
+    a = ok ? a : zero;
+    img_store4<T16>(img_a, rg, cg, a);
+    *reinterpret_cast<unsigned*>(msk + rg * MSK_STRIDE + 4 * cg) = relu_mask4(a);
+    ev[rg] = ok ? pe[s] : 0.f;   // every thread of the row group (the same value): no branch in the round
     issue(s, base + 2 * R16);   // the set is free: the round after next
-    __syncthreads();            // this round's images complete (the other buffer is the previous round's)
+  };
+  auto compute = [&](const int s) {
+    const unsigned char* img_g = sm + s * EEB2_BUF;
+    const unsigned char* img_a = img_g + IMG16;
+    const unsigned char* msk = img_g + 2 * IMG16;
+    const float* ev = reinterpret_cast<const float*>(msk + MSK16);
     wgrad_round<1, T16>(acc, img_g, img_a);                // dW2 += gz2^T a1
     f32x4 d[1][1];
     const unsigned char* imgs[1] = {img_g};
@@ -1447,10 +1470,31 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd2_kernel(
       sb[j] += (double)z;
     }
   };
+  // software-pipelined: the products of round k and the stage of round k + 1 (its rows already in
+  // registers, its images in the other buffer) between the same two barriers, interleaved by scheduling
+  // groups (two operand reads, one matrix instruction, three vector ones; left to itself the compiler
+  // issues all 36 products of a round before any of the stage's vector work).  94 -> 88 us per config-2
+  // call against the stage-then-products loop, same box, bitwise the same (gpurun_out/r04r).
+  auto weave = [&]() {
+#pragma unroll
+    for (int i = 0; i < 36; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+    }
+  };
   // both rounds of a 32-row step always run: a round past r1 stages zero rows (exact zeros)
+  stage(0, r0);
+  __syncthreads();
   for (int base = r0; base < r1; base += 2 * R16) {
-    round(0, base);
-    round(1, base + R16);
+    compute(0);
+    stage(1, base + R16);
+    weave();
+    __syncthreads();
+    compute(1);
+    stage(0, base + 2 * R16);   // past r1 on the last step: zero rows nobody reads
+    weave();
+    __syncthreads();
   }
   __syncthreads();   // the last rounds' image reads precede the LDS reuse below
   slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
