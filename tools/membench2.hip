@@ -30,7 +30,7 @@ __device__ __forceinline__ int clampr(int r, int r1) { return r < r1 ? r : r1 - 
 // XI: XCD-interleaved rounds (blocks b and b + 8 share an XCD's L2: each XCD owns a contiguous eighth of
 // the rows and its blocks take its 32-row rounds round-robin, so the XCD's blocks sweep its range
 // together and the gathered rows' reuse stays inside its L2); otherwise one contiguous range per block.
-template <int R, int G, int W, int DEPTH, bool NT, int BPC, bool XI = false>
+template <int R, int G, int W, int DEPTH, bool NT, int BPC, bool XI = false, bool IL = false>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC, 2 * BPC))) void mix(const float* const* __restrict__ in, float* const* __restrict__ out,
                                                const int* __restrict__ gd, const int* __restrict__ gs,
                                                const float* __restrict__ P, const float* __restrict__ Q, int E) {
@@ -74,9 +74,10 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int a = 0; a < G; ++a) {
-        const float* tb = (a & 1) ? Q : P;
         const int node = ((a >> 1) ^ (a & 1)) ? si[s][u] : di[s][u];
-        g[gslot][a][u] = *reinterpret_cast<const f32x4*>(tb + (size_t)node * L + c);
+        // IL: P and Q interleaved per node ([P | Q], 1 KB rows in P's buffer): a node's two rows adjacent
+        const float* row = IL ? P + (size_t)node * 2 * L + ((a & 1) ? L : 0) : ((a & 1) ? Q : P) + (size_t)node * L;
+        g[gslot][a][u] = *reinterpret_cast<const f32x4*>(row + c);
       }
   };
 #pragma unroll
@@ -214,19 +215,19 @@ double time_us(F launch, int reps = 20) {
   return ms * 1e3 / reps;
 }
 
-template <int R, int G, int W, int DEPTH, bool NT, int BPC = 1, bool XI = false>
+template <int R, int G, int W, int DEPTH, bool NT, int BPC = 1, bool XI = false, bool IL = false>
 void run(const Bufs& B, int cus, bool small = false) {
   const int blocks_per_cu = BPC;
   const int nblk = cus * blocks_per_cu;
   const double us = time_us([&] {
-    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC, XI>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out,
+    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC, XI, IL>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out,
                        small ? B.gd_small : B.gd, small ? B.gs_small : B.gs, B.P, B.Q, B.E);
   });
   const double streamed = (double)B.E * 512.0 * (R + W);
   const double gathered = (double)B.E * 512.0 * G;
-  printf("{\"mix\": \"%dR+%dG+%dW\", \"table\": \"%s\", \"rows\": \"%s\", \"depth\": %d, \"waves_per_cu\": %d, \"stores\": \"%s\", \"us\": %.1f, "
+  printf("{\"mix\": \"%dR+%dG+%dW\", \"table\": \"%s%s\", \"rows\": \"%s\", \"depth\": %d, \"waves_per_cu\": %d, \"stores\": \"%s\", \"us\": %.1f, "
          "\"streamed_TBps\": %.3f, \"with_gathers_TBps\": %.3f}\n",
-         R, G, W, small ? "1k nodes" : "N nodes", XI ? "xcd-interleaved" : "contiguous", DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
+         R, G, W, small ? "1k nodes" : "N nodes", IL ? ", P|Q interleaved" : "", XI ? "xcd-interleaved" : "contiguous", DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
          (streamed + gathered) / us * 1e-6);
   fflush(stdout);
 }
@@ -267,9 +268,9 @@ int main() {
   (void)hipMalloc(&B.gs_small, E * sizeof(int));
   (void)hipMemcpy(B.gd_small, hd.data(), E * sizeof(int), hipMemcpyHostToDevice);
   (void)hipMemcpy(B.gs_small, hs.data(), E * sizeof(int), hipMemcpyHostToDevice);
-  (void)hipMalloc(&B.P, (size_t)N * 512);
+  (void)hipMalloc(&B.P, (size_t)N * 1024);   // room for the interleaved [P | Q] table
   (void)hipMalloc(&B.Q, (size_t)N * 512);
-  (void)hipMemset(B.P, 0, (size_t)N * 512);
+  (void)hipMemset(B.P, 0, (size_t)N * 1024);
   (void)hipMemset(B.Q, 0, (size_t)N * 512);
 
   {  // the guide's anchor: grid-stride float4 copy over 1 GiB arrays
@@ -284,6 +285,18 @@ int main() {
            2.0 * n * 16 / us * 1e-6);
     (void)hipFree(a);
     (void)hipFree(b);
+  }
+  // P / Q as two tables vs interleaved per node, contiguous and XCD-interleaved rows (the edge forward's)
+  if (getenv("MB_IL")) {
+    for (int rep = 0; rep < 3; ++rep) {
+      run<2, 4, 5, 1, true, 1, false, false>(B, cus);
+      run<2, 4, 5, 1, true, 1, false, true>(B, cus);
+      run<2, 4, 5, 1, true, 1, true, false>(B, cus);
+      run<2, 4, 5, 1, true, 1, true, true>(B, cus);
+      run<0, 4, 0, 1, true, 1, true, false>(B, cus);
+      run<0, 4, 0, 1, true, 1, true, true>(B, cus);
+    }
+    return 0;
   }
   // the edge forward's mix in one set of waves vs split over stream waves and gather waves
   for (int rep = 0; rep < 2; ++rep) {
