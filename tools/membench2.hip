@@ -30,7 +30,7 @@ __device__ __forceinline__ int clampr(int r, int r1) { return r < r1 ? r : r1 - 
 // XI: XCD-interleaved rounds (blocks b and b + 8 share an XCD's L2: each XCD owns a contiguous eighth of
 // the rows and its blocks take its 32-row rounds round-robin, so the XCD's blocks sweep its range
 // together and the gathered rows' reuse stays inside its L2); otherwise one contiguous range per block.
-template <int R, int G, int W, int DEPTH, bool NT, int BPC, bool XI = false, bool IL = false>
+template <int R, int G, int W, int DEPTH, bool NT, int BPC, bool XI = false, bool IL = false, int GSEL = 0>
 __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC, 2 * BPC))) void mix(const float* const* __restrict__ in, float* const* __restrict__ out,
                                                const int* __restrict__ gd, const int* __restrict__ gs,
                                                const float* __restrict__ P, const float* __restrict__ Q, int E) {
@@ -74,7 +74,13 @@ __global__ __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(2 * BPC
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int a = 0; a < G; ++a) {
-        const int node = ((a >> 1) ^ (a & 1)) ? si[s][u] : di[s][u];
+        // GSEL 1: only the source-side rows (Q[src], P[src]) of the four, 2: only the destination-side ones
+        const bool src_side = (a >> 1) ^ (a & 1);
+        if ((GSEL == 1 && !src_side) || (GSEL == 2 && src_side)) {
+          g[gslot][a][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+          continue;
+        }
+        const int node = src_side ? si[s][u] : di[s][u];
         // IL: P and Q interleaved per node ([P | Q], 1 KB rows in P's buffer): a node's two rows adjacent
         const float* row = IL ? P + (size_t)node * 2 * L + ((a & 1) ? L : 0) : ((a & 1) ? Q : P) + (size_t)node * L;
         g[gslot][a][u] = *reinterpret_cast<const f32x4*>(row + c);
@@ -215,19 +221,19 @@ double time_us(F launch, int reps = 20) {
   return ms * 1e3 / reps;
 }
 
-template <int R, int G, int W, int DEPTH, bool NT, int BPC = 1, bool XI = false, bool IL = false>
+template <int R, int G, int W, int DEPTH, bool NT, int BPC = 1, bool XI = false, bool IL = false, int GSEL = 0>
 void run(const Bufs& B, int cus, bool small = false) {
   const int blocks_per_cu = BPC;
   const int nblk = cus * blocks_per_cu;
   const double us = time_us([&] {
-    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC, XI, IL>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out,
+    hipLaunchKernelGGL((mix<R, G, W, DEPTH, NT, BPC, XI, IL, GSEL>), dim3(nblk), dim3(THREADS), 0, 0, B.d_in, B.d_out,
                        small ? B.gd_small : B.gd, small ? B.gs_small : B.gs, B.P, B.Q, B.E);
   });
   const double streamed = (double)B.E * 512.0 * (R + W);
   const double gathered = (double)B.E * 512.0 * G;
   printf("{\"mix\": \"%dR+%dG+%dW\", \"table\": \"%s%s\", \"rows\": \"%s\", \"depth\": %d, \"waves_per_cu\": %d, \"stores\": \"%s\", \"us\": %.1f, "
          "\"streamed_TBps\": %.3f, \"with_gathers_TBps\": %.3f}\n",
-         R, G, W, small ? "1k nodes" : "N nodes", IL ? ", P|Q interleaved" : "", XI ? "xcd-interleaved" : "contiguous", DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
+         R, G, W, small ? "1k nodes" : "N nodes", IL ? ", P|Q interleaved" : (GSEL == 1 ? ", src-side gathers only" : (GSEL == 2 ? ", dst-side gathers only" : "")), XI ? "xcd-interleaved" : "contiguous", DEPTH, 8 * blocks_per_cu, NT ? "nt" : "default", us, streamed / us * 1e-6,
          (streamed + gathered) / us * 1e-6);
   fflush(stdout);
 }
@@ -287,6 +293,15 @@ int main() {
     (void)hipFree(b);
   }
   // P / Q as two tables vs interleaved per node, contiguous and XCD-interleaved rows (the edge forward's)
+  if (getenv("MB_GSEL")) {   // which half of the four gathers costs what beside the streams
+    for (int rep = 0; rep < 3; ++rep) {
+      run<2, 4, 5, 1, true, 1, true, false, 0>(B, cus);
+      run<2, 4, 5, 1, true, 1, true, false, 1>(B, cus);
+      run<2, 4, 5, 1, true, 1, true, false, 2>(B, cus);
+      run<2, 0, 5, 1, true, 1, true>(B, cus);
+    }
+    return 0;
+  }
   if (getenv("MB_IL")) {
     for (int rep = 0; rep < 3; ++rep) {
       run<2, 4, 5, 1, true, 1, false, false>(B, cus);
