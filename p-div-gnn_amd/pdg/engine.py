@@ -82,8 +82,11 @@ VARIANTS = {
     # pdg_segment_sum re-reading a2m, and a2m is not stored (config 5: 11.8 -> 11.5 ms per step, same box).
     # Training keeps pdg_segment_sum (seg_sums_train False): a2m is stored for the backward anyway and the
     # in-kernel sums cost more than the re-read they save (9.91 vs 10.12 ms, config 2).  fp64, because fp32
-    # raw sums (sum a2m - deg mean cancels) flipped a relu mask bit against the fp64 reference.
-    "seg_sums": ("PDG_SEG_SUMS", True),
+    # raw sums (sum a2m - deg mean cancels) flipped a relu mask bit against the fp64 reference.  Off since
+    # the end of round 4: the deferred + XCD-interleaved edge forward (not combinable with the sums) and
+    # pdg_segment_sum beat it in inference too (config 5: 10.41-10.46 vs 10.46-10.67 ms per step in three
+    # same-box pairs, tools/r04z4.sh); kept as the A/B alternative.
+    "seg_sums": ("PDG_SEG_SUMS", False),
     "seg_sums_train": ("PDG_SEG_SUMS_TRAIN", False),
     # the backward's input gradient of x (gP, gQ -> gx) in bf16x6 (pdg_gemm_sum2_coop) instead of the fp32-MFMA
     # pdg_gemm_sum2_rw

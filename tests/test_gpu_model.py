@@ -282,8 +282,8 @@ def test_gz1e_from_gc_matches_stored_gz1e(nmesh, ngraph, steps):
 @pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
 def test_forward_variants_agree(nmesh, ngraph, steps):
     """The three edge-forward / aggregation variants of the engine: pdg_edge_fwd_coop_seg (message
-    sums formed in the edge forward, message LayerNorm applied by node_net's loaders; default),
-    pdg_edge_fwd_coop + pdg_segment_sum, and pdg_edge_fwd + pdg_segment_sum.  Output (training and
+    sums formed in the edge forward, message LayerNorm applied by node_net's loaders; the A/B form),
+    pdg_edge_fwd_coop + pdg_segment_sum (default), and pdg_edge_fwd + pdg_segment_sum.  Output (training and
     inference, where the seg variant stores no a2m) agree to 1e-5 and every parameter gradient to
     VARIANT_TOL (two fp32 evaluations may differ in a relu mask bit whose pre-activation is within
     rounding of zero)."""
