@@ -59,3 +59,15 @@ def test_sq_counters_only_from_this_tree(tmp_path, monkeypatch):
     assert path is None and "bbbb" in reason
     path, reason = bench.sq_file("aaaa")
     assert reason is None and bench.load_sq(path) == {"edge_fwd": 0.42}
+
+
+def test_edge_backward_bytes_follow_the_gz1e_variant():
+    """The edge backward's algorithmic bytes drop one E-row stream (E x 512 B) when gz1e is formed by the
+    P/Q gather backward from gC - gz1m instead of being stored (engine variant gz1e_from_gc)."""
+    N, E, S, slab = 40328, 239744, 10, 256 * (128 * 128 + 128) * 4
+    with_sum = bench.kernel_work(False, N, E, S, slab, True, e_sum=True)["edge_bwd"][1]
+    stored = bench.kernel_work(False, N, E, S, slab, True, e_sum=False)["edge_bwd"][1]
+    assert stored - with_sum == E * 128 * 4
+    # the unfused edge backward does not depend on it
+    assert (bench.kernel_work(False, N, E, S, slab, False, e_sum=True)["edge_bwd"]
+            == bench.kernel_work(False, N, E, S, slab, False, e_sum=False)["edge_bwd"])
