@@ -293,6 +293,14 @@ int main() {
     (void)hipFree(b);
   }
   // P / Q as two tables vs interleaved per node, contiguous and XCD-interleaved rows (the edge forward's)
+  if (getenv("MB_EBW")) {   // the edge backward's mixes: the split pair today vs a fused pass (memory only)
+    for (int rep = 0; rep < 3; ++rep) {
+      run<5, 1, 2, 2, false>(B, cus);   // edge_bwd_w2: gaggr[dst] + a2m, a1m, ge_next, a2e, a1e -> gz1m, gC
+      run<4, 0, 1, 2, false>(B, cus);   // edge_gout_wc: gC, e, ge_next, a2ln -> ge_out
+      run<7, 1, 3, 2, false>(B, cus);   // fused: + e, a2ln; -> gz1m, gC, ge_out (no gC re-read, one ge_next)
+    }
+    return 0;
+  }
   if (getenv("MB_GSEL")) {   // which half of the four gathers costs what beside the streams
     for (int rep = 0; rep < 3; ++rep) {
       run<2, 4, 5, 1, true, 1, true, false, 0>(B, cus);
