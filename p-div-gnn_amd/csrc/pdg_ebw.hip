@@ -38,6 +38,9 @@ constexpr int EBW_IMG = 3 * X6_TERM;        // one bf16x6 image of 32 rows (24 K
 // from 16 rows at a time, which a 128-B stride put on 2 of the 32 banks of a ds_read_b32 lane
 // group (16-way conflicts); 136 B (34 words) spreads them over all 32.  The staging writes (32
 // consecutive words of a row per lane group) stay conflict free.
+#ifndef PDG_EFWD_X6F   // 1: the edge forward's W2 products in gemm_x6f's unbiased form (A/B only)
+#define PDG_EFWD_X6F 0
+#endif
 #ifndef PDG_MSK_STRIDE
 #define PDG_MSK_STRIDE 136
 #endif
@@ -948,7 +951,15 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     const unsigned char* ia[NI];
     ia[0] = img_m;
     if (EU) ia[NI - 1] = img_x;
+#if PDG_EFWD_X6F   // A/B build (tools/grad_err_stages.py): the W2 products in gemm_x6f's unbiased form
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      d2[u][0] = d2[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      gemm_x6f<2, X6_TERM, true>(d2[u], ws2, ia[u]);
+    }
+#else
     gemm_round<NI>(d2, ws2, ia);
+#endif
     if (!D) __syncthreads();   // the a1 tiles are read; reuse them for a2
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {

@@ -46,7 +46,7 @@ import torch
 import torch.distributed as dist
 
 from pdg.collate import DeviceGraphStore
-from pdg.dist import shard_minibatch
+from pdg.dist import shard_minibatch, sync_shardable
 from pdg.graph import index_loader
 from pdg.trainer import Trainer
 
@@ -141,6 +141,11 @@ def train(model: models.EncodeProcessDecode, train_store: DeviceGraphStore, test
         for idx in train_loader:
             if world == 1:
                 out = trainer.step(train_store.batch(idx))
+            elif dp_mode == "sync" and not sync_shardable(idx, train_store, world):
+                # a shard would be empty or edgeless (e.g. the epoch's last minibatch holds fewer graphs than
+                # ranks): rank 0 steps on the whole minibatch, the others contribute zeros (Trainer.step solo)
+                out = trainer.step(train_store.batch(idx) if rank == 0 else None, n_global_graphs=len(idx),
+                                   solo=True)
             else:   # this rank's share of the reference-ordered global minibatch, losses / B_global
                 mine = shard_minibatch(idx, train_store.n, world, rank)
                 out = trainer.step(train_store.batch(mine) if mine else None, n_global_graphs=len(idx))

@@ -47,6 +47,16 @@ def shard_minibatch(indices: Sequence[int], node_counts: Sequence[int], world: i
     return [int(indices[p]) for p in pos]
 
 
+def sync_shardable(indices: Sequence[int], store, world: int) -> bool:
+    """Whether every rank's ``shard_minibatch`` share of one minibatch has a graph with edges, as the
+    exact dp_mode="sync" LayerNorm exchange needs (every rank joins every statistic collective).
+    ``store``: per-graph node counts ``n`` and edge counts ``e`` (pdg.collate.DeviceGraphStore)."""
+    if len(indices) < world:
+        return False
+    shards = shard_graphs([store.n[i] for i in indices], world)
+    return all(sum(int(store.e[indices[p]]) for p in sh) > 0 for sh in shards)
+
+
 def allreduce_sum_(flat: torch.Tensor, group=None) -> torch.Tensor:
     """In-place sum of a flat bucket over the process group (one collective)."""
     if dist.is_available() and dist.is_initialized():

@@ -218,6 +218,9 @@ class EPDEngine:
         self._seg_info = torch.empty(4 * self._nslabs_e, dtype=torch.int32, device=self.device)
         # optional live kernel timing: name -> list of (start, end) hiptimer.Event pairs
         self.timed: dict | None = None
+        # optional backward probe (tools/grad_err_stages.py): step t -> copies of d loss / d x_t,
+        # d loss / d e_t (edges in plan order) and d loss / d aggr_t
+        self.probe: dict | None = None
 
     def variants(self) -> dict:
         """The kernel variants in effect (recorded in the bench line): every VARIANTS entry, so a new
@@ -633,6 +636,8 @@ class EPDEngine:
             segs["Wn2"].append((gz2n, d["a1n"], N))
             segs["Wn1a"].append((gz1n, d["aggr"], N))
             segs["Wn1b"].append((gz1n, d["x"], N))
+            if self.probe is not None:
+                self.probe[t] = dict(gx=gx_t.clone(), ge=ge_out.clone() if E else None, gaggr=gaggr.clone())
             gx_next, gx_t = gx_t, gx_next
             ge_next = ge_out
         # encoders

@@ -157,7 +157,7 @@ class Trainer:
         torch.distributed.all_reduce(t, group=self.pg)
         return int(t.item())
 
-    def step(self, batch, n_global_graphs: int | None = None) -> dict:
+    def step(self, batch, n_global_graphs: int | None = None, solo: bool = False) -> dict:
         """One optimisation step; returns device scalars (no host sync, except one read of the
         global row counts in dp_mode="sync", or of the global graph count when a process group is
         set and `n_global_graphs` is not given).
@@ -165,14 +165,23 @@ class Trainer:
         `n_global_graphs`: graphs in the global minibatch this rank's `batch` is a shard of (the
         loss normaliser B of gnn_train.py:193/196); defaults to the batch's own count on one device.
         `batch=None` under a process group: this rank got no graph of the minibatch; it contributes
-        zero gradient and zero loss to the collective and takes the same Adam step as every rank."""
+        zero gradient and zero loss to the collective and takes the same Adam step as every rank.
+
+        `solo=True` (dp_mode="sync", a minibatch that cannot give every rank a shard with edges, e.g. the
+        last minibatch of an epoch holding fewer graphs than ranks): ONE rank passes the whole minibatch
+        and every other rank passes None, all with solo=True.  No LayerNorm statistic is exchanged; the
+        whole-minibatch rank normalises its losses by its own graph count and the others contribute zeros,
+        so the summed bucket is exactly one device's step on the minibatch (gnn_local_stress/train.py)."""
         m = self.model
         s = stream_handle(self.device)
         f32 = dict(dtype=torch.float32, device=self.device)
+        if solo and self.pg is None:
+            raise ValueError("solo=True needs a process group")
         if batch is None:
-            if self.pg is None or self.sync:
-                raise ValueError("batch=None (an empty shard) needs a process group in dp_mode='replica'")
-            if n_global_graphs is None:
+            if self.pg is None or (self.sync and not solo):
+                raise ValueError("batch=None (an empty shard) needs a process group, and in dp_mode='sync' "
+                                 "solo=True with the whole minibatch on one rank")
+            if n_global_graphs is None and not solo:
                 n_global_graphs = self._global_graphs(0)
             self.flat_g.zero_()
             return self._update({"B": 0}, f32, s, None)
@@ -180,11 +189,15 @@ class Trainer:
         stats8 = m.stats_tensor(self.device)
         B, N = plan.n_graphs, plan.n_nodes
         Bn = B                                      # loss normaliser (gnn_train.py:193/196)
-        if self.pg is not None and not self.sync:
+        if solo:
+            if n_global_graphs is not None and int(n_global_graphs) != B:
+                raise ValueError(f"solo=True: this rank must hold the whole minibatch ({n_global_graphs} graphs), "
+                                 f"it holds {B}")
+        elif self.pg is not None and not self.sync:
             Bn = int(n_global_graphs) if n_global_graphs is not None else self._global_graphs(B)
             if Bn < B:
                 raise ValueError(f"n_global_graphs={Bn} is smaller than this rank's {B} graphs")
-        if self.sync:
+        if self.sync and not solo:
             cnt = torch.tensor([N, plan.n_edges, B], dtype=torch.float64, device=self.device)
             end = self._mark("sync_collective")
             torch.distributed.all_reduce(cnt, group=self.pg)
@@ -208,7 +221,9 @@ class Trainer:
         Every device buffer the graph reads must outlive it at a fixed address: the batch and
         its plan are held by the record, the target by the record's copy of the _gt cache entry,
         and the 8 dataset statistics (a fresh tensor per step) are copied into the captured one."""
-        if self._graph is None or self._graph[0] is not batch:
+        # keyed by (batch object, loss normaliser): 1/Bn is a captured constant, so a step on the same batch
+        # with another n_global_graphs must record a new graph, not replay the old normaliser
+        if self._graph is None or self._graph[0] is not batch or self._graph[6] != Bn:
             self._graph = None
             stats_c = stats8.clone()
             side = torch.cuda.Stream(self.device)
@@ -219,8 +234,8 @@ class Trainer:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 static = self._fwd_bwd(batch, plan, stats_c, B, N, Bn, f32, stream_handle(self.device))
-            self._graph = (batch, g, static, stats_c, plan, self._gt(batch))
-        _, g, static, stats_c, _, _ = self._graph
+            self._graph = (batch, g, static, stats_c, plan, self._gt(batch), Bn)
+        _, g, static, stats_c, _, _, _ = self._graph
         stats_c.copy_(stats8)
         g.replay()
         return dict(static)

@@ -103,3 +103,20 @@ def test_shard_minibatch_partitions_reference_batches():
                 assert p == [i for i in idx if i in p]          # the loader's relative order
             loads = [sum(counts[i] for i in p) for p in parts]
             assert max(loads) <= sum(loads) / world + max(counts[i] for i in idx)
+
+
+def test_sync_shardable_detects_empty_and_edgeless_shards():
+    """dp_mode "sync" needs every rank's share to hold edges (every rank joins every LayerNorm
+    statistic collective); a minibatch failing that (fewer graphs than ranks, or a shard of edgeless
+    graphs) is stepped whole on one rank (gnn_local_stress/train.py, Trainer.step solo)."""
+    import numpy as np
+    from pdg.dist import shard_graphs, sync_shardable
+
+    class Store:
+        n = np.array([10, 20, 30, 5])
+        e = np.array([40, 0, 90, 12])
+    assert sync_shardable([0, 1, 2, 3], Store, 2)
+    assert not sync_shardable([2], Store, 2)            # one graph, two ranks
+    assert shard_graphs([20, 5], 2) == [[0], [1]]
+    assert not sync_shardable([1, 3], Store, 2)         # rank 0's shard is the edgeless graph 1
+    assert sync_shardable([1, 3], Store, 1)

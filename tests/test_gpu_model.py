@@ -7,44 +7,51 @@
   reference's own CPU path.
 
 Tolerance (north_star: "within 1e-5 rel fp32"): relative L2 error of the
-output field and of the losses <= 1e-5.  Gradients: each parameter's gradient
-must be as close to the float64 restatement as the reference's own fp32 CPU
-result is, within a factor 2, and never worse than 3e-5 relative L2 (they
-aggregate 10^5-10^7 fp32 products through the tied steps and graph-global
-LayerNorms; DESIGN.md "Parity").  Against the golden fixtures the reference's
-own distance is host-dependent (the same fp32 ops on the generating host and
-on this one: 1.7e-5 vs 6.5e-6 on one tensor of batch2_div_s10), so there the
-factor is GOLDEN_FACTOR = 3 on the larger of the two.  Two fp32 evaluations of the HIP path with
-different kernel variants are compared at VARIANT_TOL = 1e-4: they may differ
-in a relu mask bit whose pre-activation is within rounding of zero.  Every
-gradient comparison against fp64 is appended to gpurun_out/parity.jsonl.
+output field and of the losses <= 1e-5.  Gradients against the oracle at larger
+sizes: each parameter's gradient must be as close to the float64 restatement as
+the reference's own fp32 CPU result is, within a factor 2, and never worse than
+3e-5 relative L2.  Golden cases (a few hundred nodes, up to 10
+tied steps): there a gradient's distance to fp64 is decided by which relu
+pre-activations within rounding of zero flip (one flipped bit of 3.6e6 moves
+node_encoder.0.weight's gradient by 7e-5 in the fp32 oracle on one host, 5e-6
+with the GPU's association of the same sums: tools/grad_err_stages.py,
+profiles/r05_grad_err_stages.txt), so the gradient is compared with fp64 IN THE
+GPU FORWARD'S OWN RELU REGION, within GOLDEN_FACTOR = 2 of the fp32 oracle's
+distance in its own region (floor MASKED_FLOOR), and every flipped bit must have
+a pre-activation within FLIP_EPS of zero.  Two fp32 evaluations of the HIP path
+with different kernel variants are compared at VARIANT_TOL = 1e-4: they may
+differ in such a bit.  Every gradient comparison against fp64 is appended to
+gpurun_out/parity.jsonl.
 """
 import pytest
 import torch
 
 from golden_io import CASES
-from gpu_common import dataset_stats, golden_batch, make_batch, rel
+from gpu_common import capture_forward, dataset_stats, golden_batch, gpu_relu_masks, make_batch, mask_flips, rel
 
 pytestmark = pytest.mark.gpu
 
 OUT_TOL = 1e-5
 GRAD_TOL = 3e-5
-GOLDEN_FACTOR = 3.0
+GOLDEN_FACTOR = 2.0
+MASKED_FLOOR = 1e-6
+FLIP_EPS = 1e-5
+FLIP_MAX = 8
 VARIANT_TOL = 1e-4
 
 
-def _log_grads(case, model, g64, ref32, factor=2.0):
+def _log_grads(case, model, g64, ref32, factor=2.0, floor=GRAD_TOL, extra=None):
     """Append every parameter's gradient error vs fp64 beside the fp32 reference's own to
     gpurun_out/parity.jsonl (the margins to the bound on record, not only "passed")."""
     import json
     import os
     from pathlib import Path
     errs = {n: (rel(p.grad, g64[n]), ref32[n]) for n, p in model.named_parameters()}
-    worst = max(errs, key=lambda n: errs[n][0] / max(GRAD_TOL, factor * errs[n][1]))
+    worst = max(errs, key=lambda n: errs[n][0] / max(floor, factor * errs[n][1]))
     rec = {"case": case, "worst_grad": [worst, *errs[worst]],
-           "worst_margin": errs[worst][0] / max(GRAD_TOL, factor * errs[worst][1]),
+           "worst_margin": errs[worst][0] / max(floor, factor * errs[worst][1]),
            "max_grad_err": max(e[0] for e in errs.values()),
-           "grad_tol_rule": f"max({GRAD_TOL}, {factor:g} x fp32 vs fp64)"}
+           "grad_tol_rule": f"max({floor}, {factor:g} x fp32 vs fp64)", **(extra or {})}
     out = Path(os.environ.get("GRAFT_REPO_ROOT", Path(__file__).resolve().parents[1])) / "gpurun_out"
     try:
         out.mkdir(exist_ok=True)
@@ -73,13 +80,20 @@ def _need_gpu():
 
 @pytest.mark.parametrize("case", CASES)
 def test_forward_and_grads_match_golden(case):
+    """Output and losses against the golden (the reference run on its fp32 CPU path) and fp64; every
+    gradient against fp64 evaluated in the GPU forward's own relu region ("relu
+    region"): within GOLDEN_FACTOR = 2 of the fp32 oracle's distance to fp64 in ITS own region.
+    Every relu bit where the GPU's forward and fp64's differ must have a pre-activation within
+    FLIP_EPS of zero (relative to the layer's rms), and there may be at most FLIP_MAX of them."""
     from gnn_local_stress import losses
+    from oracle.epd_oracle import ReluRegion
     g, batch = golden_batch(case)
     steps = int(g["steps"])
     model = _model(steps, g["stats"], g["params"])
     with torch.no_grad():
         out = model(batch, scale_output=True).local_stress
     assert rel(out, g["out_scaled"]) < OUT_TOL, rel(out, g["out_scaled"])
+    cap = capture_forward(model)
     pred = model(batch, scale_output=False).local_stress
     assert rel(pred.detach(), g["pred"]) < OUT_TOL
     gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
@@ -89,19 +103,30 @@ def test_forward_and_grads_match_golden(case):
     assert abs(float(total.detach()) - float(g["loss_total"])) <= OUT_TOL * abs(float(g["loss_total"]))
     model.zero_grad()
     total.backward()
-    # float64 restatement of the same step, and the fp32 reference's own distance to it: the golden's
-    # (the reference run on the generating host) and the fp32 oracle's on this host (an fp32 CPU result
-    # depends on the host: the same ops 4e-5 apart on two CPUs, DESIGN.md "Parity"); the larger is the
-    # reference's noise floor here
     st = {k: float(v) for k, v in g["stats"].items()}
-    _, _, g64 = _oracle_grads(g["params"], st, batch, steps, torch.float64, bool(g["divergence"]), float(g["penalty"]))
-    _, _, g32 = _oracle_grads(g["params"], st, batch, steps, torch.float32, bool(g["divergence"]), float(g["penalty"]))
-    ref32s = {n: max(rel(g["grads"][n], g64[n]), rel(g32[n], g64[n])) for n in g64}
-    _log_grads(f"golden:{case}", model, g64, ref32s, GOLDEN_FACTOR)
+    a = (g["params"], st, batch, steps)
+    kw = dict(divergence=bool(g["divergence"]), penalty=float(g["penalty"]))
+    r64, r32 = ReluRegion(keep=True), ReluRegion(keep=True)
+    _, _, g64 = _oracle_grads(*a, torch.float64, region=r64, **kw)
+    _, _, g32 = _oracle_grads(*a, torch.float32, region=r32, **kw)
+    gmask = gpu_relu_masks(cap["ctx"])
+    # fp64 in the GPU's relu region, and in the fp32 oracle's (its noise floor without the flips)
+    _, _, g64_gpu = _oracle_grads(*a, torch.float64, region=ReluRegion(masks=gmask), **kw)
+    m32 = {k: v > 0 for k, v in r32.keep.items()}
+    _, _, g64_32 = _oracle_grads(*a, torch.float64, region=ReluRegion(masks=m32), **kw)
+    flips = mask_flips(gmask, r64.keep)
+    n_relu = sum(v.numel() for v in gmask.values())
+    ref32 = {n: rel(g32[n], g64_32[n]) for n in g64}
+    _log_grads(f"golden:{case}", model, g64_gpu, ref32, GOLDEN_FACTOR, floor=MASKED_FLOOR,
+               extra={"flips": flips, "n_relu": n_relu,
+                      "unmasked": {n: [rel(p.grad, g64[n]), rel(g["grads"][n], g64[n]), rel(g32[n], g64[n])]
+                                   for n, p in model.named_parameters()}})
+    assert len(flips) <= FLIP_MAX and all(h <= FLIP_EPS * rms for _, _, h, rms in flips), flips
     for name, p in model.named_parameters():
-        ref32 = ref32s[name]
-        assert rel(p.grad, g64[name]) <= max(GRAD_TOL, GOLDEN_FACTOR * ref32), (name, rel(p.grad, g64[name]), ref32)
-        # direct check against the reference's fp32 gradient: bounded by the two errors to fp64
+        err = rel(p.grad, g64_gpu[name])
+        assert err <= max(MASKED_FLOOR, GOLDEN_FACTOR * ref32[name]), (name, err, ref32[name])
+        # the reference's own fp32 gradient: the two distances to fp64 bound it (a flipped bit's step
+        # in either evaluation is the same exact-arithmetic jump as in fp64)
         d = rel(p.grad, g["grads"][name])
         assert d <= max(GRAD_TOL, 1.5 * (rel(p.grad, g64[name]) + rel(g["grads"][name], g64[name]))), (name, d)
 
@@ -131,14 +156,14 @@ def test_per_graph_losses_match_oracle():
         losses.compute_divergence(pred[:5], g["op_divs"][0].cuda(), batch.nodes_types[:5], reduce_strategy="cube")
 
 
-def _oracle_grads(model_params, stats, batch, steps, dtype, divergence, penalty, scale_output=False):
+def _oracle_grads(model_params, stats, batch, steps, dtype, divergence, penalty, scale_output=False, region=None):
     from oracle import epd_oracle as O
     P = {k: v.detach().cpu().to(dtype).clone().requires_grad_(True) for k, v in model_params.items()}
     st = {k: torch.as_tensor(v).cpu().to(dtype) for k, v in stats.items()}
     b = batch
     args = (b.pos.cpu().to(dtype), b.mean_stress.cpu().to(dtype), b.nodes_types.cpu(), b.edge_index.cpu(),
             b.edge_attr.cpu().to(dtype))
-    pred = O.epd_forward(P, st, *args, steps, scale_output=scale_output)
+    pred = O.epd_forward(P, st, *args, steps, scale_output=scale_output, region=region)
     gt = (b.local_stress.cpu().to(dtype) - st["mean_local_stress"]) / st["std_local_stress"]
     if scale_output:    # loss on the unscaled field: exercises the d(unscale)/dy = std factor
         gt = b.local_stress.cpu().to(dtype)

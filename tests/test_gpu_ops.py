@@ -220,6 +220,43 @@ def test_pq_scatter_bwd(env, N, E, isolated, e_is_sum):
     assert rel(gP, refP) < TOL and rel(gQ, refQ) < TOL
 
 
+def test_pq_scatter_bwd_gz1e_from_gc_under_cancellation(env):
+    """e_is_sum with |gz1e| = 1e-4 |gz1m| (gC dominated by gz1m): the formed row gz1e = gC - gz1m is
+    exact up to the one rounding of gC (Sterbenz: gC and gz1m within a factor 2), so its absolute
+    error is <= 2^-24 |gC| (~6e-4 of |gz1e| here) and gP / gQ, whose own magnitude is |gz1m|'s, stay at
+    fp32 accuracy against the exact sums (pdg_pq_scatter_bwd)."""
+    lib, sh, _ = env
+    s = sh()
+    N, E = 5000, 30000
+    src, dst, rp = _csr(N, E, seed=4)
+    perm_src = torch.sort(src * N + dst, stable=True).indices
+    rps = torch.zeros(N + 1, dtype=torch.int64)
+    rps[1:] = torch.cumsum(torch.bincount(src, minlength=N), 0)
+    gm, ge = rnd(E, L), rnd(E, L, scale=1e-4)
+    gC = gm + ge
+    out = {}
+    rp_d, rps_d, perm_d = rp.int().cuda(), rps.int().cuda(), perm_src.int().cuda()
+    for e_is_sum, g2 in ((1, gC), (0, ge)):
+        gP, gQ = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
+        lib.pdg_pq_scatter_bwd(N, rp_d.data_ptr(), rps_d.data_ptr(), perm_d.data_ptr(), gm.data_ptr(), g2.data_ptr(),
+                               e_is_sum, gP.data_ptr(), gQ.data_ptr(), s)
+        out[e_is_sum] = (gP, gQ)
+    z = lambda: torch.zeros(N, L, dtype=torch.float64)
+    ge_x = gC.double().cpu() - gm.double().cpu()     # the exact gz1e the fp32 gC encodes
+    refP = z().index_add_(0, dst, gm.double().cpu()).index_add_(0, src, ge_x)
+    refQ = z().index_add_(0, src, gm.double().cpu()).index_add_(0, dst, ge_x)
+    gP, gQ = out[1]
+    assert rel(gP, refP) < TOL and rel(gQ, refQ) < TOL
+    # against the stored-gz1e form: the difference is the gz1e rows' rounding, <= 2^-24 |gC| per row
+    # (+ the two fp32 accumulations' own rounding, the recursive-summation bound deg * 2^-24 * sum|terms| each)
+    aC = gC.double().abs().cpu()
+    bP = z().index_add_(0, src, aC) * 2.0 ** -24
+    A = z().index_add_(0, dst, gm.double().abs().cpu()).index_add_(0, src, aC)
+    deg = (torch.bincount(dst, minlength=N) + torch.bincount(src, minlength=N)).double().unsqueeze(1)
+    dP = (out[1][0].double() - out[0][0].double()).abs().cpu()
+    assert float((dP - bP - 2.0 ** -23 * deg * A).max()) <= 0.0
+
+
 def test_ln_colsum_and_mlp2_bwd_vs_autograd(env):
     """LayerNorm(graph) -> relu -> Linear backward of one MLP tail, against torch autograd in fp64."""
     lib, sh, _ = env

@@ -147,11 +147,10 @@ def test_harness_dp_sync_world2_equals_one_device(tmp_path):
     """torchrun-style 2-rank run of the harness (gloo, one GPU) in dp_mode "sync": each rank trains
     on its share of every reference-ordered minibatch, yet the epoch losses equal the one-device run
     (the exact mode: LayerNorm statistics exchanged, losses / B_global, gradients summed); only
-    rank 0 logs and writes."""
+    rank 0 logs and writes.  5 training graphs at batch size 2: every epoch ends with a one-graph
+    minibatch, which cannot give both ranks a shard (rank 0 steps on it whole, Trainer.step solo)."""
     from gnn_local_stress import train
     cfg_path, cfg = _config(tmp_path, epochs=2)
-    cfg_path.write_text(yaml.safe_dump({**cfg, "dataset_train_csv": _dataset(tmp_path, "train4", 4, 41).as_posix(),
-                                        "dataset_test_csv": _dataset(tmp_path, "test2", 2, 42).as_posix()}))
     tr1, te1 = train.main(cfg_path.as_posix(), device="cuda:0", log=lambda *a: None,
                           results_folder=(tmp_path / "one").as_posix())
     got = _run_world2(cfg_path.as_posix(), "sync", (tmp_path / "two").as_posix())

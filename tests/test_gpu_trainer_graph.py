@@ -42,3 +42,35 @@ def test_graph_replay_equals_eager(divergence):
     assert torch.equal(g0, g1)
     assert torch.equal(p0, p1)
     assert len(set(l0)) > 1                       # the parameters moved between steps
+
+
+def test_graph_recaptured_when_the_loss_normaliser_changes():
+    """A captured step holds 1/B_global as a constant: stepping the same batch object with another
+    n_global_graphs records a new graph instead of replaying the old normaliser (world-1 gloo group,
+    replica mode), so captured and eager runs stay bit-identical."""
+    import os
+    import socket
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(s.getsockname()[1]))
+    s.close()
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        b = _batch(13)
+        runs = []
+        for capture in (False, True):
+            tr = _trainer(b, True, capture)
+            tr.pg = dist.group.WORLD
+            tr.capture = capture
+            gs = []
+            for bn in (3, 3, 6, 6, 3):
+                tr.step(b, n_global_graphs=bn)
+                gs.append(tr.flat_g.clone())
+            torch.cuda.synchronize()
+            runs.append((gs, tr.flat_p.clone()))
+        (g0, p0), (g1, p1) = runs
+        assert all(torch.equal(a, c) for a, c in zip(g0, g1))
+        assert torch.equal(p0, p1)
+    finally:
+        dist.destroy_process_group()

@@ -1,3 +1,4 @@
+// Build (not tracked in git): hipcc -O3 --offload-arch=gfx950 tools/membench2.hip -o tools/membench2
 // Streaming ceiling for the exact row mix of the edge forward (not part of the library; VERDICT r03
 // "reconcile the streaming ceiling"): per edge R streamed 512-B row reads, G gathered 512-B rows from
 // two node-sized tables (P / Q: N = E / 6 rows each, the edge forward's P[dst], Q[src], P[src], Q[dst]
