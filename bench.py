@@ -272,6 +272,21 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
     }
 
 
+def compulsory_bytes(work: dict, N: int, E: int) -> dict:
+    """Per-launch bytes with every GATHERED row priced once per node instead of once per edge (the
+    compulsory traffic when each node's row is fetched from HBM once and every later use is a cache
+    hit): the edge forward's 4 P / Q gathers (4 N rows instead of 4 E; 2 with no edge update) and the
+    fused edge backward's gaggr[dst] (N instead of E).  kernel_work's figure prices a gather per edge
+    (SURVEY §8d); `frac_compulsory` in the roofline is this figure's rate, the lower of the two."""
+    row = 4 * L
+    out = {k: nb for k, (_, nb) in work.items()}
+    if "edge_fwd" in out:   # the timed "edge_fwd" launches are the steps with an edge update: 4 gathers
+        out["edge_fwd"] = work["edge_fwd"][1] - 4 * E * row + 4 * N * row
+    if "edge_bwd" in out:
+        out["edge_bwd"] = work["edge_bwd"][1] - E * row + N * row
+    return out
+
+
 def pmc_file(tree: str | None = None):
     """(path, None) of the newest profiles/rNN_pmc_traffic.json measured on this tree (its "_meta"
     "tree" equals tree_hash()), or (None, reason).  PMC bytes of another tree would price a kernel's
@@ -345,9 +360,10 @@ def load_sq(path) -> dict:
     return out
 
 
-def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None, pmc_source=None):
+def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None, pmc_source=None, comp=None):
     nlaunch = nlaunch or {}
     terms, nbytes = work[k]
+    cbytes = (comp or {}).get(k, nbytes)
     t = kt[k]
     flops = sum(f for f, _ in terms)
     t_peak = sum(f / pk for f, pk in terms)     # matrix-core time at peak rate
@@ -364,6 +380,9 @@ def roofline(k, work, kt, ktot, step_s, pmc, nlaunch=None, pmc_source=None):
             # real DRAM rate: the PMC bytes of a launch (profiles/, same tree when traffic_tree matches)
             # over this run's event-timed launch average, against 8 TB/s
             "frac_pmc": round(traffic / t / PEAK_HBM, 4) if traffic else None,
+            # every gathered row priced once per node (compulsory_bytes): the honest lower bound of the
+            # algorithmic rate beside `frac`, which prices the cache-served gathers at HBM cost
+            "bytes_compulsory_per_launch": cbytes, "frac_compulsory": round(cbytes / t / PEAK_HBM, 4),
             "traffic_source": (f"profiles/{Path(pmc_source).name}: 2*FETCH_SIZE+WRITE_SIZE per dispatch"
                                if k in pmc and pmc_source else None),
             "flops_per_launch": flops, "bytes_per_launch": nbytes, "frac_mfma": round(f_mfma, 4),
@@ -500,6 +519,7 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     # the fused message sums run in inference only unless PDG_SEG_SUMS_TRAIN=1 (engine.py:253)
     seg = getattr(eng, "seg_sums", False) if infer else getattr(eng, "seg_sums_train", False)
     work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg, fused and getattr(eng, "gz1e_from_gc", False))
+    comp = compulsory_bytes(work, N, E)
     pmc_path, pmc_reason = pmc_file() if with_pmc else (None, "not collected for this config")
     pmc = load_pmc(fused, pmc_path)
     sq_path, sq_reason = sq_file() if with_pmc else (None, "not collected for this config")
@@ -523,10 +543,10 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
                    "final_loss": round(loss, 6), "hip_graph_steps": graph_steps,
                    "per_rank": per_rank_rec},
         "kernel_variants": eng.variants(),
-        "roofline": roofline(dominant, work, kt, ktot, step_s, pmc, nlaunch, pmc_path),
-        "roofline_gather_scatter": [roofline(k, work, kt, ktot, step_s, pmc, nlaunch, pmc_path)
+        "roofline": roofline(dominant, work, kt, ktot, step_s, pmc, nlaunch, pmc_path, comp),
+        "roofline_gather_scatter": [roofline(k, work, kt, ktot, step_s, pmc, nlaunch, pmc_path, comp)
                                     for k in ("segment_sum", "pq_scatter_bwd") if k in kt],
-        "roofline_node_net": (roofline("node_net", work, kt, ktot, step_s, pmc, nlaunch, pmc_path)
+        "roofline_node_net": (roofline("node_net", work, kt, ktot, step_s, pmc, nlaunch, pmc_path, comp)
                               if "node_net" in kt else None),
         "traffic_null_reason": pmc_reason,
         # MFMA busy from rocprofv3 SQ counters of this tree (tools/sq_pass.sh), beside each roofline's

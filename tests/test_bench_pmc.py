@@ -71,3 +71,19 @@ def test_edge_backward_bytes_follow_the_gz1e_variant():
     # the unfused edge backward does not depend on it
     assert (bench.kernel_work(False, N, E, S, slab, False, e_sum=True)["edge_bwd"]
             == bench.kernel_work(False, N, E, S, slab, False, e_sum=False)["edge_bwd"])
+
+
+def test_compulsory_bytes_of_the_edge_forward_at_config_2():
+    """frac_compulsory prices each gathered P / Q row once per node: at config 2 (N = 40,328,
+    E = 239,744) the edge forward's 7 streamed rows per edge + 4 gathered rows per node + the int32
+    src / dst come to 943.8 MB per launch (roofline table), against 1,352.2 MB with the
+    gathers priced per edge."""
+    N, E, S, slab = 40328, 239744, 10, 256 * (128 * 128 + 128) * 4
+    work = bench.kernel_work(False, N, E, S, slab, True, e_sum=True)
+    comp = bench.compulsory_bytes(work, N, E)
+    assert round(work["edge_fwd"][1] / 1e6, 1) == 1352.2
+    assert round(comp["edge_fwd"] / 1e6, 1) == 943.8
+    assert comp["edge_bwd"] == work["edge_bwd"][1] - (E - N) * 512
+    assert comp["node_net"] == work["node_net"][1]
+    r = bench.roofline("edge_fwd", work, {"edge_fwd": 2e-4}, {"edge_fwd": 2e-3}, 8e-3, {}, {"edge_fwd": 10}, None, comp)
+    assert r["frac_compulsory"] == round(comp["edge_fwd"] / 2e-4 / bench.PEAK_HBM, 4) < r["frac"]
