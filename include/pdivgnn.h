@@ -359,6 +359,22 @@ int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* 
                      const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
                      const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,
                      int accumulate, int slab_init, void* stream);
+/* pdg_edge_bwd_w2 + pdg_edge_gout_wc in one pass (the backward of both edge_net evaluations of one
+ * message-passing step, models.py:219-225 / :233-238): gz1m, gC (= gz1m + gz1e; gz1e is not stored),
+ * ge_out = [ge_next +] WcT gC, slabs_w2 += the dW2 / db2 sums, slabs_wc += the dWc / db1 sums, and the
+ * column sums / pairs of the LayerNorm that produced e (a2ln, st_ln, ln_g_e -> ln_partials, ln_pairs,
+ * accumulate) as pdg_edge_gout_wc.  ln_g_msg: the edge_net LayerNorm weight (both branches' gz2).
+ * ge_next == NULL: the message branch only; gC must then be the gz1m pointer.  gz1m / gC / ge_out equal
+ * the split pair's bit for bit; the slab weight sums too, the bias and column sums add in another order.
+ * A weight-specialised block per slab (4 waves on W2, 4 on Wc; pdg_ebw.hip), 157 KB of LDS. */
+int pdg_edge_bwd_fused(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
+                       const float* a2m, const float* a1m, const float* a2e, const float* a1e,
+                       const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
+                       const pdg_ln_bwd* lb_e, const float* ln_g_msg, const float* W2T, const float* WcT,
+                       const float* e, const float* a2ln, const pdg_ln_stat* st_ln, const float* ln_g_e,
+                       float* gz1m, float* gC, float* ge_out, float* slabs_w2, float* slabs_wc, int nslabs,
+                       double* ln_partials, double* ln_pairs, const double* pairs_m, int npairs_m,
+                       const double* pairs_e, int npairs_e, int slab_init, int accumulate, void* stream);
 
 /* Mesh graph on the device (pdg_graph.hip): FaceToEdge of a triangle
  * mesh (convert_utils.py:47-60), edge lengths (datasets.py:182-188) and, when `periodic`,

@@ -518,6 +518,476 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
   }
 }
 
+// ============================================================================ fused edge backward
+// pdg_edge_bwd_fused: pdg_edge_bwd_w2 + pdg_edge_gout_wc in one pass over the edge rows, as a weight-
+// specialised block.  The split pair re-read gC and ge_next from HBM in
+// the Wc pass (13 E-row passes per call); here the Wc work takes gC from an LDS image the W2 work just
+// wrote, and ge_next from an LDS tile the W2 work's staging filled: 11 passes (reads gaggr[dst], a2m, a1m,
+// ge_next, a2e, a1e, e, a2ln; writes gz1m, gC, ge_out).
+//
+// No wave holds both 128x128 weights: waves 0-3 (group A) own W2^T output features 32 wl + [0, 32) (hi /
+// mid bf16 terms in registers, the lo term in LDS) and the dW2 slab rows 32 wl + [0, 32); waves 4-7
+// (group B) own Wc^T and dWc likewise (all three terms in registers) and the column sums of the
+// LayerNorm that produced e.  Per 16-row round k, two barriers:
+//   phase 1  A: dW2 += gz2m^T a1m + gz2e^T a1e; gz1 = (W2^T gz2) [a1 > 0]; gC = gz1m + gz1e -> HBM and
+//               the gC image                                  (4 product units)
+//            B: stage round k's e image and xhat(a2ln) tile; issue round k+1's e / a2ln loads
+//   phase 2  B: dWc += gC^T e; ge_out = ge_next + Wc^T gC -> HBM; LayerNorm column sums   (2 units)
+//            A: stage round k+1 (gz2 = LN_bwd(gy) [a2 > 0], a1 images, masks, ge_next tile); issue
+//               round k+2's loads
+// so each SIMD runs one wave of each group, the matrix work of one overlapping the other's staging.
+// Per-element MFMA order as in the split pair: gz1m / gC / ge_out and the dW2 / dWc weight sums are
+// bitwise theirs; the bias and LayerNorm column sums add in another order.
+namespace {
+
+constexpr int EBF_LO = 4 * 4 * 2 * 64 * 16;   // lo terms of one weight's four wave slices in LDS (32 KB)
+// LDS: A images + masks, the gC and e images, the ge_next tiles (2) and the xhat tile, the W2^T lo terms
+constexpr int EBF_SHM = 4 * IMG16 + 2 * MSK16 + 2 * IMG16 + 2 * R16 * OT_STRIDE * 4 + 2 * EBF_LO;   // 156.75 KB
+
+// dW += G^T X over one 16-row image pair for a 4-wave group: wave wl owns o in 32 wl + [0, 32) and all
+// 128 i as four 32x32 accumulators (wgrad_round's operand reads and per-accumulator MFMA order).
+__device__ __forceinline__ void wgrad_round_g4(f32x16 (&acc)[4], const unsigned char* gimg, const unsigned char* ximg,
+                                               int wl) {
+  const int l = lane_id(), h = l >> 5;
+  const int lrow = 8 * h + ((l & 15) >> 2);
+  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
+  bf16x8 A[3];
+  const int g0 = x6_addr(lrow, lcolb + 64 * wl), g1 = x6_addr(lrow + 4, lcolb + 64 * wl);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) A[p] = x6_operand(gimg + p * T16, g0, g1);
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    bf16x8 B[3];
+    const int x0 = x6_addr(lrow, lcolb + 64 * b), x1 = x6_addr(lrow + 4, lcolb + 64 * b);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) B[p] = x6_operand(ximg + p * T16, x0, x1);
+    f32x16 t = acc[b];
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], t, 0, 0, 0);
+    acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], t, 0, 0, 0);
+  }
+}
+
+// Two 16-feature W^T slices (output blocks 2 wl, 2 wl + 1); lo terms either in `a[..][2]` or in LDS.
+struct WSlice2 {
+  bf16x8 a[2][4][3];
+};
+
+// d[u][b] = W^T block (2 wl + b) x image u (16 rows): gemm_round<NI, 1, T16>'s chain per output block.
+// LO: the lo-term A operands come from LDS (lo + ((ks * 2 + b) * 64 + lane) * 16), not from ws.
+template <int NI, bool LO>
+__device__ __forceinline__ void gemm_round_g4(f32x4 (&d)[NI][2], const WSlice2& ws, const unsigned char* lo,
+                                              const unsigned char* const (&img)[NI]) {
+  const int l = lane_id(), n = l & 15, kg = l >> 4;
+#pragma unroll
+  for (int u = 0; u < NI; ++u)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) d[u][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    bf16x8 wl2[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+      wl2[b] = LO ? *reinterpret_cast<const bf16x8*>(lo + ((ks * 2 + b) * 64 + l) * 16) : ws.a[b][ks][2];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+      const int off = x6_addr(n, 64 * ks + 16 * kg);
+      bf16x8 B[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(img[u] + p * T16 + off);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        f32x4 t = d[u][b];
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl2[b], B[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][1], B[1], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][0], B[2], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][1], B[0], t, 0, 0, 0);
+        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][0], B[1], t, 0, 0, 0);
+        d[u][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][0], B[0], t, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // one image operand live at a time (register bound)
+    }
+  }
+}
+
+// The two slices of output blocks 2 wl, 2 wl + 1 of W^T (row-major, out x in); with LO the lo terms go
+// to this wave's part of the LDS array instead (read back by gemm_round_g4<.., true>).
+template <bool LO>
+__device__ __forceinline__ void load_wslice2(WSlice2& ws, const float* __restrict__ WT, int wl, unsigned char* lo) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    WSlice s;
+    load_wslice(s, WT, 2 * wl + b);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      ws.a[b][ks][0] = s.a[ks][0];
+      ws.a[b][ks][1] = s.a[ks][1];
+      if (LO)
+        *reinterpret_cast<bf16x8*>(lo + ((ks * 2 + b) * 64 + lane_id()) * 16) = s.a[ks][2];
+      else
+        ws.a[b][ks][2] = s.a[ks][2];
+    }
+  }
+}
+
+// slab rows 32 wl + [0, 32), all 128 columns, += acc (init: =) — slab_accumulate's element map for a
+// 4-wave group (ib = 0, four column blocks); every load before any store.
+__device__ __forceinline__ void slab_accumulate_g4(float* __restrict__ slab, const f32x16 (&acc)[4], int wl, int init) {
+  const int l = lane_id(), h = l >> 5, c = l & 31;
+  const int ob = 32 * wl;
+  float old[4][16];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h, i = 32 * b + c;
+      old[b][r] = init ? 0.f : slab[o * L + i];
+    }
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h, i = 32 * b + c;
+      slab[o * L + i] = old[b][r] + acc[b][r];
+    }
+}
+
+}  // namespace
+
+// LDS map of the fused kernel (EBF_SHM): A images gz2m, a1m, gz2e, a1e (16-row bf16x6), the masks, the gC
+// and e images, the ge_next tiles (by round parity), the lo terms of W2^T (group A) and Wc^T (group B)
+struct EbfLds {
+  unsigned char *img_gm, *img_am, *img_ge, *img_ae, *msk_m, *msk_e, *img_c, *img_e;
+  float* t_gn;
+  unsigned char *lo_a, *lo_b;
+  __device__ explicit EbfLds(unsigned char* sm) {
+    img_gm = sm;
+    img_am = sm + IMG16;
+    img_ge = sm + 2 * IMG16;
+    img_ae = sm + 3 * IMG16;
+    msk_m = sm + 4 * IMG16;
+    msk_e = msk_m + MSK16;
+    img_c = msk_e + MSK16;
+    img_e = img_c + IMG16;
+    t_gn = reinterpret_cast<float*>(img_e + IMG16);
+    lo_a = reinterpret_cast<unsigned char*>(t_gn + 2 * R16 * OT_STRIDE);
+    lo_b = lo_a + EBF_LO;
+  }
+};
+
+// Reduce-scatter of per-lane values over the lanes that differ in the lane-index bits of MASKS (a
+// butterfly; each step sends half of the values still held to the partner and keeps the other half):
+// afterwards v[0 .. N >> steps) of a lane hold the sums of the entries whose index's high bits equal the
+// lane's bits, in order (step s keeps the upper half where the lane's s-th mask bit is set).
+template <int N, int M, int SZ>
+__device__ __forceinline__ void rs_step(float (&v)[SZ], int l) {
+  static_assert(N <= SZ, "rs_step: more entries than the array holds");
+  const bool up = (l & M) != 0;
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) {
+    const float keep = up ? v[i + N / 2] : v[i], send = up ? v[i] : v[i + N / 2];
+    v[i] = keep + __shfl_xor(send, M);
+  }
+}
+
+// Group A (waves 0-3): the message branch and the W2 side.  Its own function, so that none of its values
+// is live in group B's code (one body holding both groups' loops made the register allocation the union of
+// both).  Stages gz2m = LN_bwd(gaggr[dst]) [a2m > 0], a1m and its mask; in phase 1 the dW2 and W2^T
+// products for both branches.
+template <bool EU>
+__device__ __forceinline__ void ebf_group_a(
+    const EbfLds& S, int r0, int r1, int nr, const int* __restrict__ dst, const float* __restrict__ gaggr,
+    const float* __restrict__ a2m, const float* __restrict__ a1m, const pdg_ln_stat* __restrict__ stm_p,
+    const pdg_ln_bwd* __restrict__ lbm_p, const float* __restrict__ lg, const float* __restrict__ W2T,
+    float* __restrict__ gz1m, float* __restrict__ gC, float* __restrict__ slab, const double* __restrict__ pm, int npm,
+    int slab_init, float* red_b2, float* red_b1) {
+  const int l = lane_id(), wl = wave_id() & 3;
+  const int srow = (threadIdx.x & 255) >> 4, sc = threadIdx.x & 15;   // staged row, columns 8 sc .. +7
+  unsigned char* lo = S.lo_a + wl * (EBF_LO / 4);
+  const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
+  WSlice2 ws;
+  f32x16 acc[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  f32x4 pg[2], pa2[2], pa1[2];   // one prefetched round
+  int dn;
+  // bias sums, reduce-scattered every round: db2 part of features 8 sc + 4 bit5(l) + 2 bit4(l) + {0, 1}
+  // over this wave's 4 staged rows (the split pair's message + edge-update gz2 rows; B adds gz2e's); db1
+  // entry (l & 15) >> 1 of the product layout's 8 (block b = idx >> 2, feature 4 (l >> 4) + (idx & 3))
+  float b2s[2] = {0.f, 0.f}, b1s = 0.f;
+  const __amdgpu_buffer_rsrc_t out_m = rows_rsrc(gz1m, r0, r1);
+  const __amdgpu_buffer_rsrc_t out_c = rows_rsrc(EU || gC != gz1m ? gC : nullptr, r0, r1);
+  auto issue = [&](int base) {
+    const size_t rc = (size_t)clamp_row(base + srow, r1) * L + 8 * sc;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pg[h] = *reinterpret_cast<const f32x4*>(gaggr + (size_t)dn * L + 8 * sc + 4 * h);
+      pa2[h] = *reinterpret_cast<const f32x4*>(a2m + rc + 4 * h);
+      pa1[h] = *reinterpret_cast<const f32x4*>(a1m + rc + 4 * h);
+    }
+  };
+  // the round at `base` from the prefetch set; rows past r1 get gz2 = 0, which zeroes every product they enter
+  auto stage = [&](int base, const pdg_ln_bwd& lbm) {
+    const bool ok = base + srow < r1;
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cg = 2 * sc + h;
+      const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+      const f32x4 zm = ok ? ln_relu_bwd4(pg[h], pa2[h], stm, lbm, g4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * h + j] = zm[j];
+      img_store4<T16>(S.img_gm, srow, cg, zm);
+      img_store4<T16>(S.img_am, srow, cg, pa1[h]);
+      *reinterpret_cast<unsigned*>(S.msk_m + srow * MSK_STRIDE + 4 * cg) = relu_mask4(pa1[h]);
+    }
+    rs_step<8, 32>(v, l);
+    rs_step<4, 16>(v, l);
+    b2s[0] += v[0];
+    b2s[1] += v[1];
+  };
+  dn = dst[clamp_row(r0 + srow, r1)];   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
+  issue(r0);
+  dn = dst[clamp_row(r0 + R16 + srow, r1)];
+  load_wslice2<true>(ws, W2T, wl, lo);
+  const pdg_ln_bwd lbm = lnb_resolve(lbm_p, pm, npm, stm_p);
+  stage(r0, lbm);
+  issue(r0 + R16);
+  dn = dst[clamp_row(r0 + 2 * R16 + srow, r1)];
+  __syncthreads();   // round 0's images (B stages the edge-update ones) complete
+  for (int k = 0; k < nr; ++k) {
+    const int base = r0 + k * R16, r = l & 15, row = base + r;
+    // ---- phase 1: dW2, the W2^T products, gz1m / gC to HBM and gC into the image
+    wgrad_round_g4(acc, S.img_gm, S.img_am, wl);
+    if (EU) wgrad_round_g4(acc, S.img_ge, S.img_ae, wl);
+    constexpr int NI = EU ? 2 : 1;
+    f32x4 d[NI][2];
+    const unsigned char* imgs[NI];
+    imgs[0] = S.img_gm;
+    if (EU) imgs[NI - 1] = S.img_ge;
+    gemm_round_g4<NI, true>(d, ws, lo, imgs);
+    float v[8];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int oc = 32 * wl + 16 * b + 4 * (l >> 4);
+      const unsigned mm = *reinterpret_cast<const unsigned*>(S.msk_m + r * MSK_STRIDE + oc);
+      f32x4 zm;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) zm[j] = (mm >> (8 * j)) & 1u ? d[0][b][j] : 0.f;
+      f32x4 c = zm;
+      if (EU) {
+        const unsigned me = *reinterpret_cast<const unsigned*>(S.msk_e + r * MSK_STRIDE + oc);
+        f32x4 ze;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ze[j] = (me >> (8 * j)) & 1u ? d[NI - 1][b][j] : 0.f;
+        c = zm + ze;
+      }
+      rows_store4(out_m, row - r0, oc, zm);
+      rows_store4(out_c, row - r0, oc, c);
+      img_store4<T16>(S.img_c, r, oc >> 2, c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * b + j] = c[j];   // rows past r1: c = 0 (their gz2 rows are zero)
+    }
+    rs_step<8, 8>(v, l);
+    rs_step<4, 4>(v, l);
+    rs_step<2, 2>(v, l);
+    b1s += v[0] + __shfl_xor(v[0], 1);
+    __syncthreads();   // gC image complete (B reads it in phase 2); the A images are read
+    // ---- phase 2: the next round's message images (its rows have had phase 1 to land), the round after's loads
+    if (k + 1 < nr) {
+      stage(base + R16, lbm);
+      issue(base + 2 * R16);
+      dn = dst[clamp_row(base + 3 * R16 + srow, r1)];
+    }
+    __syncthreads();   // the next round's images complete
+  }
+  slab_accumulate_g4(slab, acc, wl, slab_init);
+  // db2 parts: [wave][128] (B adds its own rows below: [4 + wave]); db1: one entry per feature
+  red_b2[wl * L + 8 * sc + 4 * ((l >> 5) & 1) + 2 * ((l >> 4) & 1)] = b2s[0];
+  red_b2[wl * L + 8 * sc + 4 * ((l >> 5) & 1) + 2 * ((l >> 4) & 1) + 1] = b2s[1];
+  if ((l & 1) == 0) {
+    const int idx = (l & 15) >> 1;
+    red_b1[32 * wl + 16 * (idx >> 2) + 4 * (l >> 4) + (idx & 3)] = b1s;
+  }
+}
+
+// Group B (waves 4-7): the edge-update branch and the Wc side.  Stages gz2e = LN_bwd(ge_next) [a2e > 0],
+// a1e and its mask, the ge_next tile and the e image; in phase 2 dWc, Wc^T gC, ge_out = ge_next + Wc^T gC
+// and the column sums of the LayerNorm that produced e (its input a2ln read in the product layout, xhat
+// formed per element; the sums reduce-scattered over the 16 row lanes every round, fp64 across rounds).
+template <bool EU>
+__device__ __forceinline__ void ebf_group_b(
+    const EbfLds& S, int r0, int r1, int nr, const float* __restrict__ ge_next, const float* __restrict__ a2e,
+    const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ ste_p, const pdg_ln_bwd* __restrict__ lbe_p,
+    const float* __restrict__ lg, const double* __restrict__ pe, int npe, const float* __restrict__ WcT,
+    const float* __restrict__ e, const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p,
+    float* __restrict__ ge_out, float* __restrict__ slab, int slab_init, float* red_b2, double* ln_row) {
+  const int l = lane_id(), wl = wave_id() & 3;
+  const int srow = (threadIdx.x & 255) >> 4, sc = threadIdx.x & 15;
+  unsigned char* lo = S.lo_b + wl * (EBF_LO / 4);
+  const LNStat stln = *reinterpret_cast<const LNStat*>(stln_p);
+  WSlice2 ws;
+  f32x16 acc[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
+  f32x4 pge[2], pa2e[2], pa1e[2], pe_[2], pl[2];
+  float b2s[2] = {0.f, 0.f};   // gz2e's db2 part (as group A's)
+  double cs = 0.0;             // LayerNorm column sum entry (l & 15) of this lane's 16: see below
+  const __amdgpu_buffer_rsrc_t out_g = rows_rsrc(ge_out, r0, r1);
+  auto issue_u = [&](int base) {   // the edge-update rows (whole rows, staged for A's next round)
+    const size_t rc = (size_t)clamp_row(base + srow, r1) * L + 8 * sc;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pge[h] = *reinterpret_cast<const f32x4*>(ge_next + rc + 4 * h);
+      pa2e[h] = *reinterpret_cast<const f32x4*>(a2e + rc + 4 * h);
+      pa1e[h] = *reinterpret_cast<const f32x4*>(a1e + rc + 4 * h);
+    }
+  };
+  auto issue_e = [&](int base) {   // e (whole rows, for the image) and a2ln (this lane's product-layout rows)
+    const size_t rc = (size_t)clamp_row(base + srow, r1) * L + 8 * sc;
+    const size_t rp = (size_t)clamp_row(base + (l & 15), r1) * L + 32 * wl + 4 * (l >> 4);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      pe_[h] = *reinterpret_cast<const f32x4*>(e + rc + 4 * h);
+      pl[h] = *reinterpret_cast<const f32x4*>(a2ln + rp + 16 * h);
+    }
+  };
+  auto stage_u = [&](int base, int par, const LNStat& ste, const pdg_ln_bwd& lbe) {
+    const bool ok = base + srow < r1;
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int cg = 2 * sc + h;
+      const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+      const f32x4 ze = ok ? ln_relu_bwd4(pge[h], pa2e[h], ste, lbe, g4) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * h + j] = ze[j];
+      img_store4<T16>(S.img_ge, srow, cg, ze);
+      img_store4<T16>(S.img_ae, srow, cg, pa1e[h]);
+      *reinterpret_cast<unsigned*>(S.msk_e + srow * MSK_STRIDE + 4 * cg) = relu_mask4(pa1e[h]);
+      *reinterpret_cast<f32x4*>(S.t_gn + (par * R16 + srow) * OT_STRIDE + 4 * cg) = pge[h];
+    }
+    rs_step<8, 32>(v, l);
+    rs_step<4, 16>(v, l);
+    b2s[0] += v[0];
+    b2s[1] += v[1];
+  };
+  const LNStat ste = EU ? *reinterpret_cast<const LNStat*>(ste_p) : stln;
+  pdg_ln_bwd lbe;
+  if (EU) issue_u(r0);
+  issue_e(r0);
+  load_wslice2<true>(ws, WcT, wl, lo);
+  if (EU) {
+    lbe = lnb_resolve(lbe_p, pe, npe, ste_p);
+    stage_u(r0, 0, ste, lbe);
+    issue_u(r0 + R16);
+  }
+  __syncthreads();   // round 0's images complete
+  for (int k = 0; k < nr; ++k) {
+    const int base = r0 + k * R16, r = l & 15, row = base + r;
+    // ---- phase 1: this round's e image (rows past r1 zero, as the split Wc pass)
+    {
+      const bool ok = base + srow < r1;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        img_store4<T16>(S.img_e, srow, 2 * sc + h, ok ? pe_[h] : f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+    __syncthreads();   // gC and e images complete; A's edge-update images and masks are read
+    // ---- phase 2: dWc, Wc^T gC, ge_out = ge_next + Wc^T gC, LayerNorm column sums
+    wgrad_round_g4(acc, S.img_c, S.img_e, wl);
+    f32x4 d[1][2];
+    const unsigned char* imgs[1] = {S.img_c};
+    gemm_round_g4<1, true>(d, ws, lo, imgs);
+    const bool ok = row < r1;
+    float v[16];   // entry 8 b + 2 j + {0: go, 1: go xhat}
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int oc = 32 * wl + 16 * b + 4 * (l >> 4);
+      f32x4 go = d[0][b];
+      if (EU) go = *reinterpret_cast<const f32x4*>(S.t_gn + ((k & 1) * R16 + r) * OT_STRIDE + oc) + d[0][b];
+      rows_store4(out_g, row - r0, oc, go);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xv = div_den(pl[b][j] - stln.mean, stln.den, stln.rstd);
+        v[8 * b + 2 * j] = ok ? go[j] : 0.f;
+        v[8 * b + 2 * j + 1] = ok ? go[j] * xv : 0.f;
+      }
+    }
+    rs_step<16, 8>(v, l);
+    rs_step<8, 4>(v, l);
+    rs_step<4, 2>(v, l);
+    rs_step<2, 1>(v, l);
+    cs += (double)v[0];
+    // the next rounds' rows: e / a2ln now; the edge-update images of A's next round, their loads two ahead
+    issue_e(base + R16);
+    if (EU && k + 1 < nr) {
+      stage_u(base + R16, (k + 1) & 1, ste, lbe);
+      issue_u(base + 2 * R16);
+    }
+    __syncthreads();   // A's next images complete; gC / e images and the ge_next tile are read
+  }
+  slab_accumulate_g4(slab, acc, wl, slab_init);
+  red_b2[(4 + wl) * L + 8 * sc + 4 * ((l >> 5) & 1) + 2 * ((l >> 4) & 1)] = b2s[0];
+  red_b2[(4 + wl) * L + 8 * sc + 4 * ((l >> 5) & 1) + 2 * ((l >> 4) & 1) + 1] = b2s[1];
+  {   // lane entry (l & 15) = 8 b + 2 j + gx of feature 32 wl + 16 b + 4 (l >> 4) + j
+    const int idx = l & 15, b = idx >> 3, j = (idx >> 1) & 3, gx = idx & 1;
+    ln_row[gx * L + 32 * wl + 16 * b + 4 * (l >> 4) + j] = cs;
+  }
+}
+
+template <bool EU>
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_fused_kernel(
+    const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
+    const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
+    const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ stm_p, const pdg_ln_stat* __restrict__ ste_p,
+    const pdg_ln_bwd* __restrict__ lbm_p, const pdg_ln_bwd* __restrict__ lbe_p, const float* __restrict__ lg,
+    const float* __restrict__ W2T, const float* __restrict__ WcT, const float* __restrict__ e,
+    const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, const float* __restrict__ ln_g,
+    float* __restrict__ gz1m, float* __restrict__ gC, float* __restrict__ ge_out, float* __restrict__ slabs_w2,
+    float* __restrict__ slabs_wc, double* __restrict__ ln_part, double* __restrict__ ln_pairs, int E,
+    const double* __restrict__ pm, int npm, const double* __restrict__ pe, int npe, int slab_init, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  int r0, r1;
+  block_rows(E, r0, r1);
+  const int nr = (r1 - r0 + R16 - 1) / R16;
+  // end-of-kernel reduction space (the images are dead by then)
+  float* red_b2 = reinterpret_cast<float*>(sm);                 // [8 waves][128]: db2 parts
+  float* red_b1 = red_b2 + 8 * L;                               // [128]: db1
+  double* ln_row = reinterpret_cast<double*>(red_b1 + L);       // [256] column-sum row + lnb_emit's scratch [256]
+#ifndef PDG_EBF_ONLY   // register-pressure probe builds: 1 compiles only group A's code, 2 only B's
+#define PDG_EBF_ONLY 0
+#endif
+  const EbfLds S(sm);
+  if (PDG_EBF_ONLY != 2 && (PDG_EBF_ONLY == 1 || wave_id() < 4))
+    ebf_group_a<EU>(S, r0, r1, nr, dst, gaggr, a2m, a1m, stm_p, lbm_p, lg, W2T, gz1m, gC,
+                    slabs_w2 + (size_t)blockIdx.x * WSLAB, pm, npm, slab_init, red_b2, red_b1);
+  else if (PDG_EBF_ONLY != 1)
+    ebf_group_b<EU>(S, r0, r1, nr, ge_next, a2e, a1e, ste_p, lbe_p, lg, pe, npe, WcT, e, a2ln, stln_p, ge_out,
+                    slabs_wc + (size_t)blockIdx.x * WSLAB, slab_init, red_b2, ln_row);
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < L) {   // db2: the 8 waves' parts in order (message rows: waves 0-3, edge-update rows: 4-7)
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s += red_b2[g * L + t];
+    float* bp = slabs_w2 + (size_t)blockIdx.x * WSLAB + L * L + t;
+    *bp = (slab_init ? 0.f : *bp) + s;
+  } else if (t < 2 * L) {   // db1
+    const int f = t - L;
+    float* bp = slabs_wc + (size_t)blockIdx.x * WSLAB + L * L + f;
+    *bp = (slab_init ? 0.f : *bp) + red_b1[f];
+  }
+  __syncthreads();
+  lnb_emit(ln_row, ln_g, ln_part, accumulate, ln_pairs, ln_row + 2 * L);
+}
+
 // ============================================================================ edge encoder backward
 // Backward of edge_encoder = Lin(1 -> 128) ReLU Lin(128 -> 128) ReLU LN (models.py:268-274) over the
 // E scalar inputs e_in, upstream gradient gy = d loss / d e_0 (ge_out of the first step):
@@ -1812,6 +2282,45 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
                        a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g, W2T, gz1m, gz1e, gC, slabs, n_edges, pairs_m,
                        npairs_m, pairs_m, npairs_m, slab_init);
   PDG_CHECK_LAUNCH("pdg_edge_bwd_w2");
+  return PDG_OK;
+}
+
+extern "C" int pdg_edge_bwd_fused(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
+                                  const float* a2m, const float* a1m, const float* a2e, const float* a1e,
+                                  const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
+                                  const pdg_ln_bwd* lb_e, const float* ln_g_msg, const float* W2T, const float* WcT,
+                                  const float* e, const float* a2ln, const pdg_ln_stat* st_ln, const float* ln_g_e,
+                                  float* gz1m, float* gC, float* ge_out, float* slabs_w2, float* slabs_wc, int nslabs,
+                                  double* ln_partials, double* ln_pairs, const double* pairs_m, int npairs_m,
+                                  const double* pairs_e, int npairs_e, int slab_init, int accumulate, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_fused: n_edges must be > 0");
+  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs_w2 && slabs_wc, "pdg_edge_bwd_fused: bad slabs");
+  PDG_CHECK_ARG(dst && gaggr && a2m && a1m && st_m && (lb_m || pairs_m) && ln_g_msg && W2T && WcT && e && a2ln &&
+                    st_ln && ln_g_e && gz1m && gC && ge_out && ln_partials,
+                "pdg_edge_bwd_fused: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(ln_g_msg) &&
+                    PDG_ALIGNED(W2T) && PDG_ALIGNED(WcT) && PDG_ALIGNED(e) && PDG_ALIGNED(a2ln) && PDG_ALIGNED(gz1m) &&
+                    PDG_ALIGNED(gC) && PDG_ALIGNED(ge_out) && PDG_ALIGNED(slabs_w2) && PDG_ALIGNED(slabs_wc),
+                "pdg_edge_bwd_fused: misaligned pointer");
+  const bool eu = ge_next != nullptr;
+  PDG_CHECK_ARG(eu || gC == gz1m, "pdg_edge_bwd_fused: without the edge update gC is gz1m (pass the same array)");
+  PDG_CHECK_ARG(!eu || gC != gz1m, "pdg_edge_bwd_fused: gC may alias gz1m only without the edge update");
+  PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd_fused: ge_out must not alias ge_next");
+  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && st_e && (lb_e || pairs_e) && PDG_ALIGNED(a2e) &&
+                        PDG_ALIGNED(a1e)),
+                "pdg_edge_bwd_fused: edge-update arguments missing or misaligned");
+  hipStream_t s = (hipStream_t)stream;
+  if (eu)
+    hipLaunchKernelGGL(edge_bwd_fused_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), EBF_SHM, s, dst, gaggr, ge_next,
+                       a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g_msg, W2T, WcT, e, a2ln, st_ln, ln_g_e, gz1m, gC,
+                       ge_out, slabs_w2, slabs_wc, ln_partials, ln_pairs, n_edges, pairs_m, npairs_m, pairs_e, npairs_e,
+                       slab_init, accumulate);
+  else
+    hipLaunchKernelGGL(edge_bwd_fused_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), EBF_SHM, s, dst, gaggr, ge_next,
+                       a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g_msg, W2T, WcT, e, a2ln, st_ln, ln_g_e, gz1m, gC,
+                       ge_out, slabs_w2, slabs_wc, ln_partials, ln_pairs, n_edges, pairs_m, npairs_m, pairs_m, npairs_m,
+                       slab_init, accumulate);
+  PDG_CHECK_LAUNCH("pdg_edge_bwd_fused");
   return PDG_OK;
 }
 

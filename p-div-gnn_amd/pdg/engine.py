@@ -68,6 +68,9 @@ VARIANTS = {
     # edge backward with the W2 / Wc weight gradients fused (pdg_edge_bwd_w2 / pdg_edge_gout_wc); False:
     # pdg_edge_bwd + deferred pdg_wgrad_segments passes
     "fused_edge_wgrad": ("PDG_FUSED_EDGE_WGRAD", True),
+    # the two fused edge-backward kernels as ONE weight-specialised pass (pdg_edge_bwd_fused: gC and ge_next
+    # reach the Wc work through LDS instead of HBM; needs fused_edge_wgrad and gz1e_from_gc)
+    "fused_edge_bwd": ("PDG_FUSED_EDGE_BWD", False),
     # P/Q gather backward before the Wc pass (gz1m / gz1e re-read while still in the Infinity Cache:
     # pq_scatter_bwd 63.6 -> 59.7 us and edge_gout_wc 145 -> 140 us per call, same box)
     "pq_first": ("PDG_PQ_FIRST", True),
@@ -205,6 +208,7 @@ class EPDEngine:
         self.fused_edge_wgrad = var["fused_edge_wgrad"]
         self.pq_first = var["pq_first"]
         self.gz1e_from_gc = var["gz1e_from_gc"]
+        self.fused_edge_bwd = var["fused_edge_bwd"]
         self.coop_fwd = var["coop_fwd"]
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
@@ -580,14 +584,30 @@ class EPDEngine:
                 if eu:   # edge-update LayerNorm: gy = ge_next (per edge)
                     pp, n_e = edge_ln_pairs(PE(t), ge_next, d["a2e"], st[d["i_e"]], ACC_E, g_edge)
                     pe, ne = src(pp, n_e if not fused else n_edge)
-                if fused:
+                one_pass = fused and self.fused_edge_bwd
+                if one_pass:
+                    if not e_sum:
+                        raise ValueError("fused_edge_bwd forms no gz1e: it needs gz1e_from_gc")
+                    # + the column sums / pairs of the LayerNorm that produced e_t (as pdg_edge_gout_wc)
+                    if t > 0:
+                        a2ln, st_ln, accb, gl, pp = (ctx.per_step[t - 1]["a2e"], st[ctx.per_step[t - 1]["i_e"]], ACC_E,
+                                                     g_edge, PE(t - 1))
+                    else:
+                        a2ln, st_ln, accb, gl, pp = ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"], P_EENC
+                    self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_fused, E, _p(plan.dst), _p(gaggr),
+                            _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
+                            st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(T["WcT"]),
+                            _p(d["e"]), _p(a2ln), st_ln, _p(gl), _p(gz1m), _p(gC), _p(ge_out), _p(slabs_w2),
+                            _p(slabs_wc), nse, _p(accb), _p(pp), pm, nm, pe, ne, int(t == S - 1), 1, s)
+                    n_edge = nse
+                elif fused:
                     self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
                             _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, int(t == S - 1), s)
                 # the edge-update rows of the P/Q gather backward: gz1e, or gC (= gz1m + gz1e) with e_is_sum
                 ge_rows, e_is_sum = (gC, 1) if (e_sum and eu) else (gz1e if eu else None, 0)
-                if fused:
+                if fused and not one_pass:
                     # + the column sums / pairs of the LayerNorm that produced e_t (LN_e of step t-1, or the
                     # edge encoder's)
                     if t > 0:
@@ -609,7 +629,7 @@ class EPDEngine:
                     ge_rows, e_is_sum = gz1e if eu else None, 0
                 self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
                         _p(plan.perm_src), _p(gz1m), _p(ge_rows), e_is_sum, _p(gP), _p(gQ), s)
-                if fused and self.pq_first:   # gz1m / gz1e read while still in the Infinity Cache
+                if fused and self.pq_first and not one_pass:   # gz1m / gz1e read while still in the Infinity Cache
                     self._t("edge_gout", gout_fn, *gout_args)
             # gx_t, with the column sums / pairs of the LayerNorm whose output it is the gradient of:
             # the node LayerNorm of step t-1, or the node encoder's

@@ -91,6 +91,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_enc_narrow_reduce": [P, I, P, P, P],
     "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P, I, I, P],
     "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P, P, I, I, P],
+    "pdg_edge_bwd_fused": [I] + [P] * 23 + [I, P, P, P, I, P, I, I, I, P],
     "pdg_mesh_graph": [I, P, I, I, P, I, P, P, P, ctypes.c_long, P, P, ctypes.c_long, P],
     "pdg_mesh_graph_scratch_bytes": [I, I],
     "pdg_wgrad_segments": [I, P, P, P, P, I, P],

@@ -23,12 +23,14 @@ sizes at which the bf16x6 products (W2 in the edge kernels, every weight gradien
 graph-LayerNorm reductions accumulate the most terms (up to 9.6e5 rows per LayerNorm and 2e7
 rows per weight gradient), so they are where a precision shortfall would show.
 
-At configs 3 and 4 the oracle keeps activations of one message-passing step at a time
-(checkpoint_steps: ~35 GB of host memory in float64 instead of ~170 GB) and the float32 oracle
-runs only when a gradient is outside the fixed 3e-5 bound (it can only loosen the bound) or when
-PDG_PARITY_FP32=1 asks for the record (profiles/r04_parity.jsonl holds such a run: the fp32
-oracle's own distance to fp64 beside the GPU's, per tensor): the float64 run alone takes a few
-minutes of host CPU.  A heartbeat line is appended to
+The oracle's results at these sizes are cached fixtures (tests/golden/fullsize_c{2,3,4,5}.npz, made by
+tests/golden/make_fullsize.py with the same oracle in float64 and float32): the float64 run alone takes
+200-340 s of the GPU box's host cores at configs 3 / 4, most of the suite's budget.  Each fixture carries a
+hash of the batch arrays, divergence operators, initial parameters and statistics it was computed from;
+the test hashes its own workload and uses the fixture only when they are equal, otherwise (or with
+PDG_FULLSIZE_LIVE=1) it runs the oracle live (configs 3 / 4 keeping one message-passing step's activations
+at a time: checkpoint_steps).  Every config now has the fp32 oracle's own distance to fp64 per tensor
+(the fixture's host; an fp32 CPU result is host-dependent).  A heartbeat line is appended to
 gpurun_out/fullsize_heartbeat.log every 20 s while a test runs (long silent runs look hung).
 Every test appends its measured errors as one JSON line to gpurun_out/parity.jsonl (and to
 $PDG_PARITY_LOG when set), so the margins to the tolerances are on record, not only "passed".
@@ -42,7 +44,11 @@ from pathlib import Path
 import pytest
 import torch
 
+import sys
+
 from gpu_common import dev, rel
+
+sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
 
 pytestmark = pytest.mark.gpu
 
@@ -92,33 +98,45 @@ def _log(rec):
 
 
 def _workload(config):
-    import bench
-    cfg = bench.CONFIGS[config]
-    batch, _ = bench.build_batch(cfg, seed=69, device=dev())
-    stats = bench.dataset_stats(batch)
+    """The bench's batch and the model's initial state, built on the host exactly as the fixture
+    generator builds them (statistics from the host copy of the batch), then moved to the GPU."""
+    from make_fullsize import workload
     from gnn_local_stress.models import EncodeProcessDecode
-    torch.manual_seed(69)
+    cfg, batch, stats, params = workload(config)
     model = EncodeProcessDecode(input_edges_features_size=1, message_passing_steps=cfg["steps"], latent_size=128,
-                                input_nodes_features_size=6, output_nodes_features_size=3, **stats).to(dev())
-    return cfg, batch, {k: float(v) for k, v in stats.items()}, model
+                                input_nodes_features_size=6, output_nodes_features_size=3,
+                                **{k: torch.tensor(v) for k, v in stats.items()})
+    model.load_state_dict(params)
+    return cfg, batch, stats, params, model.to(dev())
 
 
-def _oracle(params, stats, batch, steps, dtype, divergence, train, checkpoint=False):
-    from oracle import epd_oracle as O
-    P = {k: v.detach().cpu().to(dtype).clone().requires_grad_(train) for k, v in params.items()}
-    st = {k: torch.tensor(v, dtype=dtype) for k, v in stats.items()}
-    b = batch
-    args = (b.pos.cpu().to(dtype), b.mean_stress.cpu().to(dtype), b.nodes_types.cpu(), b.edge_index.cpu(),
-            b.edge_attr.cpu().to(dtype))
-    with torch.set_grad_enabled(train):
-        pred = O.epd_forward(P, st, *args, steps, scale_output=not train, checkpoint_steps=checkpoint)
-    if not train:
-        return pred, None, None, None
-    gt = (b.local_stress.cpu().to(dtype) - st["mean_local_stress"]) / st["std_local_stress"]
-    ops = [d.op_div_matrix.to(dtype) for d in b._data_list] if divergence else None
-    total, nmse, _ = O.batch_loss(pred, gt, b.ptr, ops, b.nodes_types.cpu(), divergence, 10.0)
-    total.backward()
-    return pred.detach(), float(total), float(nmse), {k: v.grad for k, v in P.items()}
+def _reference(config, cfg, batch, stats, params):
+    """The oracle's float64 results and the float32 run's distances: from the fixture when its workload
+    hash equals this workload's, else computed live.  Returns (rec, source)."""
+    import numpy as np
+    from make_fullsize import oracle, workload_hash
+    path = Path(__file__).resolve().parent / "golden" / f"fullsize_c{config}.npz"
+    h = workload_hash(batch, params, stats)
+    if path.exists() and os.environ.get("PDG_FULLSIZE_LIVE") != "1":
+        z = np.load(path, allow_pickle=False)
+        if str(z["hash"]) == h:
+            rec = {"pred64": torch.from_numpy(z["pred64"]), "f32_vs_f64": float(z["f32_vs_f64"])}
+            if "total64" in z.files:
+                rec.update(total64=float(z["total64"]), nmse64=float(z["nmse64"]),
+                           grad64={k[7:]: torch.from_numpy(z[k]) for k in z.files if k.startswith("grad64.")},
+                           grad32_vs_f64={k[14:]: float(z[k]) for k in z.files if k.startswith("grad32_vs_f64.")})
+            return rec, f"{path.name} (hash {h})"
+        source = f"live: {path.name} hash {z['hash']} != workload {h}"
+    else:
+        source = "live" if path.exists() else f"live: no {path.name}"
+    train = not cfg.get("inference")
+    big = batch.num_edges > 500_000
+    p64, t64, n64, g64 = oracle(params, stats, batch, cfg["steps"], torch.float64, cfg["divergence"], train, big)
+    p32, _, _, g32 = oracle(params, stats, batch, cfg["steps"], torch.float32, cfg["divergence"], train, big)
+    rec = {"pred64": p64, "f32_vs_f64": rel(p32, p64)}
+    if train:
+        rec.update(total64=t64, nmse64=n64, grad64=g64, grad32_vs_f64={k: rel(g32[k], g64[k]) for k in g64})
+    return rec, source
 
 
 @pytest.mark.parametrize("config", [pytest.param(2, marks=pytest.mark.timeout(900)),
@@ -127,51 +145,46 @@ def _oracle(params, stats, batch, steps, dtype, divergence, train, checkpoint=Fa
 def test_training_step_at_baseline_size(config):
     from pdg.trainer import Trainer
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    cfg, batch, stats, model = _workload(config)
-    params = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    cfg, batch, stats, params, model = _workload(config)
+    gbatch = batch.to(dev())
     with torch.no_grad():
-        pred = model(batch, scale_output=False).local_stress.cpu()
+        pred = model(gbatch, scale_output=False).local_stress.cpu()
     tr = Trainer(model, lr=1e-3, divergence=cfg["divergence"], divergence_penalty=10.0)
-    out = tr.step(batch)                      # the benchmarked step: forward, loss, backward, Adam
+    out = tr.step(gbatch)                     # the benchmarked step: forward, loss, backward, Adam
     torch.cuda.synchronize()
     total, nmse = float(out["total"]), float(out["nmse"])
     grads = {n: tr.G[n].detach().cpu().clone() for n in tr.G}
-    del tr, out
-    big = batch.num_edges > 500_000
+    del tr, out, gbatch
     t0 = time.time()
-    p64, t64, n64, g64 = _oracle(params, stats, batch, cfg["steps"], torch.float64, cfg["divergence"], True, big)
+    ref, source = _reference(config, cfg, batch, stats, params)
+    g64 = ref["grad64"]
     rec = {"config": config, "nodes": batch.num_nodes, "edges": batch.num_edges, "graphs": batch.num_graphs,
-           "internal_boundary_nodes": int((batch.nodes_types == -1).sum()),
-           "pred_vs_f64": rel(pred, p64), "loss_vs_f64": abs(total - t64) / abs(t64),
-           "nmse_vs_f64": abs(nmse - n64) / abs(n64), "grads": {}}
-    need32 = (not big or os.environ.get("PDG_PARITY_FP32") == "1"
-              or any(rel(grads[n], g64[n]) > GRAD_TOL for n in g64))
-    g32 = None
-    if need32:
-        p32, t32, _, g32 = _oracle(params, stats, batch, cfg["steps"], torch.float32, cfg["divergence"], True, big)
-        rec.update(pred_vs_f32=rel(pred, p32), f32_vs_f64=rel(p32, p64), loss_f32_vs_f64=abs(t32 - t64) / abs(t64))
+           "internal_boundary_nodes": int((batch.nodes_types == -1).sum()), "oracle_source": source,
+           "pred_vs_f64": rel(pred, ref["pred64"]), "f32_vs_f64": ref["f32_vs_f64"],
+           "loss_vs_f64": abs(total - ref["total64"]) / abs(ref["total64"]),
+           "nmse_vs_f64": abs(nmse - ref["nmse64"]) / abs(ref["nmse64"]), "grads": {}}
     for name in g64:
-        rec["grads"][name] = (rel(grads[name], g64[name]), rel(g32[name], g64[name]) if g32 else None)
+        rec["grads"][name] = (rel(grads[name], g64[name]), ref["grad32_vs_f64"][name])
     worst = max(rec["grads"], key=lambda n: rec["grads"][n][0])
     rec["worst_grad"] = [worst, *rec["grads"][worst]]
+    rec["worst_margin"] = max(g / max(GRAD_TOL, 2 * r) for g, r in rec["grads"].values())
     rec["oracle_s"] = round(time.time() - t0, 1)
     _log(rec)
-    assert rec["pred_vs_f64"] < OUT_TOL and rec.get("pred_vs_f32", 0.0) < OUT_TOL, rec
+    # the fp32 oracle's output is within f32_vs_f64 of fp64, so both bounds below hold against it too
+    assert rec["pred_vs_f64"] < OUT_TOL and rec["pred_vs_f64"] + rec["f32_vs_f64"] < 2 * OUT_TOL, rec
     assert rec["loss_vs_f64"] < OUT_TOL and rec["nmse_vs_f64"] < OUT_TOL, rec
     for name, (got, ref32) in rec["grads"].items():
-        assert got <= max(GRAD_TOL, 2 * (ref32 or 0.0)), (name, got, ref32)
+        assert got <= max(GRAD_TOL, 2 * ref32), (name, got, ref32)
 
 
 @pytest.mark.timeout(900)
 def test_inference_at_baseline_size():
     torch.set_num_threads(min(16, os.cpu_count() or 1))
-    cfg, batch, stats, model = _workload(5)
-    params = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    cfg, batch, stats, params, model = _workload(5)
     with torch.no_grad():                     # gnn_inference.py:58-60
-        out = model(batch, scale_output=True).local_stress.cpu()
-    ref64, _, _, _ = _oracle(params, stats, batch, cfg["steps"], torch.float64, False, False)
-    ref32, _, _, _ = _oracle(params, stats, batch, cfg["steps"], torch.float32, False, False)
-    rec = {"config": 5, "nodes": batch.num_nodes, "edges": batch.num_edges, "out_vs_f64": rel(out, ref64),
-           "out_vs_f32": rel(out, ref32), "f32_vs_f64": rel(ref32, ref64)}
+        out = model(batch.to(dev()), scale_output=True).local_stress.cpu()
+    ref, source = _reference(5, cfg, batch, stats, params)
+    rec = {"config": 5, "nodes": batch.num_nodes, "edges": batch.num_edges, "oracle_source": source,
+           "out_vs_f64": rel(out, ref["pred64"]), "f32_vs_f64": ref["f32_vs_f64"]}
     _log(rec)
-    assert rec["out_vs_f64"] < OUT_TOL and rec["out_vs_f32"] < OUT_TOL, rec
+    assert rec["out_vs_f64"] < OUT_TOL and rec["out_vs_f64"] + rec["f32_vs_f64"] < 2 * OUT_TOL, rec

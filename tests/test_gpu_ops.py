@@ -1234,3 +1234,69 @@ def test_nmse_fwd_bwd_equals_fwd_then_bwd(env, sizes, accumulate):
         t, p = gt64[lo:hi], pr64[lo:hi]
         ref = (((t - p) ** 2).sum(0) / ((t - t.mean(0)) ** 2).sum(0)).mean()
         assert abs(float(l1[b]) - float(ref)) <= 1e-5 * abs(float(ref)), (b, float(l1[b]), float(ref))
+
+
+@pytest.mark.parametrize("E,eu", [(77, 1), (4099, 1), (4099, 0), (30011, 1)])
+def test_edge_bwd_fused_matches_split_pair(env, E, eu):
+    """pdg_edge_bwd_fused (one weight-specialised pass) against pdg_edge_bwd_w2 + pdg_edge_gout_wc on the
+    same inputs, twice (the first call initialises the slabs and LayerNorm partials, the second adds):
+    gz1m, gC, ge_out and the dW2 / dWc slab sums bitwise (the same MFMA sequence per element); the db2 / db1
+    slab sums, the LayerNorm column-sum rows and pairs to fp32 summation order.  E = 77: fewer rows than
+    blocks x 16 (empty and ragged blocks); eu = 0: the message branch only (gC is gz1m)."""
+    lib, sh, _ = env
+    s = sh()
+    N, ns = max(E // 6, 7), 37
+    g = torch.Generator().manual_seed(E + eu)
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values.int().cuda()
+    gaggr = rnd(N, L)
+    ge_next = rnd(E, L) if eu else None
+    a2m, a1m, a2e, a1e, a2ln = (torch.relu(rnd(E, L)) for _ in range(5))
+    e = rnd(E, L)
+    W2T, WcT = rnd(L, L) * 0.1, rnd(L, L) * 0.1
+    lg, lge = rnd(L) * 0.3 + 1.0, rnd(L) * 0.3 + 1.0
+
+    def stat(a):
+        part = torch.tensor([float(a.double().sum()), float((a.double() ** 2).sum())], dtype=torch.float64,
+                            device="cuda")
+        return finalize(lib, s, part, 1, a.numel())
+    st_m, st_e, st_ln = stat(a2m), stat(a2e), stat(a2ln)
+    pm, pe = rnd(5, 2).double() * 0.01, rnd(7, 2).double() * 0.01
+    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    res = {}
+    for arm in ("split", "fused"):
+        o = {k: torch.full((E, L), float("nan"), device="cuda") for k in ("gz1m", "gC", "ge_out")}
+        if not eu:
+            o["gC"] = o["gz1m"]
+        sw2, swc = (torch.full((ns, L * L + L), float("nan"), device="cuda") for _ in range(2))
+        lnp = torch.full((ns + 1, 2 * L), float("nan"), dtype=torch.float64, device="cuda")
+        prs = torch.full((ns, 2), float("nan"), dtype=torch.float64, device="cuda")
+        for call in (0, 1):
+            init, accum = int(call == 0), int(call == 1)
+            if arm == "split":
+                lib.pdg_edge_bwd_w2(E, dst.data_ptr(), gaggr.data_ptr(), P(ge_next), a2m.data_ptr(), a1m.data_ptr(),
+                                    a2e.data_ptr(), a1e.data_ptr(), st_m.data_ptr(), st_e.data_ptr(), None, None,
+                                    lg.data_ptr(), W2T.data_ptr(), o["gz1m"].data_ptr(), None, o["gC"].data_ptr(),
+                                    sw2.data_ptr(), ns, pm.data_ptr(), 5, pe.data_ptr(), 7, init, s)
+                lib.pdg_edge_gout_wc(E, o["gC"].data_ptr(), e.data_ptr(), P(ge_next), WcT.data_ptr(),
+                                     o["ge_out"].data_ptr(), swc.data_ptr(), ns, a2ln.data_ptr(), st_ln.data_ptr(),
+                                     lnp.data_ptr(), lge.data_ptr(), prs.data_ptr(), accum, init, s)
+            else:
+                lib.pdg_edge_bwd_fused(E, dst.data_ptr(), gaggr.data_ptr(), P(ge_next), a2m.data_ptr(), a1m.data_ptr(),
+                                       a2e.data_ptr(), a1e.data_ptr(), st_m.data_ptr(), st_e.data_ptr(), None, None,
+                                       lg.data_ptr(), W2T.data_ptr(), WcT.data_ptr(), e.data_ptr(), a2ln.data_ptr(),
+                                       st_ln.data_ptr(), lge.data_ptr(), o["gz1m"].data_ptr(), o["gC"].data_ptr(),
+                                       o["ge_out"].data_ptr(), sw2.data_ptr(), swc.data_ptr(), ns, lnp.data_ptr(),
+                                       prs.data_ptr(), pm.data_ptr(), 5, pe.data_ptr(), 7, init, accum, s)
+        torch.cuda.synchronize()
+        res[arm] = (o, sw2, swc, lnp[:ns], prs)
+    (o0, w0, c0, l0, p0), (o1, w1, c1, l1, p1) = res["split"], res["fused"]
+    for k in ("gz1m", "gC", "ge_out"):
+        assert torch.equal(o0[k], o1[k]), k
+    assert torch.equal(w0[:, : L * L], w1[:, : L * L]) and torch.equal(c0[:, : L * L], c1[:, : L * L])
+    for a, b in ((w0[:, L * L:], w1[:, L * L:]), (c0[:, L * L:], c1[:, L * L:]), (l0, l1), (p0, p1)):
+        assert torch.isfinite(b).all() and rel(b, a) < 1e-6
+    # the fp64 restatement of the outputs the split pair is checked against elsewhere: ge_out = [ge_next +] gC Wc
+    ref = o0["gC"].double() @ WcT.double().T
+    if eu:
+        ref = ref + ge_next.double()
+    assert rel(o1["ge_out"], ref) < TOL
