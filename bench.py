@@ -62,6 +62,7 @@ PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd
              "wgrad_W2": "wgrad_x6_kernel",
              # the edge-update instantiations
              "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
+             "edge_bwd_fused": "void edge_bwd_fused_kernel<true>",
              "edge_gout": "void edge_gout_wc_kernel<true>",
              "node_bwd": "node_bwd_coop_kernel", "node_pq": "void node_pq_x6_kernel<true>",
              "gemm_sum2": "void gemm_sum2_coop_kernel<true>", "wgrad_pairs": "void wgrad_x6_pair2_kernel"}
@@ -235,13 +236,13 @@ def cpu_baseline(cfg, samples, full_graphs: int, reps: int = 5, one_thread: bool
 
 # ---------------------------------------------------------------------------------- roofline
 def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, seg: bool = False,
-                e_sum: bool = True) -> dict:
+                e_sum: bool = True, one_pass: bool = False) -> dict:
     """Algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops with the peak of their
     instruction type, and the bytes the kernel must read/write (inputs once, outputs once, int32
     indices).  An fp32-accurate 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA,
     or 6x that in bf16 (bf16x6)."""
     g = 2 * L * L
-    return {
+    out = {
         # W_c product (fp32 MFMA) + 2 W2 products (bf16x6) per edge; reads a2e_prev, e_prev, 4 gathered
         # P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e;
         # seg: also the N message sums rows, and a2m only when training
@@ -270,6 +271,11 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
                      2 * 4 * L * N + (1 if infer else 2) * 4 * L * N),
         "pq_scatter_bwd": ([], 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
     }
+    if one_pass:   # pdg_edge_bwd_fused: the W2 and Wc work of both kernels (6 bf16x6 products per edge);
+        # reads gaggr[dst], a2m, a1m, ge_next, a2e, a1e, e, a2ln, dst; writes gz1m, gC, ge_out; two slab sets
+        out["edge_bwd"] = ([(E * 6 * g * X6, PEAK_BF16_MFMA)], E * (11 * 4 * L + 4) + 4 * nslab_bytes)
+        out.pop("edge_gout")
+    return out
 
 
 def compulsory_bytes(work: dict, N: int, E: int) -> dict:
@@ -313,7 +319,7 @@ def pmc_tree() -> str | None:
     return json.loads(f.read_text())["_meta"]["tree"] if f else None
 
 
-def load_pmc(fused: bool, path=None) -> dict:
+def load_pmc(fused: bool, path=None, one_pass: bool = False) -> dict:
     """Per-launch PMC bytes by kernel from `path` (a pmc_file() result; {} when None)."""
     pmc = {}
     if path is not None and Path(path).exists():
@@ -321,7 +327,7 @@ def load_pmc(fused: bool, path=None) -> dict:
         data.pop("_meta", None)
         for k, prefix in PMC_NAMES.items():
             if fused and k == "edge_bwd":
-                prefix = PMC_NAMES["edge_bwd_w2"]
+                prefix = PMC_NAMES["edge_bwd_fused" if one_pass else "edge_bwd_w2"]
             hit = [v for name, v in data.items() if name.startswith(prefix if isinstance(prefix, tuple) else (prefix,))]
             if hit:
                 pmc[k] = round(hit[0]["total"])
@@ -518,10 +524,12 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
     # the fused message sums run in inference only unless PDG_SEG_SUMS_TRAIN=1 (engine.py:253)
     seg = getattr(eng, "seg_sums", False) if infer else getattr(eng, "seg_sums_train", False)
-    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg, fused and getattr(eng, "gz1e_from_gc", False))
+    one_pass = fused and getattr(eng, "fused_edge_bwd", False)
+    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg, fused and getattr(eng, "gz1e_from_gc", False),
+                       one_pass)
     comp = compulsory_bytes(work, N, E)
     pmc_path, pmc_reason = pmc_file() if with_pmc else (None, "not collected for this config")
-    pmc = load_pmc(fused, pmc_path)
+    pmc = load_pmc(fused, pmc_path, one_pass)
     sq_path, sq_reason = sq_file() if with_pmc else (None, "not collected for this config")
     sq = load_sq(sq_path)
     step_s = el * ev_steps / args.steps

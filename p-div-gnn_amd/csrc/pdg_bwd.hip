@@ -599,6 +599,11 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
                             void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd: n_edges must be > 0");
   PDG_CHECK_ARG(lb_m || pairs_m, "pdg_edge_bwd: need lb_m or pairs_m");
+  // null outputs are refused here rather than written through on the device (a host-side mix-up of the
+  // fused and unfused paths once passed gz2m == NULL and faulted the GPU)
+  PDG_CHECK_ARG(dst && gaggr && a2m && a1m && st_m && ln_g && W2T && WcT && gz2m && gz1m && gC && ge_out,
+                "pdg_edge_bwd: null argument");
+  PDG_CHECK_ARG(!ge_next || (a2e && a1e && gz2e && gz1e), "pdg_edge_bwd: null edge-update argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(gz2m) &&
                     PDG_ALIGNED(gz1m) && PDG_ALIGNED(gC) && PDG_ALIGNED(ge_out),
                 "pdg_edge_bwd: misaligned pointer");

@@ -621,7 +621,7 @@ class EPDEngine:
                     if not self.pq_first:
                         self._t("edge_gout", gout_fn, *gout_args)
                     n_edge = nse
-                else:
+                elif not fused:
                     self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr),
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(T["WcT"]),

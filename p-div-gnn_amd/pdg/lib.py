@@ -110,6 +110,8 @@ SIGNATURES: dict[str, list] = {
 _RESTYPES = {"pdg_last_error": ctypes.c_char_p, "pdg_source_hash": ctypes.c_char_p, "pdg_mesh_graph_scratch_bytes": ctypes.c_long}
 
 LN_STAT_BYTES = 40   # sizeof(pdg_ln_stat)
+# PDG_DEBUG_SYNC=1: synchronise after every library call and name it on stderr (locating a faulting kernel)
+_DEBUG_SYNC = os.environ.get("PDG_DEBUG_SYNC") == "1"
 LN_BWD_BYTES = 24    # sizeof(pdg_ln_bwd)
 
 
@@ -153,6 +155,10 @@ class _Lib:
             if rc != 0:
                 msg = self.load().pdg_last_error().decode(errors="replace")
                 raise PdgError(f"{name} failed ({rc}): {msg}")
+            if _DEBUG_SYNC:   # fault localisation: every launch completes before the next (stderr names it)
+                import sys
+                print(f"[pdg] {name}", file=sys.stderr, flush=True)
+                torch.cuda.synchronize()
             return rc
 
         call.__name__ = name
