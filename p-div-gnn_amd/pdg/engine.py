@@ -69,7 +69,8 @@ VARIANTS = {
     # pdg_edge_bwd + deferred pdg_wgrad_segments passes
     "fused_edge_wgrad": ("PDG_FUSED_EDGE_WGRAD", True),
     # the two fused edge-backward kernels as ONE weight-specialised pass (pdg_edge_bwd_fused: gC and ge_next
-    # reach the Wc work through LDS instead of HBM; needs fused_edge_wgrad and gz1e_from_gc)
+    # reach the Wc work through LDS instead of HBM; applies with fused_edge_wgrad and gz1e_from_gc, the split
+    # pair runs otherwise)
     "fused_edge_bwd": ("PDG_FUSED_EDGE_BWD", False),
     # P/Q gather backward before the Wc pass (gz1m / gz1e re-read while still in the Infinity Cache:
     # pq_scatter_bwd 63.6 -> 59.7 us and edge_gout_wc 145 -> 140 us per call, same box)
@@ -584,10 +585,9 @@ class EPDEngine:
                 if eu:   # edge-update LayerNorm: gy = ge_next (per edge)
                     pp, n_e = edge_ln_pairs(PE(t), ge_next, d["a2e"], st[d["i_e"]], ACC_E, g_edge)
                     pe, ne = src(pp, n_e if not fused else n_edge)
-                one_pass = fused and self.fused_edge_bwd
+                # (the one-pass kernel forms no gz1e: with gz1e_from_gc off the split pair runs)
+                one_pass = fused and self.fused_edge_bwd and e_sum
                 if one_pass:
-                    if not e_sum:
-                        raise ValueError("fused_edge_bwd forms no gz1e: it needs gz1e_from_gc")
                     # + the column sums / pairs of the LayerNorm that produced e_t (as pdg_edge_gout_wc)
                     if t > 0:
                         a2ln, st_ln, accb, gl, pp = (ctx.per_step[t - 1]["a2e"], st[ctx.per_step[t - 1]["i_e"]], ACC_E,

@@ -52,13 +52,53 @@ def workload_hash(batch, params: dict, stats: dict) -> str:
     return h.hexdigest()[:16]
 
 
+def exact_stats(b) -> dict:
+    """bench.dataset_stats (datasets.py:283-291's mean / unbiased std of the batch) computed host-
+    independently: exactly rounded sums (math.fsum over float64) rounded once to float32.  torch's CPU
+    reductions split the work by thread count and vector width, so the same batch gave statistics a few
+    ulps apart on two hosts, and with them different fixtures."""
+    import math
+    out = {}
+    for name, t in (("pos", b.pos), ("mean_stress", b.mean_stress), ("local_stress", b.local_stress),
+                    ("edge_weight", b.edge_attr)):
+        x = t.detach().cpu().double().reshape(-1).tolist()
+        n = len(x)
+        mean = math.fsum(x) / n
+        var = math.fsum((v - mean) ** 2 for v in x) / (n - 1)
+        key_m = "mean_" + name if name != "edge_weight" else "mean_edge_weight"
+        out[key_m] = float(np.float32(mean))
+        out[key_m.replace("mean_", "std_", 1)] = float(np.float32(math.sqrt(var)))
+    return {k: out[k] for k in ("mean_pos", "std_pos", "mean_mean_stress", "std_mean_stress", "mean_local_stress",
+                                "std_local_stress", "mean_edge_weight", "std_edge_weight")}
+
+
+def workload_parts(batch, params: dict, stats: dict) -> dict:
+    """Component hashes of workload_hash (to find which input differs between two hosts)."""
+    out = {}
+    b = batch
+    for name in ("pos", "mean_stress", "local_stress", "nodes_types", "edge_index", "edge_attr", "ptr"):
+        out[name] = hashlib.sha256(getattr(b, name).detach().cpu().contiguous().numpy().tobytes()).hexdigest()[:8]
+    h = hashlib.sha256()
+    for d in b._data_list:
+        op = d.op_div_matrix.coalesce()
+        h.update(op.indices().numpy().tobytes())
+        h.update(op.values().numpy().tobytes())
+    out["op_div"] = h.hexdigest()[:8]
+    h = hashlib.sha256()
+    for k in sorted(params):
+        h.update(params[k].detach().cpu().contiguous().numpy().tobytes())
+    out["params"] = h.hexdigest()[:8]
+    out["stats"] = hashlib.sha256(repr(sorted(stats.items())).encode()).hexdigest()[:8]
+    return out
+
+
 def workload(config: int, device="cpu"):
     """(cfg, batch, stats as floats, params) of a BASELINE config, as the tests and bench build it."""
     import bench
     from gnn_local_stress.models import EncodeProcessDecode
     cfg = bench.CONFIGS[config]
     batch, _ = bench.build_batch(cfg, seed=69, device="cpu")
-    stats = {k: float(v) for k, v in bench.dataset_stats(batch).items()}
+    stats = exact_stats(batch)
     torch.manual_seed(69)
     model = EncodeProcessDecode(input_edges_features_size=1, message_passing_steps=cfg["steps"], latent_size=128,
                                 input_nodes_features_size=6, output_nodes_features_size=3,
@@ -115,6 +155,20 @@ def make(config: int) -> Path:
     return path
 
 
+def _heartbeat(period: float = 30.0):
+    """A line on stdout every `period` s (a long silent run on the GPU box is taken to be hung)."""
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(period)
+            print(f"  ... {time.time() - t0:.0f} s", flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 if __name__ == "__main__":
+    _heartbeat()
     for c in [int(a) for a in sys.argv[1:]] or [2, 3, 4, 5]:
+        print(f"config {c} ...", flush=True)
         make(c)

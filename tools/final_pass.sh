@@ -3,7 +3,7 @@
 #   tools/final_pass.sh TAG tests     GPU test suite (the full-size parity log lands in gpurun_out/parity.jsonl)
 #   tools/final_pass.sh TAG measure   rocprofv3 kernel stats, the two PMC passes (FETCH_SIZE, WRITE_SIZE), then
 #                                     the default bench line, which finds the PMC traffic of the same tree
-#                                     (the PMC summary is copied to profiles/${ROUND:-r04}_pmc_traffic.json first)
+#                                     (the PMC summary is copied to profiles/${ROUND:-r05}_pmc_traffic.json first)
 # Every GPU step has its own time limit; the script stops at the first failure.
 set -o pipefail
 TAG=$1
@@ -45,12 +45,12 @@ if [ "$WHAT" = measure ]; then
   python tools/prof_window.py "$O/prof/bench_kernel_trace.csv" 3 --json "$O/prof_window.json" > "$O/prof_window.txt"
   grep '^{' "$O/prof.log" | tail -1 > "$O/prof_bench_line.json"
   rm -f "$O"/prof/*kernel_trace.csv "$O"/*/*.db
-  cp "$O/pmc_traffic.json" "$R/profiles/${ROUND:-r04}_pmc_traffic.json"
+  cp "$O/pmc_traffic.json" "$R/profiles/${ROUND:-r05}_pmc_traffic.json"
   # SQ counters of the same tree (MFMA busy, wave-cycle split), two passes with kernel traces, before the
   # bench line so that it carries the counter MFMA busy beside its flop-derived frac_mfma
   bash tools/sq_pass.sh "$TAG/sq" > "$O/sq_pass.log" 2>&1 || { tail -5 "$O/sq_pass.log"; exit 1; }
-  cp "$R/gpurun_out/$TAG/sq/sq.txt" "$R/profiles/${ROUND:-r04}_sq.txt"
-  cp "$R/gpurun_out/$TAG/sq/sq.json" "$R/profiles/${ROUND:-r04}_sq.json"
+  cp "$R/gpurun_out/$TAG/sq/sq.txt" "$R/profiles/${ROUND:-r05}_sq.txt"
+  cp "$R/gpurun_out/$TAG/sq/sq.json" "$R/profiles/${ROUND:-r05}_sq.json"
   step bench 500 python bench.py || exit 1
   grep '^{' "$O/bench.log" | tail -1 > "$O/bench_line.json"
   python -c "import json; d = json.load(open('$O/bench_line.json')); print(d['value'], d['ms_per_step'], d['tree'], d['traffic_tree_match'], d['roofline'])"
