@@ -296,16 +296,6 @@ int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, 
                       const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                       const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                       double* part_e, int with_edge_update, int nblocks, void* stream);
-/* pdg_edge_fwd_coop for dst-sorted rows whose every 32-row group (rows 32i .. 32i + 31, the last group
- * ragged) has dst values spanning at most dst_span nodes (dst[last] - dst[first]; GraphPlan.dst_span32).
- * With dst_span < 16 on the 256-block grid, a round's P[dst] / Q[dst] rows are loaded once per
- * destination node into an LDS tile instead of gathered per edge; outputs bitwise pdg_edge_fwd_coop's.
- * The span is the caller's guarantee (a wrong one gives wrong rows, not a fault). */
-int pdg_edge_fwd_coop_span(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                           const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
-                           const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
-                           const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
-                           double* part_e, int with_edge_update, int dst_span, int nblocks, void* stream);
 /* pdg_edge_fwd_coop that also forms the aggregation's message sums (models.py:215-217) from its
  * a2m tiles, replacing pdg_segment_sum's re-read of a2m: sums[v] (fp64, N x 128) = sum of a2m over
  * v's incoming edges, raw (the message LayerNorm's statistics come out of this launch); rows of

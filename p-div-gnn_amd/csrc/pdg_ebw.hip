@@ -23,8 +23,6 @@
 // Per round: stage (loads -> LN backward / split -> images) | loads of a later round issued |
 // barrier | weight-gradient MFMAs | activation MFMAs | stores.  Every load of a round is issued
 // before the previous round's stores (vmcnt counts loads and stores together, in issue order).
-#include <climits>
-
 #include "pdg_common.hpp"
 #include "pdg_runtime.hpp"
 #include "pdg_x6.hpp"
@@ -1185,18 +1183,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // reused by the edges of the mesh neighbours of its nodes, about +-13 rounds away in dst order: with
 // per-block ranges every block of an XCD keeps such a window live (32 x ~280 KB, over the 4 MiB L2, so
 // the reuse was served by the Infinity Cache), with interleaved rounds the XCD has one window.
-//
-// DL (dst rows from LDS; with D): a round's rows are dst-sorted, so its destination nodes are one short
-// range dlo .. dhi (about 6 nodes at config 2, a node's incoming edges being adjacent rows).  The P (and,
-// with EU, Q) rows of that range are loaded whole-row once per round into an LDS tile (issued a round
-// ahead beside the row loads, written to the tile in stage) and the message's P[dst] / the edge update's
-// Q[dst] are read from it instead of being gathered per edge: half the gathers become LDS reads.  The
-// caller guarantees that every 32-row group's dst values span fewer than EFC_DN nodes (the launcher
-// checks the span the engine measured per graph plan); bitwise the same outputs.
-constexpr int EFC_DN = 16;                            // tile rows per array
-constexpr int EFC_DS = L + 4;                         // tile row stride in floats: rows 4 banks apart
-constexpr int EFC_DL_BYTES = 2 * EFC_DN * EFC_DS * 4;  // P rows, then Q rows
-template <bool RES, bool EU, bool SEG, bool D = false, bool X = false, bool DL = false>
+template <bool RES, bool EU, bool SEG, bool D = false, bool X = false>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
@@ -1216,10 +1203,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   double* carry = reinterpret_cast<double*>(sdst0 + 2 * X6_ROWS);   // open segment's sum, 2 rows
   float* t_am = t_e + X6_ROWS * EFC_ES;                        // D: a2m / a2e tiles (in place of SEG's)
   float* t_ae = t_am + EFC_TILE;
-  float* t_d = t_ae + EFC_TILE;                                // DL: the round's dst rows of P, Q
   static_assert(!(SEG && D), "deferred a2 stores and the segment sums use the same LDS");
   static_assert(!(SEG && X), "the segment sums need contiguous block ranges");
-  static_assert(!DL || D, "the dst row tile follows the deferred a2 tiles");
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
@@ -1237,13 +1222,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
   f32x4 xa[2], xr[2];
   int dq[2], sq[2];
-  // DL: dn (even lanes / odd lanes) = dst of the first / last row of the round after the one issue() loads
-  // rows for, dlo_n = the first dst node of that round (its tile's row 0), pdv = this thread's share of
-  // its tile: (EU) array t >> 8, rows ((t >> 5) & 7) + 8v, or rows t >> 5 of P alone
-  constexpr int NDV = EU ? 2 : 1;
-  int dn = 0, dlo_n = 0;
-  f32x4 pdv[NDV];
-  const int dv_arr = EU ? threadIdx.x >> 8 : 0, dv_row = EU ? (threadIdx.x >> 5) & 7 : threadIdx.x >> 5;
   // the row outputs through range-checked buffer stores: no memory operation of the loop is
   // conditional, so the compiler's vmcnt counts stay exact (a store skipped on some path made them
   // collapse).  An omitted output (a1m / a1e in inference, a2m beside the inference sums) gets an
@@ -1263,15 +1241,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       dq[u] = dst[pr];
       sq[u] = src[pr];
     }
-    if (DL) {   // the round's dst rows dlo .. min(dlo + 15, dhi) (dn loaded one issue earlier), and dn ahead
-      const int lo = __builtin_amdgcn_readlane(dn, 0), hi = __builtin_amdgcn_readlane(dn, 1);
-      dlo_n = lo;
-      const float* A = dv_arr ? Q : P;
-#pragma unroll
-      for (int v = 0; v < NDV; ++v)
-        pdv[v] = *reinterpret_cast<const f32x4*>(A + (size_t)min(lo + dv_row + 8 * v, hi) * L + 4 * cg);
-      dn = dst[clamp_row(base + stride + (l & 1) * (X6_ROWS - 1), r1)];
-    }
   };
   auto stage = [&](int base) {
 #pragma unroll
@@ -1287,11 +1256,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       }
       rows_store4_nt(rs_e, base + r - r0, 4 * cg, e);
       *reinterpret_cast<f32x4*>(t_e + r * EFC_ES + 4 * cg) = ok ? e : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (DL) {   // the dst row tile (its last reads, the previous round's, came before the second barrier)
-#pragma unroll
-      for (int v = 0; v < NDV; ++v)
-        *reinterpret_cast<f32x4*>(t_d + (dv_arr * EFC_DN + dv_row + 8 * v) * EFC_DS + 4 * cg) = pdv[v];
     }
   };
   // SEG: the node of the previous block's last edge (a segment of it here is a head partial),
@@ -1352,7 +1316,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     }
     prev_last = sdst[nr - 1];
   };
-  if (DL) dn = dst[clamp_row(first + (l & 1) * (X6_ROWS - 1), r1)];
   issue(first);   // E > 0: an empty block (first = r1 = E) reads row E - 1
   {
     const float* pc = W1 + (size_t)(16 * w + (l & 15)) * (3 * L) + 2 * L + 4 * (l >> 4);
@@ -1379,7 +1342,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     pin_vgpr(dq[u]);
     pin_vgpr(sq[u]);
   }
-  if (DL) pin_vgpr(dn);
   stage(first);
   for (int base = first; base < r1; base += stride) {
     __syncthreads();   // e tile complete
@@ -1390,17 +1352,13 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     // gathers are waited for in the C product below, and with the next round's HBM loads issued
     // ahead of them (vmcnt counts in issue order) every round waited for those too
     f32x4 gpd[2], gqs[2], gps[2], gqd[2];
-    const int dlo = dlo_n;   // DL: this round's tile row 0 (issue() below moves on to the next round's)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
-      const int rr = min(max(dc[nb] - dlo, 0), EFC_DN - 1);
-      gpd[nb] = DL ? *reinterpret_cast<const f32x4*>(t_d + rr * EFC_DS + oc)
-                   : *reinterpret_cast<const f32x4*>(P + (size_t)dc[nb] * L + oc);
+      gpd[nb] = *reinterpret_cast<const f32x4*>(P + (size_t)dc[nb] * L + oc);
       gqs[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)sc[nb] * L + oc);
       if (EU) {
         gps[nb] = *reinterpret_cast<const f32x4*>(P + (size_t)sc[nb] * L + oc);
-        gqd[nb] = DL ? *reinterpret_cast<const f32x4*>(t_d + (EFC_DN + rr) * EFC_DS + oc)
-                     : *reinterpret_cast<const f32x4*>(Q + (size_t)dc[nb] * L + oc);
+        gqd[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)dc[nb] * L + oc);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -2427,7 +2385,7 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
                                 const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                                 const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                                 double* part_e, int with_edge_update, double* sums, double* seg_part, int* seg_info,
-                                int dst_span, int nblocks, void* stream);
+                                int nblocks, void* stream);
 
 // deferred a2 stores in the cooperative edge forward (edge_fwd_coop_kernel's D)
 // (default: bitwise the same outputs; with X below 216 -> 210.5 us per config-2 call, the step -0.05 ms, in
@@ -2446,23 +2404,8 @@ extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln
                                  const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                                  double* part_e, int with_edge_update, int nblocks, void* stream) {
   return edge_fwd_coop_launch(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m,
-                              a2m, a1e, a2e, part_m, part_e, with_edge_update, nullptr, nullptr, nullptr, INT_MAX,
-                              nblocks, stream);
-}
-
-// pdg_edge_fwd_coop for dst-sorted rows whose every 32-row group (rows 32i .. 32i + 31) has dst values
-// spanning dst_span nodes at most (dst[last] - dst[first]); below EFC_DN the round's dst rows of P and Q
-// come from an LDS tile (edge_fwd_coop_kernel's DL), otherwise this is pdg_edge_fwd_coop
-extern "C" int pdg_edge_fwd_coop_span(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                                      const float* ln_b, const float* e_res, float* e_out, const int* src,
-                                      const int* dst, const float* P, const float* Q, const float* W1, const float* b1,
-                                      const float* W2, const float* b2, float* a1m, float* a2m, float* a1e, float* a2e,
-                                      double* part_m, double* part_e, int with_edge_update, int dst_span, int nblocks,
-                                      void* stream) {
-  PDG_CHECK_ARG(dst_span >= 0, "pdg_edge_fwd_coop_span: dst_span must be >= 0");
-  return edge_fwd_coop_launch(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m,
-                              a2m, a1e, a2e, part_m, part_e, with_edge_update, nullptr, nullptr, nullptr, dst_span,
-                              nblocks, stream);
+                              a2m, a1e, a2e, part_m, part_e, with_edge_update, nullptr, nullptr, nullptr, nblocks,
+                              stream);
 }
 
 extern "C" int pdg_edge_fwd_coop_seg(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
@@ -2472,8 +2415,8 @@ extern "C" int pdg_edge_fwd_coop_seg(int n_edges, const float* a2_prev, const pd
                                      double* part_m, double* part_e, int with_edge_update, double* sums,
                                      double* seg_part, int* seg_info, int nblocks, void* stream) {
   return edge_fwd_coop_launch(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m,
-                              a2m, a1e, a2e, part_m, part_e, with_edge_update, sums, seg_part, seg_info, INT_MAX,
-                              nblocks, stream);
+                              a2m, a1e, a2e, part_m, part_e, with_edge_update, sums, seg_part, seg_info, nblocks,
+                              stream);
 }
 
 static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
@@ -2481,7 +2424,7 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
                                 const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                                 const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                                 double* part_e, int with_edge_update, double* sums, double* seg_part, int* seg_info,
-                                int dst_span, int nblocks, void* stream) {
+                                int nblocks, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd_coop: n_edges must be > 0");
   PDG_CHECK_ARG(nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_fwd_coop: bad nblocks");
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
@@ -2499,27 +2442,21 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
   // the XCD-interleaved rounds are compiled for the 256-block grid; any other grid (tests, other parts)
   // walks contiguous block ranges
   const bool xcd = PDG_EFC_XCD && !seg && nblocks == XCD_GRID;
-  // the dst row tile: deferred a2 stores and the XCD grid only (the production launch; 148 KB of LDS)
-  const bool dl = defer && xcd && dst_span < EFC_DN;
   const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float) + (seg ? EFC_SEG_BYTES : 0) +
-                     (defer ? 2 * EFC_TILE * sizeof(float) : 0) + (dl ? EFC_DL_BYTES : 0);
+                     (defer ? 2 * EFC_TILE * sizeof(float) : 0);
   hipStream_t s = (hipStream_t)stream;
-#define PDG_EFC_X(R, U, S, X, DL)                                                                                     \
-  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER, X, DL>), \
+#define PDG_EFC_X(R, U, S, X)                                                                                         \
+  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER, X>), \
                      dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
                      ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e,  \
                      sums, seg_part, seg_info)
-#define PDG_EFC(R, U, S)                                                  \
-  do {                                                                    \
-    if (!(S) && PDG_EFC_XCD && xcd) {                                     \
-      if (!(S) && PDG_EFC_DEFER && dl) {                                  \
-        PDG_EFC_X(R, U, S, (!(S) && PDG_EFC_XCD), (!(S) && PDG_EFC_DEFER)); \
-      } else {                                                            \
-        PDG_EFC_X(R, U, S, (!(S) && PDG_EFC_XCD), false);                 \
-      }                                                                   \
-    } else {                                                              \
-      PDG_EFC_X(R, U, S, false, false);                                   \
-    }                                                                     \
+#define PDG_EFC(R, U, S)                           \
+  do {                                             \
+    if (!(S) && PDG_EFC_XCD && xcd) {              \
+      PDG_EFC_X(R, U, S, (!(S) && PDG_EFC_XCD));   \
+    } else {                                       \
+      PDG_EFC_X(R, U, S, false);                   \
+    }                                              \
   } while (0)
 #define PDG_EFC2(S)                                                \
   if (e_res) {                                                     \

@@ -81,9 +81,6 @@ VARIANTS = {
     # edge forward in the block-cooperative layout (pdg_edge_fwd_coop; 240 -> 230 us per call at config 2)
     # instead of pdg_edge_fwd
     "coop_fwd": ("PDG_EDGE_FWD_COOP", True),
-    # cooperative edge forward: the P[dst] / Q[dst] rows of a 32-row round from an LDS tile loaded once per
-    # destination node (pdg_edge_fwd_coop_span, when the plan's dst_span32 < 16) instead of gathered per edge
-    "dst_rows_lds": ("PDG_DST_ROWS_LDS", False),
     # inference: the cooperative edge forward also forms the aggregation's message sums in fp64
     # (pdg_edge_fwd_coop_seg + pdg_segsum_fixup; pdg_segsum_finish applies the message LayerNorm) instead of
     # pdg_segment_sum re-reading a2m, and a2m is not stored (config 5: 11.8 -> 11.5 ms per step, same box).
@@ -214,7 +211,6 @@ class EPDEngine:
         self.gz1e_from_gc = var["gz1e_from_gc"]
         self.fused_edge_bwd = var["fused_edge_bwd"]
         self.coop_fwd = var["coop_fwd"]
-        self.dst_rows_lds = var["dst_rows_lds"]
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
         self.seg_sums = self.coop_fwd and var["seg_sums"]
@@ -364,13 +360,10 @@ class EPDEngine:
                 self._nparts.value = self._nslabs_e
                 lib.pdg_segsum_fixup(self._nslabs_e, _p(self._seg_part), _p(self._seg_info), _p(sums), s)
             elif E and self.coop_fwd:
-                # dst_rows_lds: the launcher reads the round's dst rows of P / Q from an LDS tile when the
-                # plan's 32-row groups span few enough destination nodes (plan.dst_span32)
-                span = plan.dst_span32 if self.dst_rows_lds else 2 ** 31 - 1
-                self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop_span, E, _p(a2e_prev),
-                        ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm),
-                        _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e),
-                        _p(self._part_a), _p(self._part_b), int(eu), span, self._nslabs_e, s)
+                self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop, E, _p(a2e_prev), ste_prev,
+                        _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm),
+                        _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a),
+                        _p(self._part_b), int(eu), self._nslabs_e, s)
                 self._nparts.value = self._nslabs_e
             elif E:
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),

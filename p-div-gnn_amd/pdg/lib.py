@@ -76,7 +76,6 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_edge_fwd_coop_seg": [I] + [P] * 20 + [I, P, P, P, I, P],
-    "pdg_edge_fwd_coop_span": [I] + [P] * 20 + [I, I, I, P],
     "pdg_segsum_fixup": [I, P, P, P, P],
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],

@@ -47,13 +47,6 @@ class GraphPlan:
         self.src = src[order].to(torch.int32).contiguous()
         self.dst = dst[order].to(torch.int32).contiguous()
         self.rowptr_dst = _rowptr(dst, n)
-        # the widest destination range of a 32-row group of the sorted edges (dst[32i + 31] - dst[32i]; the
-        # cooperative edge forward's rounds are such groups): pdg_edge_fwd_coop_span's guarantee
-        self.dst_span32 = 0
-        if self.n_edges:
-            lo = torch.arange(0, self.n_edges, 32, device=dev)
-            hi = torch.clamp(lo + 31, max=self.n_edges - 1)
-            self.dst_span32 = int((self.dst[hi] - self.dst[lo]).max())
         key2 = self.src.long() * n + self.dst.long()
         self.perm_src = torch.sort(key2, stable=True).indices.to(torch.int32).contiguous()
         self.rowptr_src = _rowptr(src, n)

@@ -338,36 +338,6 @@ def test_forward_variants_agree(nmesh, ngraph, steps):
             assert rel(g, g0[name]) < VARIANT_TOL, (key, name, rel(g, g0[name]))
 
 
-@pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
-def test_dst_rows_lds_is_bitwise_the_gathering_edge_forward(nmesh, ngraph, steps):
-    """Engine variant dst_rows_lds (pdg_edge_fwd_coop_span reading a round's P[dst] / Q[dst] rows from an
-    LDS tile) against the gathering edge forward through a whole training step and an inference pass:
-    output, loss and every parameter gradient bit for bit (the same values reach the same arithmetic)."""
-    from gnn_local_stress import losses
-    from pdg import meshgen
-    samples = meshgen.make_dataset(ngraph, n=nmesh, hole_radius=(0.15, 0.3), seed=7)
-    batch = make_batch(samples)
-    stats = {k: float(v) for k, v in dataset_stats(batch).items()}
-    res = {}
-    for dl in (False, True):
-        model = _model(steps, stats)
-        eng = model._engine_for(batch.pos.device)
-        eng.dst_rows_lds = dl
-        with torch.no_grad():
-            y_inf = model(batch, scale_output=True).local_stress.clone()
-        pred = model(batch, scale_output=False).local_stress
-        gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
-        total, _, _ = losses.batch_loss(pred, batch, gt, divergence=True, divergence_penalty=10.0)
-        total.backward()
-        res[dl] = (y_inf, float(total.detach()), {n: p.grad.detach().clone() for n, p in model.named_parameters()})
-    from pdg.plan import GraphPlan
-    assert GraphPlan(batch.edge_index, batch.num_nodes).dst_span32 < 16
-    (y0, t0, g0), (y1, t1, g1) = res[False], res[True]
-    assert torch.equal(y0, y1) and t0 == t1
-    for name, g in g1.items():
-        assert torch.equal(g, g0[name]), name
-
-
 def test_edgeless_batch_matches_oracle():
     """A batch whose graphs have no edge at all (SURVEY §4 T1 'E=0 graphs'): as in the reference,
     every message aggregate is zero and the edge parameters get zero gradients; output and every

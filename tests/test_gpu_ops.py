@@ -776,78 +776,6 @@ def test_edge_fwd_coop_matches_edge_fwd(env, E, eu, res):
         assert rel(pe1, pe0) < 1e-6
 
 
-def _span_graph(kind, g):
-    """dst-sorted edge lists for pdg_edge_fwd_coop_span: (N, E, dst)."""
-    if kind == "mesh":        # degree 6 everywhere (a periodic triangle mesh): 6-7 nodes per round
-        N = 3000
-        dst = torch.arange(N).repeat_interleave(6)
-    elif kind == "holes":     # degrees 2 .. 9 and isolated nodes (mesh holes): up to ~16 nodes per round
-        N = 4000
-        deg = torch.randint(2, 10, (N,), generator=g)
-        deg[torch.randint(0, N, (300,), generator=g)] = 0
-        dst = torch.arange(N).repeat_interleave(deg)
-    elif kind == "deg2":      # 16 nodes per round: the whole tile
-        N = 2500
-        dst = torch.arange(N).repeat_interleave(2)
-    elif kind == "deg1":      # 32 nodes per round: over the tile, the launcher gathers
-        N = 1000
-        dst = torch.arange(N)
-    else:                     # tiny: fewer rounds than blocks (empty blocks), ragged last round
-        N = 30
-        dst = torch.sort(torch.randint(0, N, (77,), generator=g)).values
-    return N, dst.numel(), dst.int()
-
-
-@pytest.mark.parametrize("kind,eu,res", [("mesh", 1, 1), ("mesh", 0, 1), ("holes", 1, 0), ("deg2", 1, 1),
-                                         ("deg2", 0, 0), ("deg1", 1, 1), ("tiny", 1, 1)])
-def test_edge_fwd_coop_span_matches_coop(env, kind, eu, res):
-    """pdg_edge_fwd_coop_span (dst rows of P / Q from an LDS tile when the plan's 32-row groups span < 16
-    nodes) against pdg_edge_fwd_coop on the engine's 256-block grid: every output and the LayerNorm
-    partials bitwise (the same values, read from LDS instead of gathered).  The span is measured as
-    GraphPlan measures it, and a graph over the tile's reach (deg1) takes the gathering kernel."""
-    from pdg.plan import GraphPlan
-    lib, sh, _ = env
-    s = sh()
-    g = torch.Generator().manual_seed(11)
-    N, E, dst_c = _span_graph(kind, g)
-    src = torch.randint(0, N, (E,), generator=g).int()
-    span = GraphPlan(torch.stack([src, dst_c]).long(), N).dst_span32
-    assert (span < 16) == (kind != "deg1"), span
-    dst, src = dst_c.cuda(), src.cuda()
-    a2p, eres = torch.relu(rnd(E, L)), rnd(E, L)
-    Pn, Qn = rnd(N, L), rnd(N, L)
-    W1, b1 = lin(L, 3 * L)
-    W2, b2 = lin(L, L)
-    lg, lbv = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
-    part = torch.empty(4096, dtype=torch.float64, device="cuda")
-    n = ctypes.c_int(0)
-    tmp = torch.empty(E, L, device="cuda")
-    lib.pdg_mlp2_fwd(E, a2p.data_ptr(), W2.data_ptr(), b2.data_ptr(), tmp.data_ptr(), part.data_ptr(),
-                     ctypes.byref(n), s)
-    st = finalize(lib, s, part, n.value, E * L)
-    nb = 256
-    runs = []
-    for fn in ("coop", "span"):
-        o = {k: torch.full((E, L), float("nan"), device="cuda") for k in ("e", "a1m", "a2m", "a1e", "a2e")}
-        pm = torch.zeros(4096, dtype=torch.float64, device="cuda")
-        pe = torch.zeros(4096, dtype=torch.float64, device="cuda")
-        args = (E, a2p.data_ptr(), st.data_ptr(), lg.data_ptr(), lbv.data_ptr(), eres.data_ptr() if res else None,
-                o["e"].data_ptr(), src.data_ptr(), dst.data_ptr(), Pn.data_ptr(), Qn.data_ptr(), W1.data_ptr(),
-                b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), o["a1m"].data_ptr(), o["a2m"].data_ptr(),
-                o["a1e"].data_ptr() if eu else None, o["a2e"].data_ptr() if eu else None,
-                pm.data_ptr(), pe.data_ptr() if eu else None, eu)
-        if fn == "coop":
-            lib.pdg_edge_fwd_coop(*args, nb, s)
-        else:
-            lib.pdg_edge_fwd_coop_span(*args, span, nb, s)
-        runs.append((o, pm[: 2 * nb].clone(), pe[: 2 * nb].clone()))
-    (o0, pm0, pe0), (o1, pm1, pe1) = runs
-    for k in ("e", "a1m", "a2m") + (("a1e", "a2e") if eu else ()):
-        assert not torch.isnan(o0[k]).any(), k
-        assert torch.equal(o0[k], o1[k]), k
-    assert torch.equal(pm0, pm1) and torch.equal(pe0, pe1)
-
-
 def _seg_graph(kind, g):
     """dst-sorted edge lists that exercise the message-sum segmentation of pdg_edge_fwd_coop_seg."""
     if kind == "random":      # ~13 edges per node, isolated nodes, segments across block ends
