@@ -243,10 +243,10 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
     or 6x that in bf16 (bf16x6)."""
     g = 2 * L * L
     out = {
-        # W_c product (fp32 MFMA) + 2 W2 products (bf16x6) per edge; reads a2e_prev, e_prev, 4 gathered
-        # P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e;
+        # W_c product + 2 W2 products (all bf16x6 since round 5) per edge; reads a2e_prev, e_prev, 4
+        # gathered P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e;
         # seg: also the N message sums rows, and a2m only when training
-        "edge_fwd": ([(E * g, PEAK_FP32_MFMA), (E * 2 * g * X6, PEAK_BF16_MFMA)],
+        "edge_fwd": ([(E * 3 * g * X6, PEAK_BF16_MFMA)],
                      E * ((9 if infer else 11) * 4 * L + 8) - (E * 4 * L if (seg and infer) else 0)
                      + (8 * L * N if seg else 0)),
         # fused (pdg_edge_bwd_w2): 2 W2^T products + 2 weight-gradient products per edge (bf16x6);

@@ -41,6 +41,12 @@ constexpr int EBW_IMG = 3 * X6_TERM;        // one bf16x6 image of 32 rows (24 K
 #ifndef PDG_EFWD_X6F   // 1: the edge forward's W2 products in gemm_x6f's unbiased form (A/B only)
 #define PDG_EFWD_X6F 0
 #endif
+// the cooperative edge forward's C = Wc e as an unbiased bf16x6 product (gemm_x6f, the lo terms of Wc's
+// K chunks 0-1 in LDS) instead of fp32 MFMAs (0: A/B only).  Round 5: edge_fwd 211.4-212.9 -> 205.3-206.3 us
+// per config-2 call, the step -0.07 ms in two same-box pairs; every parity gate green (EXPERIMENTS §4).
+#ifndef PDG_EFWD_CX6
+#define PDG_EFWD_CX6 1
+#endif
 #ifndef PDG_MSK_STRIDE
 #define PDG_MSK_STRIDE 136
 #endif
@@ -1143,9 +1149,11 @@ __global__ __launch_bounds__(512) void enc_narrow_reduce_kernel(const double* __
 //   | barrier | a1 rows stored (training)
 //   product  a2 = relu(W2 a1 + b2) -> LayerNorm partials, row tiles
 //   | barrier | a2 rows stored; the next round's stage
-// C = Wc e is an exact fp32 product (v_mfma_f32_16x16x4_f32, Wc rows as register A fragments, e
-// from an fp32 row tile): bitwise edge_fwd_kernel's C.  (C in bf16x6 biased the LayerNorm statistics
-// the way bf16x6 node_net did: parameter gradients 2e-4 from fp64 instead of 2.5e-6, measured.)
+// C = Wc e is an UNBIASED bf16x6 product (gemm_x6f from an e image; Wc as bf16 terms, the lo terms of
+// its first two K chunks in LDS), round 5.  Rounds 2-4 kept C an exact fp32 product (v_mfma_f32_16x16x4_f32,
+// still the -DPDG_EFWD_CX6=0 build): C in the BIASED bf16x6 chain had shifted the LayerNorm statistics the
+// way bf16x6 node_net did (parameter gradients 2e-4 from fp64 instead of 2.5e-6), a bias gemm_x6f does not
+// have (rms error 3.6x below the fp32 MFMA chain's).  The fp32 C was half of this kernel's matrix time.
 //
 // With SEG the kernel also forms the message sums of the aggregation (models.py:215-217) from
 // the a2m row tile: sums[v] = sum over v's incoming edges of a2m (raw, before the message
@@ -1198,11 +1206,17 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   float* t_m = reinterpret_cast<float*>(sm + 2 * EBW_IMG);     // fp32 row tiles: a1m / a2m
   float* t_x = t_m + EFC_TILE;                                 //                 a1e / a2e
   float* t_e = t_x + EFC_TILE;                                 //                 e_t
-  float* t_s = t_e + X6_ROWS * EFC_ES;                         // SEG: a2m tiles (by round parity)
+  // PDG_EFWD_CX6: e as a bf16x6 image in the tile's place (24 instead of 17 KB)
+  unsigned char* img_e = reinterpret_cast<unsigned char*>(t_e);
+  constexpr int E_BYTES = PDG_EFWD_CX6 ? EBW_IMG : X6_ROWS * EFC_ES * 4;
+  float* t_s = reinterpret_cast<float*>(img_e + E_BYTES);      // SEG: a2m tiles (by round parity)
   int* sdst0 = reinterpret_cast<int*>(t_s + 2 * EFC_TILE);     //      dst of the rounds' rows
   double* carry = reinterpret_cast<double*>(sdst0 + 2 * X6_ROWS);   // open segment's sum, 2 rows
-  float* t_am = t_e + X6_ROWS * EFC_ES;                        // D: a2m / a2e tiles (in place of SEG's)
+  float* t_am = t_s;                                           // D: a2m / a2e tiles (in place of SEG's)
   float* t_ae = t_am + EFC_TILE;
+  // PDG_EFWD_CX6: the lo bf16 terms of Wc's K chunks 0 and 1 in LDS, after every region (with all 12 terms
+  // in registers the main instantiation spilled 5 VGPRs and was no faster than fp32 MFMAs)
+  unsigned char* wlo = reinterpret_cast<unsigned char*>(t_s) + (SEG ? EFC_SEG_BYTES : 0) + (D ? 2 * EFC_TILE * 4 : 0);
   static_assert(!(SEG && D), "deferred a2 stores and the segment sums use the same LDS");
   static_assert(!(SEG && X), "the segment sums need contiguous block ranges");
   const int l = lane_id(), w = wave_id();
@@ -1214,7 +1228,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   row_schedule(X, E, r0, r1, first, stride);
   // the weights as A operands, rows = output features 16w .. 16w + 15 (W is out x in, row-major):
   // Wc = W1[:, 256:384] (row stride 384), W2
+#if PDG_EFWD_CX6
+  WSlice wsc;     // Wc as bf16 terms (gemm_x6f's A operand)
+#else
   f32x4 wcf[8];   // Wc rows 16w + (l & 15), inputs 16T + 4(l >> 4) .. +3 (node_pq_rw's A fragments)
+#endif
   WSlice ws2;     // both loaded after the first round's row loads (the round trips overlap)
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg), bb4 = *reinterpret_cast<const f32x4*>(lb + 4 * cg);
@@ -1255,7 +1273,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         e[j] = y;
       }
       rows_store4_nt(rs_e, base + r - r0, 4 * cg, e);
+#if PDG_EFWD_CX6
+      img_store4(img_e, r, cg, ok ? e : f32x4{0.f, 0.f, 0.f, 0.f});
+#else
       *reinterpret_cast<f32x4*>(t_e + r * EFC_ES + 4 * cg) = ok ? e : f32x4{0.f, 0.f, 0.f, 0.f};
+#endif
     }
   };
   // SEG: the node of the previous block's last edge (a segment of it here is a head partial),
@@ -1317,18 +1339,32 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     prev_last = sdst[nr - 1];
   };
   issue(first);   // E > 0: an empty block (first = r1 = E) reads row E - 1
+#if PDG_EFWD_CX6
+  load_wslice(wsc, W1 + 2 * L, w, 3 * L);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) *reinterpret_cast<bf16x8*>(wlo + ((2 * w + ks) * 64 + l) * 16) = wsc.a[ks][2];
+#else
   {
     const float* pc = W1 + (size_t)(16 * w + (l & 15)) * (3 * L) + 2 * L + 4 * (l >> 4);
 #pragma unroll
     for (int T = 0; T < 8; ++T) wcf[T] = *reinterpret_cast<const f32x4*>(pc + 16 * T);
   }
+#endif
   load_wslice(ws2, W2, w);
   // the loop-invariant weights and biases are in registers before the loop (an empty asm using them
   // here): left to the compiler, their loads were sunk to the loop's preheader, still in flight at
   // the loop head, and the count merged there made every round's C product wait for the previous
   // round's stores (vmcnt 23 .. 16)
+#if PDG_EFWD_CX6
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      if (p < 2 || ks >= 2) pin_vgpr(wsc.a[ks][p]);
+#else
 #pragma unroll
   for (int T = 0; T < 8; ++T) pin_vgpr(wcf[T]);
+#endif
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
@@ -1375,6 +1411,15 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     }
     // ---- C = Wc e + b1 and the two first layers at this wave's 16 features
     f32x4 d[2];
+#if PDG_EFWD_CX6   // C = Wc e as an unbiased bf16x6 product (gemm_x6f), 2.7x less matrix time than fp32 MFMAs
+    d[0] = d[1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    {
+      WSlice wc = wsc;   // the lo terms of K chunks 0-1 from LDS
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) wc.a[ks][2] = *reinterpret_cast<const bf16x8*>(wlo + ((2 * w + ks) * 64 + l) * 16);
+      gemm_x6f<2, X6_TERM, true>(d, wc, img_e);
+    }
+#else
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {   // the MFMA order of gemm128: step (T, jj) sums inputs 16T + 4k + jj
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -1387,6 +1432,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       }
       d[nb] = acc;
     }
+#endif
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
       const int r = 16 * nb + (l & 15);
@@ -2442,8 +2488,9 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
   // the XCD-interleaved rounds are compiled for the 256-block grid; any other grid (tests, other parts)
   // walks contiguous block ranges
   const bool xcd = PDG_EFC_XCD && !seg && nblocks == XCD_GRID;
-  const size_t shm = 2 * EBW_IMG + (2 * EFC_TILE + X6_ROWS * EFC_ES) * sizeof(float) + (seg ? EFC_SEG_BYTES : 0) +
-                     (defer ? 2 * EFC_TILE * sizeof(float) : 0);
+  const size_t shm = 2 * EBW_IMG + 2 * EFC_TILE * sizeof(float) + (PDG_EFWD_CX6 ? EBW_IMG : X6_ROWS * EFC_ES * 4) +
+                     (seg ? EFC_SEG_BYTES : 0) + (defer ? 2 * EFC_TILE * sizeof(float) : 0) +
+                     (PDG_EFWD_CX6 ? 2 * EBW_WAVES * 64 * 16 : 0);
   hipStream_t s = (hipStream_t)stream;
 #define PDG_EFC_X(R, U, S, X)                                                                                         \
   hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER, X>), \
