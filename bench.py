@@ -56,7 +56,7 @@ TREE_GLOBS = ("p-div-gnn_amd/pdg/libpdivgnn_hip.so", "p-div-gnn_amd/csrc/*.hip",
               "p-div-gnn_amd/gnn_local_stress/*.py", "bench.py")
 PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
              "edge_bwd": "void edge_bwd_kernel<true>",
-             "segment_sum": ("segment_sum_kernel", "segsum_finish_kernel"), "node_net": ("node_net_x6_kernel", "node_net_pair_kernel", "node_net_kernel"),
+             "segment_sum": ("segment_sum_kernel",), "node_net": ("node_net_x6_kernel", "node_net_pair_kernel", "node_net_kernel"),
              # the edge-update steps' instantiation (gz1e formed as gC - gz1m); the last step's is <false>
              "pq_scatter_bwd": ("void pq_scatter_bwd_kernel<true>", "pq_scatter_bwd_kernel"),
              "wgrad_W2": "wgrad_x6_kernel",
@@ -235,8 +235,8 @@ def cpu_baseline(cfg, samples, full_graphs: int, reps: int = 5, one_thread: bool
 
 
 # ---------------------------------------------------------------------------------- roofline
-def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, seg: bool = False,
-                e_sum: bool = True, one_pass: bool = False) -> dict:
+def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, e_sum: bool = True,
+                one_pass: bool = False) -> dict:
     """Algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops with the peak of their
     instruction type, and the bytes the kernel must read/write (inputs once, outputs once, int32
     indices).  An fp32-accurate 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA,
@@ -244,11 +244,9 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
     g = 2 * L * L
     out = {
         # W_c product + 2 W2 products (all bf16x6 since round 5) per edge; reads a2e_prev, e_prev, 4
-        # gathered P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e;
-        # seg: also the N message sums rows, and a2m only when training
+        # gathered P/Q rows, src, dst; writes e_t, a2m, a2e and, when training, a1m, a1e
         "edge_fwd": ([(E * 3 * g * X6, PEAK_BF16_MFMA)],
-                     E * ((9 if infer else 11) * 4 * L + 8) - (E * 4 * L if (seg and infer) else 0)
-                     + (8 * L * N if seg else 0)),
+                     E * ((9 if infer else 11) * 4 * L + 8)),
         # fused (pdg_edge_bwd_w2): 2 W2^T products + 2 weight-gradient products per edge (bf16x6);
         # reads gaggr[dst], ge_next, a2m, a1m, a2e, a1e, dst; writes gz1m, gC (+ gz1e unless e_sum: the
         # P/Q gather backward forms it from gC - gz1m); one slab read+write per block.  unfused
@@ -261,10 +259,8 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
         "edge_gout": ([(E * 2 * g * X6, PEAK_BF16_MFMA)], E * 5 * 4 * L + 2 * nslab_bytes),
         # all steps' W2 segments: 2E rows per step of (G, X) 512-byte rows, one 64 KB slab per block
         "wgrad_W2": ([(S * 2 * E * g * X6, PEAK_BF16_MFMA)], S * 2 * E * 2 * 4 * L + 512 * (L * L + L) * 4),
-        # dst-segment sum of LN(a2m): reads a2m (E rows) and rowptr, writes aggr (+ x-hat sums); seg
-        # (pdg_segsum_finish): reads the fp64 message sums and rowptr, writes aggr
-        "segment_sum": ([], (8 * L * N + 4 * (N + 1) + 4 * L * N) if seg
-                        else 4 * L * E + 4 * (N + 1) + (1 if infer else 2) * 4 * L * N),
+        # dst-segment sum of LN(a2m): reads a2m (E rows) and rowptr, writes aggr (+ x-hat sums)
+        "segment_sum": ([], 4 * L * E + 4 * (N + 1) + (1 if infer else 2) * 4 * L * N),
         # node_net, 2 fp32-accurate GEMMs (K = 256, 128) per node as bf16x6 products (node_net_x6_kernel;
         # the fp32-MFMA kernels are A/B build variants): reads aggr, x; writes a2n (+ a1n)
         "node_net": ([(N * 2 * L * (2 * L + L) * X6, PEAK_BF16_MFMA)],
@@ -522,10 +518,8 @@ def time_config(cid: int, args, rank: int, world: int, pg, device, with_pmc: boo
     ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
     fused = eng.fused_edge_wgrad
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
-    # the fused message sums run in inference only unless PDG_SEG_SUMS_TRAIN=1 (engine.py:253)
-    seg = getattr(eng, "seg_sums", False) if infer else getattr(eng, "seg_sums_train", False)
     one_pass = fused and getattr(eng, "fused_edge_bwd", False)
-    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, seg, fused and getattr(eng, "gz1e_from_gc", False),
+    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, fused and getattr(eng, "gz1e_from_gc", False),
                        one_pass)
     comp = compulsory_bytes(work, N, E)
     pmc_path, pmc_reason = pmc_file() if with_pmc else (None, "not collected for this config")

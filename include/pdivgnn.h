@@ -296,23 +296,6 @@ int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, 
                       const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                       const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                       double* part_e, int with_edge_update, int nblocks, void* stream);
-/* pdg_edge_fwd_coop that also forms the aggregation's message sums (models.py:215-217) from its
- * a2m tiles, replacing pdg_segment_sum's re-read of a2m: sums[v] (fp64, N x 128) = sum of a2m over
- * v's incoming edges, raw (the message LayerNorm's statistics come out of this launch); rows of
- * nodes without edges are not written.  A node whose edges run across a block end is completed
- * by pdg_segsum_fixup from seg_part (2 x nblocks x 128 doubles) and seg_info (4 x nblocks ints);
- * pdg_segsum_finish then forms aggr = g (sums - deg mean) / den + deg b and, when xhat_sum != NULL,
- * xhat_sum = (sums - deg mean) / den: pdg_segment_sum's outputs (fp64, rounded once).
- * a2m may be NULL (inference: the rows have no other consumer). */
-int pdg_edge_fwd_coop_seg(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                          const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
-                          const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
-                          const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
-                          double* part_e, int with_edge_update, double* sums, double* seg_part, int* seg_info,
-                          int nblocks, void* stream);
-int pdg_segsum_fixup(int nblocks, const double* seg_part, const int* seg_info, double* sums, void* stream);
-int pdg_segsum_finish(int n_nodes, const double* sums, const int* rowptr, const pdg_ln_stat* st,
-                      const float* ln_g, const float* ln_b, float* aggr, float* xhat_sum, void* stream);
 int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                  const float* a2m, const float* a1m, const float* a2e, const float* a1e,
                  const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,

@@ -1154,52 +1154,31 @@ __global__ __launch_bounds__(512) void enc_narrow_reduce_kernel(const double* __
 // still the -DPDG_EFWD_CX6=0 build): C in the BIASED bf16x6 chain had shifted the LayerNorm statistics the
 // way bf16x6 node_net did (parameter gradients 2e-4 from fp64 instead of 2.5e-6), a bias gemm_x6f does not
 // have (rms error 3.6x below the fp32 MFMA chain's).  The fp32 C was half of this kernel's matrix time.
-//
-// With SEG the kernel also forms the message sums of the aggregation (models.py:215-217) from
-// the a2m row tile: sums[v] = sum over v's incoming edges of a2m (raw, before the message
-// LayerNorm, whose statistics are known only after this launch; the consumer applies it:
-// sum LN(a2m) = g (sums - deg mean) / den + deg b).  The rows are dst-sorted and a block owns a
-// contiguous range, so a node's segment is cut only at block ends: segments ending inside the
-// range are summed row by row in edge order (a round's piece added to the previous round's
-// carry) and stored; a segment running across a block end leaves a head / tail partial for
-// pdg_segsum_fixup.  In inference a2m is then not stored at all.  The a2m tiles and the dst ids
-// are double-buffered (by round parity) so a round's sums are formed during the next round's W2
-// product, off the barrier-to-barrier critical path, and their stores are not waited for by the
-// next gathers; after the last round once more.  Config 5 (inference), per call: 551 us + 71 us
-// pdg_segment_sum become 565 + 29 us pdg_segsum_finish; of the 565, the sums walk costs ~20 us and
-// its stores ~28 us (the same with fp32 stores: not bandwidth), against 40 us saved on a2m.  In
-// training a2m is stored for the backward anyway and the fused sums do not pay (engine: off).
 constexpr int EFC_TILE = X6_ROWS * OT_STRIDE;   // floats per fp32 row tile
 constexpr int EFC_ES = L + 8;                    // e tile row stride: the C operand reads are conflict free
-// segment sums (LDS, after the tiles): two a2m tiles, two rounds' dst ids, two fp64 carry rows
-constexpr int EFC_SEG_BYTES = 2 * EFC_TILE * 4 + 2 * X6_ROWS * 4 + 2 * L * 8;
-typedef double d64x4 __attribute__((ext_vector_type(4)));
-typedef double d64x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 
-// D (deferred a2 stores, training and plain inference; not with SEG): a2 goes into two tiles of its own
+// D (deferred a2 stores): a2 goes into two tiles of its own
 // and its rows are stored after the NEXT round's first barrier, behind that round's gathers and row
 // loads, so a round has two barriers instead of four (the barrier that freed the a1 tiles for a2 and
 // the one that completed the a2 tiles go: the loop-top barrier completes both the e tile and the
 // previous round's a2 tiles), and the C product's wait for its gathers no longer covers the previous
 // round's a2 stores.  Bitwise the same outputs; 32 KB more LDS (131 KB).
 //
-// X (XCD-interleaved rounds, not with SEG): the blocks that share an XCD's L2 (b and b + 8; the grid
+// X (XCD-interleaved rounds): the blocks that share an XCD's L2 (b and b + 8; the grid
 // a multiple of 8) sweep one contiguous eighth of the rows together, taking its 32-row rounds
 // round-robin, instead of each block owning a contiguous range.  The P / Q rows an edge gathers are
 // reused by the edges of the mesh neighbours of its nodes, about +-13 rounds away in dst order: with
 // per-block ranges every block of an XCD keeps such a window live (32 x ~280 KB, over the 4 MiB L2, so
 // the reuse was served by the Infinity Cache), with interleaved rounds the XCD has one window.
-template <bool RES, bool EU, bool SEG, bool D = false, bool X = false>
+template <bool RES, bool EU, bool D = false, bool X = false>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
     const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ P,
     const float* __restrict__ Q, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ a1m, float* __restrict__ a2m,
-    float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m, double* __restrict__ part_e,
-    double* __restrict__ sums, double* __restrict__ seg_part, int* __restrict__ seg_info) {
+    float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m, double* __restrict__ part_e) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   unsigned char* img_m = sm;                                   // a1m
   unsigned char* img_x = sm + EBW_IMG;                         // a1e (EU)
@@ -1209,16 +1188,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   // PDG_EFWD_CX6: e as a bf16x6 image in the tile's place (24 instead of 17 KB)
   unsigned char* img_e = reinterpret_cast<unsigned char*>(t_e);
   constexpr int E_BYTES = PDG_EFWD_CX6 ? EBW_IMG : X6_ROWS * EFC_ES * 4;
-  float* t_s = reinterpret_cast<float*>(img_e + E_BYTES);      // SEG: a2m tiles (by round parity)
-  int* sdst0 = reinterpret_cast<int*>(t_s + 2 * EFC_TILE);     //      dst of the rounds' rows
-  double* carry = reinterpret_cast<double*>(sdst0 + 2 * X6_ROWS);   // open segment's sum, 2 rows
-  float* t_am = t_s;                                           // D: a2m / a2e tiles (in place of SEG's)
+  float* t_am = reinterpret_cast<float*>(img_e + E_BYTES);     // D: a2m / a2e tiles
   float* t_ae = t_am + EFC_TILE;
   // PDG_EFWD_CX6: the lo bf16 terms of Wc's K chunks 0 and 1 in LDS, after every region (with all 12 terms
   // in registers the main instantiation spilled 5 VGPRs and was no faster than fp32 MFMAs)
-  unsigned char* wlo = reinterpret_cast<unsigned char*>(t_s) + (SEG ? EFC_SEG_BYTES : 0) + (D ? 2 * EFC_TILE * 4 : 0);
-  static_assert(!(SEG && D), "deferred a2 stores and the segment sums use the same LDS");
-  static_assert(!(SEG && X), "the segment sums need contiguous block ranges");
+  unsigned char* wlo = reinterpret_cast<unsigned char*>(t_am) + (D ? 2 * EFC_TILE * 4 : 0);
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
@@ -1280,64 +1254,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
 #endif
     }
   };
-  // SEG: the node of the previous block's last edge (a segment of it here is a head partial),
-  // of the next block's first edge, and of the previous round's last row
-  int headnode = -1, after = -1, prev_last = -1;
-  if (SEG && r0 < r1) {
-    headnode = r0 > 0 ? dst[r0 - 1] : -1;
-    after = r1 < E ? dst[r1] : -1;
-  }
-  // the sums of round bk (parity pk, a2m tile ts): its segment pieces start at row 0 and wherever
-  // dst changes; wave w takes pieces w, w + 8, ... with lane l on features 2l, 2l + 1 (all the
-  // segment bookkeeping is wave-uniform: scalar instructions, no divergence)
-  auto walk = [&](int bk, int pk, int next_dst, bool more_k) {
-    const int nr = min(X6_ROWS, r1 - bk);
-    const int* sdst = sdst0 + pk * X6_ROWS;
-    const float* ts = t_s + pk * EFC_TILE;
-    const int rv = l < nr ? sdst[l] : -1;
-    const int pv = (l > 0 && l < nr) ? sdst[l - 1] : -1;
-    const unsigned mask = (unsigned)__ballot(l < nr && (l == 0 || rv != pv));
-    const int nseg = __popc(mask);
-    unsigned m = mask;
-    for (int i = 0; i < w; ++i) m &= m - 1;   // m's lowest set bit: piece w's first row
-    for (int s = w; s < nseg; s += EBW_WAVES) {
-      const int k0 = __builtin_ctz(m);
-      const unsigned m2 = m & (m - 1);
-      const int k1 = m2 ? __builtin_ctz(m2) : nr;
-      const int v = __builtin_amdgcn_readfirstlane(sdst[k0]);
-      double acc0 = 0., acc1 = 0.;
-      if (s == 0 && v == prev_last) {
-        const d64x2 cv = *reinterpret_cast<const d64x2*>(carry + (pk ^ 1) * L + 2 * l);
-        acc0 = cv[0];
-        acc1 = cv[1];
-      }
-      for (int k = k0; k < k1; k += 8) {   // 8 rows in flight, added in row order
-        f32x2 x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = *reinterpret_cast<const f32x2*>(ts + min(k + u, k1 - 1) * OT_STRIDE + 2 * l);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const bool in = k + u < k1;   // rows past the piece add exactly 0
-          acc0 += in ? (double)x[u][0] : 0.;
-          acc1 += in ? (double)x[u][1] : 0.;
-        }
-      }
-      const d64x2 acc = {acc0, acc1};
-      const bool open = s == nseg - 1 && v == next_dst;   // the segment goes on past this round
-      if (open && more_k) {   // through an LDS-typed pointer: merged with the global store below, the
-                              // compiler emitted one flat store
-        typedef __attribute__((address_space(3))) d64x2 lds_d64x2;
-        *(lds_d64x2*)(carry + pk * L + 2 * l) = acc;
-      } else {
-        double* dstp = v == headnode ? seg_part + (size_t)(2 * blockIdx.x) * L
-                       : open        ? seg_part + (size_t)(2 * blockIdx.x + 1) * L
-                                     : sums + (size_t)v * L;
-        __builtin_nontemporal_store(acc, reinterpret_cast<d64x2*>(dstp + 2 * l));
-      }
-      for (int i = 0; i < EBW_WAVES && m; ++i) m &= m - 1;
-    }
-    prev_last = sdst[nr - 1];
-  };
   issue(first);   // E > 0: an empty block (first = r1 = E) reads row E - 1
 #if PDG_EFWD_CX6
   load_wslice(wsc, W1 + 2 * L, w, 3 * L);
@@ -1382,8 +1298,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   for (int base = first; base < r1; base += stride) {
     __syncthreads();   // e tile complete
     int dc[2] = {dq[0], dq[1]}, sc[2] = {sq[0], sq[1]};
-    const int par = ((base - r0) / X6_ROWS) & 1;
-    if (SEG && w == 0 && l < X6_ROWS) sdst0[par * X6_ROWS + l] = dc[l >> 4];   // lane l: row l
     // ---- this round's P / Q rows first, then the next round's rows (pinned by sched_barrier): the
     // gathers are waited for in the C product below, and with the next round's HBM loads issued
     // ahead of them (vmcnt counts in issue order) every round waited for those too
@@ -1457,10 +1371,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       rows_store4_nt(rs_a1m, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_m + r * OT_STRIDE + 4 * cg));
       if (EU) rows_store4_nt(rs_a1e, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
     }
-    // the previous round's sums (the row after its last is this round's row 0)
-    if (SEG && base > r0) walk(base - X6_ROWS, par ^ 1, sdst0[par * X6_ROWS], true);
     // ---- a2 = relu(W2 a1 + b2) for both evaluations
-    float* t_a2 = SEG ? t_s + par * EFC_TILE : D ? t_am : t_m;
+    float* t_a2 = D ? t_am : t_m;
     float* t_a2e = D ? t_ae : t_x;
     constexpr int NI = EU ? 2 : 1;
     f32x4 d2[NI][2];
@@ -1514,21 +1426,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       rows_store4_nt(rs_a2m, last + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_am + r * OT_STRIDE + 4 * cg));
       if (EU) rows_store4_nt(rs_a2e, last + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_ae + r * OT_STRIDE + 4 * cg));
     }
-  }
-  if (SEG && r0 < r1) walk(r0 + (r1 - 1 - r0) / X6_ROWS * X6_ROWS, ((r1 - 1 - r0) / X6_ROWS) & 1, after, false);
-  if (SEG && threadIdx.x == 0) {   // the block's partials: head (+ whether it also runs past r1), tail
-    int hd = -1, hc = 0, td = -1;
-    if (r0 < r1) {
-      if (headnode >= 0 && dst[r0] == headnode) {
-        hd = headnode;
-        hc = dst[r1 - 1] == headnode && after == headnode;
-      }
-      if (after >= 0 && dst[r1 - 1] == after && !hc) td = after;
-    }
-    seg_info[4 * blockIdx.x] = hd;
-    seg_info[4 * blockIdx.x + 1] = hc;
-    seg_info[4 * blockIdx.x + 2] = td;
-    seg_info[4 * blockIdx.x + 3] = 0;
   }
   double* red = reinterpret_cast<double*>(sm);
   __syncthreads();
@@ -2426,12 +2323,6 @@ extern "C" int pdg_enc_narrow_reduce(const double* narrow_sums, int nslabs, floa
   return PDG_OK;
 }
 
-static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                                const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
-                                const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
-                                const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
-                                double* part_e, int with_edge_update, double* sums, double* seg_part, int* seg_info,
-                                int nblocks, void* stream);
 
 // deferred a2 stores in the cooperative edge forward (edge_fwd_coop_kernel's D)
 // (default: bitwise the same outputs; with X below 216 -> 210.5 us per config-2 call, the step -0.05 ms, in
@@ -2449,28 +2340,6 @@ extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln
                                  const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                                  const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                                  double* part_e, int with_edge_update, int nblocks, void* stream) {
-  return edge_fwd_coop_launch(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m,
-                              a2m, a1e, a2e, part_m, part_e, with_edge_update, nullptr, nullptr, nullptr, nblocks,
-                              stream);
-}
-
-extern "C" int pdg_edge_fwd_coop_seg(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                                     const float* ln_b, const float* e_res, float* e_out, const int* src,
-                                     const int* dst, const float* P, const float* Q, const float* W1, const float* b1,
-                                     const float* W2, const float* b2, float* a1m, float* a2m, float* a1e, float* a2e,
-                                     double* part_m, double* part_e, int with_edge_update, double* sums,
-                                     double* seg_part, int* seg_info, int nblocks, void* stream) {
-  return edge_fwd_coop_launch(n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m,
-                              a2m, a1e, a2e, part_m, part_e, with_edge_update, sums, seg_part, seg_info, nblocks,
-                              stream);
-}
-
-static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
-                                const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
-                                const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
-                                const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
-                                double* part_e, int with_edge_update, double* sums, double* seg_part, int* seg_info,
-                                int nblocks, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd_coop: n_edges must be > 0");
   PDG_CHECK_ARG(nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_fwd_coop: bad nblocks");
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
@@ -2480,119 +2349,37 @@ static int edge_fwd_coop_launch(int n_edges, const float* a2_prev, const pdg_ln_
                 "pdg_edge_fwd_coop: misaligned pointer");
   PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd_coop: edge-update outputs missing or misaligned");
-  const bool seg = sums != nullptr;
-  PDG_CHECK_ARG(seg || a2m, "pdg_edge_fwd_coop: a2m may be omitted only with the segment sums");
-  PDG_CHECK_ARG(!seg || (seg_part && seg_info && PDG_ALIGNED(sums) && PDG_ALIGNED(seg_part)),
-                "pdg_edge_fwd_coop_seg: sums / seg_part / seg_info missing or misaligned");
-  const bool defer = PDG_EFC_DEFER && !seg;
+  PDG_CHECK_ARG(a2m != nullptr, "pdg_edge_fwd_coop: a2m is required");
+  const bool defer = PDG_EFC_DEFER;
   // the XCD-interleaved rounds are compiled for the 256-block grid; any other grid (tests, other parts)
   // walks contiguous block ranges
-  const bool xcd = PDG_EFC_XCD && !seg && nblocks == XCD_GRID;
+  const bool xcd = PDG_EFC_XCD && nblocks == XCD_GRID;
   const size_t shm = 2 * EBW_IMG + 2 * EFC_TILE * sizeof(float) + (PDG_EFWD_CX6 ? EBW_IMG : X6_ROWS * EFC_ES * 4) +
-                     (seg ? EFC_SEG_BYTES : 0) + (defer ? 2 * EFC_TILE * sizeof(float) : 0) +
-                     (PDG_EFWD_CX6 ? 2 * EBW_WAVES * 64 * 16 : 0);
+                     (defer ? 2 * EFC_TILE * sizeof(float) : 0) + (PDG_EFWD_CX6 ? 2 * EBW_WAVES * 64 * 16 : 0);
   hipStream_t s = (hipStream_t)stream;
-#define PDG_EFC_X(R, U, S, X)                                                                                         \
-  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, S, S ? false : (bool)PDG_EFC_DEFER, X>), \
-                     dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, st, \
-                     ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e, a2e, part_m, part_e,  \
-                     sums, seg_part, seg_info)
-#define PDG_EFC(R, U, S)                           \
-  do {                                             \
-    if (!(S) && PDG_EFC_XCD && xcd) {              \
-      PDG_EFC_X(R, U, S, (!(S) && PDG_EFC_XCD));   \
-    } else {                                       \
-      PDG_EFC_X(R, U, S, false);                   \
-    }                                              \
+#define PDG_EFC_X(R, U, X)                                                                                            \
+  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, (bool)PDG_EFC_DEFER, X>), dim3(nblocks), dim3(EBW_THREADS), shm, s, \
+                     n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e,   \
+                     a2e, part_m, part_e)
+#define PDG_EFC(R, U)                         \
+  do {                                        \
+    if (PDG_EFC_XCD && xcd) {                 \
+      PDG_EFC_X(R, U, (bool)PDG_EFC_XCD);     \
+    } else {                                  \
+      PDG_EFC_X(R, U, false);                 \
+    }                                         \
   } while (0)
-#define PDG_EFC2(S)                                                \
-  if (e_res) {                                                     \
-    if (with_edge_update) PDG_EFC(true, true, S); else PDG_EFC(true, false, S);   \
-  } else {                                                         \
-    if (with_edge_update) PDG_EFC(false, true, S); else PDG_EFC(false, false, S); \
-  }
-  if (seg) {
-    PDG_EFC2(true)
+  if (e_res) {
+    if (with_edge_update) PDG_EFC(true, true); else PDG_EFC(true, false);
   } else {
-    PDG_EFC2(false)
+    if (with_edge_update) PDG_EFC(false, true); else PDG_EFC(false, false);
   }
-#undef PDG_EFC2
 #undef PDG_EFC
 #undef PDG_EFC_X
   PDG_CHECK_LAUNCH("pdg_edge_fwd_coop");
   return PDG_OK;
 }
 
-// Message sums of the nodes whose incoming edges run across a block end of
-// pdg_edge_fwd_coop_seg: the span's first block left a tail partial, the others head partials
-// (a block entirely inside the span: head with the continue flag); the block where the span
-// ends adds them in block order.  One block per edge-forward block, thread = feature.
-__global__ __launch_bounds__(L) void segsum_fixup_kernel(const double* __restrict__ seg_part,
-                                                         const int* __restrict__ seg_info, double* __restrict__ sums) {
-  const int b = blockIdx.x, c = threadIdx.x;
-  const int hd = seg_info[4 * b], hc = seg_info[4 * b + 1];
-  if (hd < 0 || hc) return;
-  int b0 = b - 1;
-  while (b0 >= 0 && seg_info[4 * b0] == hd && seg_info[4 * b0 + 1]) --b0;
-  if (b0 < 0 || seg_info[4 * b0 + 2] != hd) return;   // malformed partials (unreachable): the test sees it
-  double acc = seg_part[(size_t)(2 * b0 + 1) * L + c];
-  for (int k = b0 + 1; k <= b; ++k) acc += seg_part[(size_t)(2 * k) * L + c];
-  sums[(size_t)hd * L + c] = acc;
-}
-
-extern "C" int pdg_segsum_fixup(int nblocks, const double* seg_part, const int* seg_info, double* sums,
-                                void* stream) {
-  PDG_CHECK_ARG(nblocks > 0 && nblocks <= MAX_BLOCKS && seg_part && seg_info && sums, "pdg_segsum_fixup: bad arguments");
-  hipLaunchKernelGGL(segsum_fixup_kernel, dim3(nblocks), dim3(L), 0, (hipStream_t)stream, seg_part, seg_info, sums);
-  PDG_CHECK_LAUNCH("pdg_segsum_fixup");
-  return PDG_OK;
-}
-
-// aggr[v] = sum over v's deg edges of LN(a2m) = g (sums[v] - deg mean) / den + deg b and (xhat_sum
-// != NULL, training) xhat_sum[v] = (sums[v] - deg mean) / den, the backward's per-node sum of xhat
-// (pdg_segment_sum's outputs), evaluated in fp64 from the fp64 sums with the call's fp32 statistics
-// and rounded once; 0 for deg = 0 (those sums rows were never written).  Half-wave (32 lanes x 4
-// features) per node.
-__global__ __launch_bounds__(256) void segsum_finish_kernel(int N, const double* __restrict__ sums,
-                                                            const int* __restrict__ rowptr,
-                                                            const pdg_ln_stat* __restrict__ stp,
-                                                            const float* __restrict__ lg, const float* __restrict__ lb,
-                                                            float* __restrict__ aggr, float* __restrict__ xsum) {
-  const int hw = threadIdx.x >> 5, j = threadIdx.x & 31;
-  const int nhw = blockDim.x >> 5;
-  const double mean = stp->mean, rden = 1.0 / (double)stp->den;
-  const f32x4 g = reinterpret_cast<const f32x4*>(lg)[j], b = reinterpret_cast<const f32x4*>(lb)[j];
-  for (int v = blockIdx.x * nhw + hw; v < N; v += gridDim.x * nhw) {
-    const int deg = rowptr[v + 1] - rowptr[v];
-    f32x4 a = {0.f, 0.f, 0.f, 0.f}, xs = {0.f, 0.f, 0.f, 0.f};
-    if (deg > 0) {
-      const d64x4 sv = reinterpret_cast<const d64x4*>(sums + (size_t)v * L)[j];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const double h = (sv[c] - deg * mean) * rden;
-        a[c] = (float)(h * (double)g[c] + deg * (double)b[c]);
-        xs[c] = (float)h;
-      }
-    }
-    stg4(aggr + (size_t)v * L + 4 * j, a);
-    if (xsum) stg4(xsum + (size_t)v * L + 4 * j, xs);
-  }
-}
-
-extern "C" int pdg_segsum_finish(int n_nodes, const double* sums, const int* rowptr, const pdg_ln_stat* st,
-                                 const float* ln_g, const float* ln_b, float* aggr, float* xhat_sum, void* stream) {
-  PDG_CHECK_ARG(n_nodes > 0 && sums && rowptr && st && ln_g && ln_b && aggr, "pdg_segsum_finish: bad arguments");
-  PDG_CHECK_ARG(PDG_ALIGNED(sums) && PDG_ALIGNED(aggr) && PDG_ALIGNED(ln_g) && PDG_ALIGNED(ln_b) &&
-                    PDG_ALIGNED(xhat_sum),
-                "pdg_segsum_finish: misaligned pointer");
-  long want = (n_nodes + 7) / 8;
-  long cap = (long)device_cus() * 8;
-  const int grid = (int)(want < cap ? want : cap);
-  hipLaunchKernelGGL(segsum_finish_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, n_nodes, sums, rowptr, st,
-                     ln_g, ln_b, aggr, xhat_sum);
-  PDG_CHECK_LAUNCH("pdg_segsum_finish");
-  return PDG_OK;
-}
 
 extern "C" int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0, const float* b0, const float* W2,
                                 const float* b2, float* a2, double* partials, int nblocks, void* stream) {

@@ -13,8 +13,7 @@ Per message-passing step t (weights shared across steps, models.py:313-314):
   x_t = LN_n(a2n_{t-1}) + x_{t-1}           pdg_node_pq      (also P = Wa x_t, Q = Wb x_t)
   e_t = LN_e(a2e_{t-1}) + e_{t-1}           pdg_edge_fwd     (C = Wc e_t + b1, both edge_net
   a1m,a2m (message), a1e,a2e (edge upd.)                      evaluations, LN partials)
-  aggr = sum_dst LN_m(a2m)                  pdg_segment_sum (inference: sums formed in pdg_edge_fwd_coop_seg,
-                                            pdg_segsum_fixup + pdg_segsum_finish)
+  aggr = sum_dst LN_m(a2m)                  pdg_segment_sum
   a1n = relu(Wn1 [aggr, x_t] + bn1)         pdg_node_mlp1
   a2n = relu(Wn2 a1n + bn2)                 pdg_mlp2_fwd
 
@@ -81,17 +80,6 @@ VARIANTS = {
     # edge forward in the block-cooperative layout (pdg_edge_fwd_coop; 240 -> 230 us per call at config 2)
     # instead of pdg_edge_fwd
     "coop_fwd": ("PDG_EDGE_FWD_COOP", True),
-    # inference: the cooperative edge forward also forms the aggregation's message sums in fp64
-    # (pdg_edge_fwd_coop_seg + pdg_segsum_fixup; pdg_segsum_finish applies the message LayerNorm) instead of
-    # pdg_segment_sum re-reading a2m, and a2m is not stored (config 5: 11.8 -> 11.5 ms per step, same box).
-    # Training keeps pdg_segment_sum (seg_sums_train False): a2m is stored for the backward anyway and the
-    # in-kernel sums cost more than the re-read they save (9.91 vs 10.12 ms, config 2).  fp64, because fp32
-    # raw sums (sum a2m - deg mean cancels) flipped a relu mask bit against the fp64 reference.  Off since
-    # the end of round 4: the deferred + XCD-interleaved edge forward (not combinable with the sums) and
-    # pdg_segment_sum beat it in inference too (config 5: 10.41-10.46 vs 10.46-10.67 ms per step in three
-    # same-box pairs, tools/r04z4.sh); kept as the A/B alternative.
-    "seg_sums": ("PDG_SEG_SUMS", False),
-    "seg_sums_train": ("PDG_SEG_SUMS_TRAIN", False),
     # the backward's input gradient of x (gP, gQ -> gx) in bf16x6 (pdg_gemm_sum2_coop) instead of the fp32-MFMA
     # pdg_gemm_sum2_rw
     "gsum2_coop": ("PDG_GSUM2_COOP", True),
@@ -213,14 +201,10 @@ class EPDEngine:
         self.coop_fwd = var["coop_fwd"]
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
-        self.seg_sums = self.coop_fwd and var["seg_sums"]
-        self.seg_sums_train = self.coop_fwd and var["seg_sums_train"]
         self.gsum2_coop = var["gsum2_coop"]
         self.nbwd_coop = var["nbwd_coop"]
         self._enc_blocks = min(var["enc_blocks_per_cu"] *
                                torch.cuda.get_device_properties(self.device).multi_processor_count, lib.pdg_max_blocks())
-        self._seg_part = torch.empty(2 * self._nslabs_e * L, dtype=torch.float64, device=self.device)
-        self._seg_info = torch.empty(4 * self._nslabs_e, dtype=torch.int32, device=self.device)
         # optional live kernel timing: name -> list of (start, end) hiptimer.Event pairs
         self.timed: dict | None = None
         # optional backward probe (tools/grad_err_stages.py): step t -> copies of d loss / d x_t,
@@ -345,21 +329,11 @@ class EPDEngine:
             # the last step's edge update has no consumer (models.py:316 decodes nodes only)
             eu = t < steps - 1
             e_t = self._empty(E, L)
-            seg = bool(E) and (self.seg_sums_train if need_grad else self.seg_sums)
-            a2m = self._empty(E, L) if (need_grad or not seg) else None   # seg: a backward-only output
-            sums = torch.empty(N, L, dtype=torch.float64, device=self.device) if seg else None
+            a2m = self._empty(E, L)
             a1m = self._empty(E, L) if need_grad else None   # layer-1 outputs: backward only
             a2e = self._empty(E, L) if eu else None
             a1e = self._empty(E, L) if (eu and need_grad) else None
-            if seg:
-                self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop_seg, E, _p(a2e_prev),
-                        ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm),
-                        _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e),
-                        _p(self._part_a), _p(self._part_b), int(eu), _p(sums), _p(self._seg_part),
-                        _p(self._seg_info), self._nslabs_e, s)
-                self._nparts.value = self._nslabs_e
-                lib.pdg_segsum_fixup(self._nslabs_e, _p(self._seg_part), _p(self._seg_info), _p(sums), s)
-            elif E and self.coop_fwd:
+            if E and self.coop_fwd:
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop, E, _p(a2e_prev), ste_prev,
                         _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm),
                         _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a),
@@ -369,7 +343,7 @@ class EPDEngine:
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
                         _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
                         _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
-            fin_in_segsum = bool(E) and not seg and self.sync is None   # reduced inside pdg_segment_sum_fin
+            fin_in_segsum = bool(E) and self.sync is None   # reduced inside pdg_segment_sum_fin
             if E and not fin_in_segsum:
                 if eu and self.sync is None:    # both edge LayerNorms in one launch
                     lib.pdg_ln_finalize2(self._part_a.data_ptr(), self._part_b.data_ptr(), self._nparts.value,
@@ -381,12 +355,7 @@ class EPDEngine:
             # aggregation (models.py:215-217) and node_net (:240-243)
             a1n = self._empty(N, L) if need_grad else None
             a2n = self._empty(N, L)
-            if seg:
-                aggr = self._empty(N, L)
-                xs = self._empty(N, L) if need_grad else None
-                self._t("segment_sum", lib.pdg_segsum_finish, N, _p(sums), _p(plan.rowptr_dst), st[i_m], _p(ge),
-                        _p(be), _p(aggr), _p(xs), s)
-            elif E:
+            if E:
                 aggr = self._empty(N, L)
                 xs = self._empty(N, L) if need_grad else None
                 if fin_in_segsum:   # + both edge LayerNorms' statistics from the edge forward's partials

@@ -75,8 +75,6 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_reduce_batch": [I, P, P, P, P, P, P, P],
     "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
-    "pdg_edge_fwd_coop_seg": [I] + [P] * 20 + [I, P, P, P, I, P],
-    "pdg_segsum_fixup": [I, P, P, P, P],
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_node_bwd_coop": [I] + [P] * 14 + [I, I, P],
@@ -84,7 +82,6 @@ SIGNATURES: dict[str, list] = {
     "pdg_decoder_bwd_coop": [I] + [P] * 11 + [I, P, I, P],
     "pdg_wgrad_narrow_finalize": [P, I, I, I, P, P, P, P],
     "pdg_bwd_epilogue": [I, P, P, P, P, P, P, I, P, P, P, P, I, P, P, P, P, P, P, P, P, I, P, P, P],
-    "pdg_segsum_finish": [I, P, P, P, P, P, P, P, P],
     "pdg_wgrad_slabs_per_cu": [],
     "pdg_wgrad_pairs": [I, P, P, P, P, I, P, P, I, P],
     "pdg_edge_enc_bwd": [I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, I, P],

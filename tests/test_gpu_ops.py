@@ -790,100 +790,6 @@ def test_edge_fwd_coop_matches_edge_fwd(env, E, eu, res):
         assert rel(pe1, pe0) < 1e-6
 
 
-def _seg_graph(kind, g):
-    """dst-sorted edge lists that exercise the message-sum segmentation of pdg_edge_fwd_coop_seg."""
-    if kind == "random":      # ~13 edges per node, isolated nodes, segments across block ends
-        N, E = 300, 4099
-        dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values
-    elif kind == "star":      # one node with 3000 edges: spans several blocks (head + continue flags)
-        N = 200
-        dst = torch.sort(torch.cat([torch.full((3000,), 57), torch.randint(0, N, (500,), generator=g)])).values
-        E = dst.numel()
-    elif kind == "deg1":      # every edge its own node: 32 segments per round
-        N = E = 1000
-        dst = torch.arange(E)
-    else:                     # tiny: fewer rows than blocks (trailing blocks empty)
-        N, E = 20, 77
-        dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values
-    return N, E, dst.int()
-
-
-@pytest.mark.parametrize("kind,eu", [("random", 1), ("star", 0), ("deg1", 1), ("tiny", 0)])
-def test_edge_fwd_coop_seg_sums(env, kind, eu):
-    """pdg_edge_fwd_coop_seg + pdg_segsum_fixup: every output of pdg_edge_fwd_coop bitwise, and the
-    fp64 message sums (sum of a2m over each node's incoming edges) against an fp64 sum of the same
-    a2m rows; with a2m omitted (inference) the sums are bitwise the same.  Then pdg_segsum_finish
-    (aggr = sum LN(a2m) and the per-node sums of xhat) against fp64 restatements."""
-    lib, sh, _ = env
-    s = sh()
-    g = torch.Generator().manual_seed(5)
-    N, E, dst_c = _seg_graph(kind, g)
-    dst = dst_c.cuda()
-    src = torch.randint(0, N, (E,), generator=g).int().cuda()
-    a2p, eres = torch.relu(rnd(E, L)), rnd(E, L)
-    Pn, Qn = rnd(N, L), rnd(N, L)
-    W1, b1 = lin(L, 3 * L)
-    W2, b2 = lin(L, L)
-    lg, lbv = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
-    part = torch.empty(4096, dtype=torch.float64, device="cuda")
-    n = ctypes.c_int(0)
-    tmp = torch.empty(E, L, device="cuda")
-    lib.pdg_mlp2_fwd(E, a2p.data_ptr(), W2.data_ptr(), b2.data_ptr(), tmp.data_ptr(), part.data_ptr(),
-                     ctypes.byref(n), s)
-    st = finalize(lib, s, part, n.value, E * L)
-    nb = 37
-    seg_part = torch.empty(2 * nb * L, dtype=torch.float64, device="cuda")
-    seg_info = torch.empty(4 * nb, dtype=torch.int32, device="cuda")
-    runs = []
-    for mode in ("plain", "seg", "seg_noa2m"):
-        o = {k: torch.full((E, L), float("nan"), device="cuda") for k in ("e", "a1m", "a2m", "a1e", "a2e")}
-        pm = torch.zeros(4096, dtype=torch.float64, device="cuda")
-        pe = torch.zeros(4096, dtype=torch.float64, device="cuda")
-        sums = torch.full((N, L), float("nan"), dtype=torch.float64, device="cuda")
-        args = (E, a2p.data_ptr(), st.data_ptr(), lg.data_ptr(), lbv.data_ptr(), eres.data_ptr(),
-                o["e"].data_ptr(), src.data_ptr(), dst.data_ptr(), Pn.data_ptr(), Qn.data_ptr(), W1.data_ptr(),
-                b1.data_ptr(), W2.data_ptr(), b2.data_ptr(), o["a1m"].data_ptr(),
-                None if mode == "seg_noa2m" else o["a2m"].data_ptr(),
-                o["a1e"].data_ptr() if eu else None, o["a2e"].data_ptr() if eu else None,
-                pm.data_ptr(), pe.data_ptr() if eu else None, eu)
-        if mode == "plain":
-            lib.pdg_edge_fwd_coop(*args, nb, s)
-        else:
-            lib.pdg_edge_fwd_coop_seg(*args, sums.data_ptr(), seg_part.data_ptr(), seg_info.data_ptr(), nb, s)
-            lib.pdg_segsum_fixup(nb, seg_part.data_ptr(), seg_info.data_ptr(), sums.data_ptr(), s)
-        runs.append((o, pm[: 2 * nb].clone(), pe[: 2 * nb].clone(), sums))
-    (o0, pm0, pe0, _), (o1, pm1, pe1, s1), (o2, pm2, pe2, s2) = runs
-    for k in ("e", "a1m", "a2m") + (("a1e", "a2e") if eu else ()):
-        assert torch.equal(o0[k], o1[k]), k
-        if k != "a2m":
-            assert torch.equal(o0[k], o2[k]), k
-    assert torch.isnan(o2["a2m"]).all()          # not stored
-    assert torch.equal(pm0, pm1) and torch.equal(pm0, pm2) and torch.equal(pe0, pe1)
-    deg = torch.bincount(dst_c.long(), minlength=N)
-    has = deg > 0
-    ref = torch.zeros(N, L, dtype=torch.float64).index_add_(0, dst_c.long(), o0["a2m"].double().cpu())
-    assert torch.isnan(s1.cpu()[~has]).all()     # rows of nodes without edges are not written
-    torch.testing.assert_close(s1, s2, rtol=0, atol=0, equal_nan=True)   # bitwise, NaN rows included
-    assert rel(s1.cpu()[has], ref[has]) < 1e-13
-    # the message LayerNorm applied to the sums (pdg_segsum_finish) and its backward column sums
-    rowptr = torch.zeros(N + 1, dtype=torch.int32)
-    rowptr[1:] = torch.cumsum(deg, 0)
-    rowptr = rowptr.cuda()
-    sd = stat_from(st)
-    d64 = deg.double()[:, None]
-    xh = torch.where(d64 > 0, (ref - d64 * sd["mean"]) / sd["den"], torch.zeros_like(d64))
-    aggr_ref = torch.where(d64 > 0, xh * lg.double().cpu() + d64 * lbv.double().cpu(), torch.zeros_like(d64))
-    aggr = torch.full((N, L), float("nan"), device="cuda")
-    lib.pdg_segsum_finish(N, s1.data_ptr(), rowptr.data_ptr(), st.data_ptr(), lg.data_ptr(), lbv.data_ptr(),
-                          aggr.data_ptr(), None, s)
-    assert bool(torch.isfinite(aggr).all()) and bool((aggr.cpu()[~has] == 0).all())
-    assert rel(aggr, aggr_ref) < 1e-7
-    xs = torch.full((N, L), float("nan"), device="cuda")
-    lib.pdg_segsum_finish(N, s1.data_ptr(), rowptr.data_ptr(), st.data_ptr(), lg.data_ptr(), lbv.data_ptr(),
-                          aggr.data_ptr(), xs.data_ptr(), s)
-    assert bool((xs.cpu()[~has] == 0).all()) and rel(xs, xh) < 1e-7
-
-
 def test_wgrad_reduce_batch_matches_single(env):
     """pdg_wgrad_reduce_batch (every deferred slab reduction of a backward in one launch) against one
     pdg_wgrad_reduce per job and an fp64 sum: column offsets, accumulation into the existing gradient
