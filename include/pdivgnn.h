@@ -57,6 +57,10 @@ int pdg_version(void);
 const char* pdg_source_hash(void);
 /* Upper bound on the number of per-block partials any launcher writes. */
 int pdg_max_blocks(void);
+/* Layout of the node pre-pass outputs P, Q (pdg_node_pq_rw[_fin] writes it, pdg_edge_fwd_coop reads it):
+ * 0 = two N x 128 row-major arrays; 1 = one N x 256 array whose rows hold, per 16-feature block b,
+ * P[16b..16b+15] then Q[16b..16b+15], passed as P = base, Q = base + 16 floats. */
+int pdg_pq_layout(void);
 
 /* ---------------------------------------------------------------- forward */
 

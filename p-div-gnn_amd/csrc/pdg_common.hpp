@@ -135,6 +135,18 @@ __device__ __forceinline__ void pin_vgpr(const T& x) {
 // Buffer resource over rows [r0, r1) of a (rows, 128) fp32 array: stores past row r1 fall outside
 // num_records and are dropped by the hardware range check (no branch around them).  A null array
 // gets an empty range (every store dropped).
+// P / Q of the node pre-pass (node_pq -> edge forward gathers).  PDG_PQ_BLOCKED (default since round 5):
+// one N x 256 array whose row holds, per 16-feature block b, P[16b .. 16b + 15] then Q[16b .. 16b + 15]
+// (Q's pointer = P's + 16 floats), so the 64 B of P and of Q a wave of the cooperative edge forward gathers
+// for one node share one 128-B line: edge_fwd 191.9-196.7 -> 188.3-191.1 us per config-2 call, bitwise the
+// same outputs (two same-box pairs).  0: two N x 128 arrays (the layout pdg_edge_fwd reads).
+#ifndef PDG_PQ_BLOCKED
+#define PDG_PQ_BLOCKED 1
+#endif
+constexpr int PQ_LD = PDG_PQ_BLOCKED ? 2 * 128 : 128;   // row stride of P / Q (floats)
+// offset of feature c (a multiple of 4: one 16-byte chunk) in a P / Q row
+__device__ __forceinline__ int pq_col(int c) { return PDG_PQ_BLOCKED ? c + (c & ~15) : c; }
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int r0, int r1) {
   return __builtin_amdgcn_make_buffer_rsrc(base ? base + (size_t)r0 * L : nullptr, (short)0,
                                            base ? (r1 - r0) * L * 4 : 0, 0x00020000);

@@ -1304,11 +1304,11 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     f32x4 gpd[2], gqs[2], gps[2], gqd[2];
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
-      gpd[nb] = *reinterpret_cast<const f32x4*>(P + (size_t)dc[nb] * L + oc);
-      gqs[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)sc[nb] * L + oc);
+      gpd[nb] = *reinterpret_cast<const f32x4*>(P + (size_t)dc[nb] * PQ_LD + pq_col(oc));
+      gqs[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)sc[nb] * PQ_LD + pq_col(oc));
       if (EU) {
-        gps[nb] = *reinterpret_cast<const f32x4*>(P + (size_t)sc[nb] * L + oc);
-        gqd[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)dc[nb] * L + oc);
+        gps[nb] = *reinterpret_cast<const f32x4*>(P + (size_t)sc[nb] * PQ_LD + pq_col(oc));
+        gqd[nb] = *reinterpret_cast<const f32x4*>(Q + (size_t)dc[nb] * PQ_LD + pq_col(oc));
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -2334,6 +2334,10 @@ extern "C" int pdg_enc_narrow_reduce(const double* narrow_sums, int nslabs, floa
 #ifndef PDG_EFC_XCD
 #define PDG_EFC_XCD 1
 #endif
+
+// the P / Q layout this library was built for (pdg_common.hpp PDG_PQ_BLOCKED): 0 = two N x 128 arrays,
+// 1 = one N x 256 array of interleaved 16-feature blocks (Q = P + 16 floats)
+extern "C" int pdg_pq_layout(void) { return PDG_PQ_BLOCKED; }
 
 extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                                  const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,

@@ -798,8 +798,18 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_pq_x6_kernel(
     const unsigned char* im = xt + (i % 3) * PQ_IMG;
     gemm_x6f<1, PQ_T16>(dp, wa, im);
     gemm_x6f<1, PQ_T16>(dq, wb, im);
+#if PDG_PQ_BLOCKED
+    {   // rows of PQ_LD floats: a buffer range over the tile's rows of the blocked P / Q array
+      const int t0 = tile * TILE, nr = max(0, min(N, t0 + TILE) - t0);
+      const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(P + (size_t)t0 * PQ_LD, (short)0, nr * PQ_LD * 4, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(Q + (size_t)t0 * PQ_LD, (short)0, nr * PQ_LD * 4, 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dp[0]), rp, (r * PQ_LD + pq_col(oc)) * 4, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, dq[0]), rq, (r * PQ_LD + pq_col(oc)) * 4, 0, 0);
+    }
+#else
     rows_store4(tile_rsrc(P, tile, N), r, oc, dp[0]);
     rows_store4(tile_rsrc(Q, tile, N), r, oc, dq[0]);
+#endif
     __syncthreads();
     // buffer (i + 2) % 3 was last read in iteration i - 1
     store_xt1<RES>(xt + ((i + 2) % 3) * PQ_IMG, nu_tile(i + 2), N, av, rv, st, gg, bb, xout);
@@ -809,6 +819,7 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_pq_x6_kernel(
 #ifndef PDG_NODE_PQ_X6
 #define PDG_NODE_PQ_X6 1
 #endif
+static_assert(!PDG_PQ_BLOCKED || PDG_NODE_PQ_X6, "the blocked P / Q layout is written by node_pq_x6_kernel only");
 
 static int node_pq_rw_launch(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                              const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,

@@ -199,6 +199,8 @@ class EPDEngine:
         self.gz1e_from_gc = var["gz1e_from_gc"]
         self.fused_edge_bwd = var["fused_edge_bwd"]
         self.coop_fwd = var["coop_fwd"]
+        # the P / Q layout the library's node pre-pass writes and its cooperative edge forward reads
+        self.pq_blocked = bool(lib.pdg_pq_layout())
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
                              lib.pdg_max_blocks())
         self.gsum2_coop = var["gsum2_coop"]
@@ -313,7 +315,11 @@ class EPDEngine:
         a2n_prev, stn_prev, gn_prev, bn_prev = a2_ne, st[0], P["node_encoder.4.weight"], P["node_encoder.4.bias"]
         a2e_prev, ste_prev, ge_prev, be_prev = a2_ee, st[1], P["edge_encoder.4.weight"], P["edge_encoder.4.bias"]
         x_prev = e_prev = None
-        Pm, Qm = self._empty(N, L), self._empty(N, L)
+        if self.pq_blocked:   # one N x 256 array, Q's blocks 16 floats after P's (pdg_pq_layout)
+            PQm = self._empty(N, 2 * L)
+            Pm, Qm = PQm, PQm.view(-1)[16:]
+        else:
+            Pm, Qm = self._empty(N, L), self._empty(N, L)
         # pend_n: deferred node LayerNorm statistics (nparts of the partials in pend_buf)
         for t in range(steps):
             i_m, i_e, i_n = 2 + 3 * t, 3 + 3 * t, 4 + 3 * t
@@ -340,8 +346,12 @@ class EPDEngine:
                         _p(self._part_b), int(eu), self._nslabs_e, s)
                 self._nparts.value = self._nslabs_e
             elif E:
+                Pu, Qu = Pm, Qm
+                if self.pq_blocked:   # pdg_edge_fwd (the A/B / reference kernel) reads two N x 128 arrays
+                    v = PQm.view(N, 8, 2, 16)
+                    Pu, Qu = v[:, :, 0].reshape(N, L).contiguous(), v[:, :, 1].reshape(N, L).contiguous()
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd, E, _p(a2e_prev), ste_prev, _p(ge_prev), _p(be_prev), _p(e_prev),
-                        _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm), _p(W1), _p(b1), _p(W2), _p(b2),
+                        _p(e_t), _p(plan.src), _p(plan.dst), _p(Pu), _p(Qu), _p(W1), _p(b1), _p(W2), _p(b2),
                         _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu), np_, s)
             fin_in_segsum = bool(E) and self.sync is None   # reduced inside pdg_segment_sum_fin
             if E and not fin_in_segsum:

@@ -40,6 +40,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_version": [],
     "pdg_source_hash": [],
     "pdg_max_blocks": [],
+    "pdg_pq_layout": [],
     "pdg_format_inputs": [I, I, P, P, P, P, P, P, I, P, P, P],
     "pdg_encoder_fwd": [I, I, P, P, P, P, P, P, P, P, P, P],
     "pdg_ln_finalize": [P, I, c_double, P, P],
@@ -144,7 +145,7 @@ class _Lib:
         if not name.startswith("pdg_"):
             raise AttributeError(name)
         fn = getattr(self.load(), name)
-        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks", "pdg_wgrad_slabs_per_cu"):
+        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks", "pdg_wgrad_slabs_per_cu", "pdg_pq_layout"):
             return fn
 
         def call(*args):

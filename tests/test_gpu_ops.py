@@ -51,6 +51,39 @@ def finalize(lib, s, part, nparts, count):
     return st
 
 
+class PQ:
+    """P / Q of the node pre-pass in the library's layout (pdg_pq_layout: two N x 128 arrays, or one
+    N x 256 array of interleaved 16-feature blocks with Q 16 floats after P): `p`, `q` are the pointers
+    the kernels take, `unpack()` returns (P, Q) as N x 128 tensors; `PQ.of(lib, P, Q)` packs inputs."""
+
+    def __init__(self, lib, N):
+        self.N, self.blocked = N, bool(lib.pdg_pq_layout())
+        if self.blocked:
+            self.buf = torch.empty(N, 2 * L, device="cuda")
+            self.p, self.q = self.buf.data_ptr(), self.buf.data_ptr() + 16 * 4
+        else:
+            self.P, self.Q = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
+            self.p, self.q = self.P.data_ptr(), self.Q.data_ptr()
+
+    def unpack(self):
+        if not self.blocked:
+            return self.P, self.Q
+        v = self.buf.view(self.N, 8, 2, 16)
+        return v[:, :, 0].reshape(self.N, L).contiguous(), v[:, :, 1].reshape(self.N, L).contiguous()
+
+    @classmethod
+    def of(cls, lib, P, Q):
+        pq = cls(lib, P.shape[0])
+        if pq.blocked:
+            v = pq.buf.view(pq.N, 8, 2, 16)
+            v[:, :, 0] = P.view(pq.N, 8, 16)
+            v[:, :, 1] = Q.view(pq.N, 8, 16)
+        else:
+            pq.P.copy_(P)
+            pq.Q.copy_(Q)
+        return pq
+
+
 def ln_ref(a, g, b, eps=1e-5):
     a = a.double()
     x = a - a.mean()
@@ -476,11 +509,16 @@ def test_register_weight_kernels_match_lds_kernels(env, N, res):
     st = torch.frombuffer(bytearray(struct.pack("ffffddd", mean, den, 1.0 / den, sd, mean, sd, N * L)),
                           dtype=torch.uint8).cuda()
     outs = []
-    for fn in (lib.pdg_node_pq, lib.pdg_node_pq_rw):
-        x, P, Q = (torch.empty(N, L, device="cuda") for _ in range(3))
-        assert fn(N, a2.data_ptr(), st.data_ptr(), g.data_ptr(), b.data_ptr(), xr.data_ptr() if res else None,
-                  x.data_ptr(), W1.data_ptr(), P.data_ptr(), Q.data_ptr(), s) == 0
-        outs.append((x, P, Q))
+    # pdg_node_pq (LDS weights) writes two N x 128 arrays; pdg_node_pq_rw the library's P / Q layout
+    x, P, Q = (torch.empty(N, L, device="cuda") for _ in range(3))
+    assert lib.pdg_node_pq(N, a2.data_ptr(), st.data_ptr(), g.data_ptr(), b.data_ptr(),
+                           xr.data_ptr() if res else None, x.data_ptr(), W1.data_ptr(), P.data_ptr(), Q.data_ptr(),
+                           s) == 0
+    outs.append((x, P, Q))
+    x, pq = torch.empty(N, L, device="cuda"), PQ(lib, N)
+    assert lib.pdg_node_pq_rw(N, a2.data_ptr(), st.data_ptr(), g.data_ptr(), b.data_ptr(),
+                              xr.data_ptr() if res else None, x.data_ptr(), W1.data_ptr(), pq.p, pq.q, s) == 0
+    outs.append((x, *pq.unpack()))
     assert torch.equal(outs[0][0], outs[1][0])
     x64 = outs[1][0].double()
     for k, Wk in ((1, W1[:, :L]), (2, W1[:, L:2 * L])):
@@ -584,17 +622,16 @@ def test_node_pq_rw_fin_equals_finalize_then_pq_rw(env, N, nparts, res):
                         for i, j in zip(edges[:-1], edges[1:])]).reshape(-1).cuda()
     st_ref = finalize(lib, s, part, nparts, N * L)
     outs = []
-    x, P, Q = (torch.empty(N, L, device="cuda") for _ in range(3))
+    x, pq = torch.empty(N, L, device="cuda"), PQ(lib, N)
     assert lib.pdg_node_pq_rw(N, a2.data_ptr(), st_ref.data_ptr(), g.data_ptr(), b.data_ptr(),
-                              xr.data_ptr() if res else None, x.data_ptr(), W1.data_ptr(), P.data_ptr(),
-                              Q.data_ptr(), s) == 0
-    outs.append((x, P, Q))
+                              xr.data_ptr() if res else None, x.data_ptr(), W1.data_ptr(), pq.p, pq.q, s) == 0
+    outs.append((x, *pq.unpack()))
     st_fin = torch.full((40,), 0xAB, dtype=torch.uint8, device="cuda")
-    x, P, Q = (torch.empty(N, L, device="cuda") for _ in range(3))
+    x, pq = torch.empty(N, L, device="cuda"), PQ(lib, N)
     assert lib.pdg_node_pq_rw_fin(N, a2.data_ptr(), part.data_ptr(), nparts, float(N * L), st_fin.data_ptr(),
                                   g.data_ptr(), b.data_ptr(), xr.data_ptr() if res else None, x.data_ptr(),
-                                  W1.data_ptr(), P.data_ptr(), Q.data_ptr(), s) == 0
-    outs.append((x, P, Q))
+                                  W1.data_ptr(), pq.p, pq.q, s) == 0
+    outs.append((x, *pq.unpack()))
     torch.cuda.synchronize()
     assert torch.equal(st_ref, st_fin)
     for u, v in zip(*outs):
@@ -763,8 +800,10 @@ def test_edge_fwd_coop_matches_edge_fwd(env, E, eu, res):
         if name == "ref":
             lib.pdg_edge_fwd(*args, pm.data_ptr(), pe.data_ptr() if eu else None, eu, ctypes.byref(n), s)
             np_ = n.value
-        else:
+        else:   # P / Q in the layout the library's node pre-pass writes (pdg_pq_layout)
             np_ = 37
+            pq = PQ.of(lib, Pn, Qn)
+            args = args[:9] + (pq.p, pq.q) + args[11:]
             lib.pdg_edge_fwd_coop(*args, pm.data_ptr(), pe.data_ptr() if eu else None, eu, np_, s)
         outs[name] = (o, pm[: 2 * np_].view(np_, 2).sum(0), pe[: 2 * np_].view(np_, 2).sum(0))
     (o0, pm0, pe0), (o1, pm1, pe1) = outs["ref"], outs["coop"]
