@@ -294,7 +294,8 @@ int pdg_node_bwd_coop(int n_nodes, const float* gy, const float* a2n, const floa
 /* pdg_edge_fwd in the block-cooperative layout (pdg_ebw.hip): nblocks blocks of 512 threads, one
  * contiguous row range each, Wc and W2 stationary in registers as bf16 terms, whole-row HBM access.
  * Same outputs to fp32 rounding (e_t bitwise; C = Wc e and the W2 products as unbiased bf16x6
- * products); part_m / part_e get nblocks partials. */
+ * products); part_m / part_e get nblocks partials.  P and Q in the pdg_pq_layout() layout (what
+ * pdg_node_pq_rw[_fin] writes; pdg_edge_fwd takes two N x 128 arrays). */
 int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                       const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
                       const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
