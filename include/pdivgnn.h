@@ -72,6 +72,11 @@ int pdg_format_inputs(int n_nodes, int n_edges, const float* pos, const float* m
                       const int64_t* node_types, const float* edge_attr, const int* perm,
                       const float* stats8, int scale_input, float* x_in, float* e_in, void* stream);
 
+/* The node encoder (models.py:260-274, 6 inputs) in the cooperative layout: a1 = relu(W0 x + b0) bitwise
+ * pdg_encoder_fwd's (stored when a1 != NULL), a2 = relu(W2 a1 + b2) as an unbiased bf16x6 product from
+ * registers, nblocks blocks of 512 threads (partials: nblocks (sum, sumsq) pairs).  x_in 8-byte aligned. */
+int pdg_node_enc_fwd(int n_nodes, const float* x_in, const float* w0, const float* b0, const float* W2,
+                     const float* b2, float* a1, float* a2, double* partials, int nblocks, void* stream);
 /* Encoder MLP (models.py:260-274): a1 = relu(W0 x + b0) (K = in_features in {1..8}),
  * a2 = relu(W2 a1 + b2); writes a1, a2 and per-block LayerNorm partials (sum, sumsq). */
 int pdg_encoder_fwd(int rows, int in_features, const float* x_in, const float* W0, const float* b0,

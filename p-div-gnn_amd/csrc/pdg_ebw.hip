@@ -1531,6 +1531,109 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_fwd_kernel(
   }
 }
 
+// ============================================================================ node encoder forward
+// The node encoder (models.py:260-274, 6 inputs -> 128 -> 128 + the LayerNorm partials of the output) in
+// the layout of edge_enc_fwd_kernel: a1 = relu(W0 x + b0) per element in encoder_kernel's order (bitwise
+// its a1, stored for the backward), W2 a1 as an UNBIASED bf16x6 product (gemm_x6f; the fp32-MFMA
+// encoder_kernel<6> was bound by its matrix time and its LDS weight copy), a2 rows stored whole.
+__global__ __launch_bounds__(EBW_THREADS, 1) void node_enc_fwd_kernel(
+    int N, const float* __restrict__ x_in, const float* __restrict__ w0, const float* __restrict__ b0,
+    const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ a1, float* __restrict__ a2,
+    double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img = sm;                                     // a1 (bf16x6)
+  float* t_a = reinterpret_cast<float*>(sm + EBW_IMG);         // a2 row tile
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(N, r0, r1);
+  WSlice ws2;
+  load_wslice(ws2, W2, w);
+  f32x4 w0v[6];   // rows 4 cg .. 4 cg + 3 of W0 (128 x 6, row-major): 24 consecutive floats
+#pragma unroll
+  for (int k = 0; k < 6; ++k) w0v[k] = *reinterpret_cast<const f32x4*>(w0 + 24 * cg + 4 * k);
+  const f32x4 b04 = *reinterpret_cast<const f32x4*>(b0 + 4 * cg);
+  const f32x4 b2o = *reinterpret_cast<const f32x4*>(b2 + oc);
+  double s1 = 0, s2 = 0;
+  float px[2][6];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const float* xr = x_in + (size_t)clamp_row(base + rg + 16 * u, r1) * 6;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const f32x2 v = *reinterpret_cast<const f32x2*>(xr + 2 * k);
+        px[u][2 * k] = v[0];
+        px[u][2 * k + 1] = v[1];
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t rs_a1 = rows_rsrc(a1, r0, r1);
+  const __amdgpu_buffer_rsrc_t rs_a2 = rows_rsrc(a2, r0, r1);
+  issue(r0);   // N > 0: an empty block (r0 = r1 = N) reads row N - 1
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) pin_vgpr(px[u][k]);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pin_vgpr(ws2.a[ks][q]);
+  pin_vgpr(b2o);
+  auto round = [&](const int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      f32x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {   // encoder_kernel's a1: fma over the 6 inputs in order, then + b0
+        float d = 0.f;   // W0 row 4 cg + j: the thread's floats 6 j .. 6 j + 5
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const int f = 6 * j + i;   // float index within the thread's 24
+          d = fmaf(w0v[f >> 2][f & 3], px[u][i], d);
+        }
+        a[j] = fmaxf(d + b04[j], 0.f);
+      }
+      const bool ok = base + r < r1;
+      rows_store4_nt(rs_a1, base + r - r0, 4 * cg, a);
+      img_store4(img, r, cg, ok ? a : f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+    issue(base + X6_ROWS);
+    __syncthreads();   // the a1 image is complete
+    f32x4 d[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    gemm_x6f<2, X6_TERM, true>(d, ws2, img);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = 16 * nb + (l & 15);
+      f32x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = fmaxf(d[nb][j] + b2o[j], 0.f);
+      *reinterpret_cast<f32x4*>(t_a + r * OT_STRIDE + oc) = a;
+      if (base + r < r1) {
+        s1 += (double)((a[0] + a[1]) + (a[2] + a[3]));
+        s2 += (double)((a[0] * a[0] + a[1] * a[1]) + (a[2] * a[2] + a[3] * a[3]));
+      }
+    }
+    __syncthreads();   // the a2 tile is complete; the image is free
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      rows_store4_nt(rs_a2, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_a + r * OT_STRIDE + 4 * cg));
+    }
+  };
+  round(r0);
+  for (int base = r0 + X6_ROWS; base < r1; base += X6_ROWS) round(base);
+  double* red = reinterpret_cast<double*>(sm);
+  __syncthreads();
+  block_sum2(s1, s2, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s1;
+    part[2 * blockIdx.x + 1] = s2;
+  }
+}
+
 // ============================================================================ node input gradient
 // pdg_gemm_sum2_rw in the cooperative layout: out = W0T in0 + W1T in1 + res (the input gradient of
 // x_t through P = Wa x, Q = Wb x plus the node_net path: in0 = gP, in1 = gQ, W0T = Wa^T, W1T = Wb^T)
@@ -2384,6 +2487,20 @@ extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln
   return PDG_OK;
 }
 
+
+extern "C" int pdg_node_enc_fwd(int n_nodes, const float* x_in, const float* w0, const float* b0, const float* W2,
+                                const float* b2, float* a1, float* a2, double* partials, int nblocks, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_node_enc_fwd: bad sizes");
+  PDG_CHECK_ARG(x_in && w0 && b0 && W2 && b2 && a2 && partials, "pdg_node_enc_fwd: null argument");
+  PDG_CHECK_ARG(((uintptr_t)x_in & 7) == 0 && PDG_ALIGNED(w0) && PDG_ALIGNED(b0) && PDG_ALIGNED(W2) &&
+                    PDG_ALIGNED(b2) && PDG_ALIGNED(a2) && (!a1 || PDG_ALIGNED(a1)),
+                "pdg_node_enc_fwd: misaligned pointer");
+  const size_t shm = EBW_IMG + (size_t)EFC_TILE * sizeof(float);
+  hipLaunchKernelGGL(node_enc_fwd_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, n_nodes, x_in,
+                     w0, b0, W2, b2, a1, a2, partials);
+  PDG_CHECK_LAUNCH("pdg_node_enc_fwd");
+  return PDG_OK;
+}
 
 extern "C" int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0, const float* b0, const float* W2,
                                 const float* b2, float* a2, double* partials, int nblocks, void* stream) {

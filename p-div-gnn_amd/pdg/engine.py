@@ -89,6 +89,9 @@ VARIANTS = {
     # pdg_wgrad_pairs blocks per CU (2 per CU ran as two sequential block waves at 166 VGPRs: 9.07-9.12 vs
     # 9.14-9.23 ms per config-2 step, same box)
     "pair_blocks_per_cu": ("PDG_PAIR_BLOCKS_PER_CU", 1),
+    # the node encoder in the cooperative layout with an unbiased bf16x6 W2 product (pdg_node_enc_fwd) instead of
+    # the LDS-weight fp32-MFMA pdg_encoder_fwd
+    "node_enc_coop": ("PDG_NODE_ENC_COOP", True),
     # pdg_edge_enc_fwd blocks per CU (104 VGPRs, 41 KB LDS per 8-wave block)
     "enc_blocks_per_cu": ("PDG_ENC_BLOCKS_PER_CU", 2),
 }
@@ -199,6 +202,7 @@ class EPDEngine:
         self.gz1e_from_gc = var["gz1e_from_gc"]
         self.fused_edge_bwd = var["fused_edge_bwd"]
         self.coop_fwd = var["coop_fwd"]
+        self.node_enc_coop = var["node_enc_coop"]
         # the P / Q layout the library's node pre-pass writes and its cooperative edge forward reads
         self.pq_blocked = bool(lib.pdg_pq_layout())
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
@@ -275,9 +279,16 @@ class EPDEngine:
                               _p(stats8), int(scale_input), _p(x_in), _p(e_in), s)
         # encoders (models.py:308-309)
         a1_ne, a2_ne = self._empty(N, L), self._empty(N, L)
-        lib.pdg_encoder_fwd(N, 6, _p(x_in), _p(P["node_encoder.0.weight"]), _p(P["node_encoder.0.bias"]),
-                            _p(P["node_encoder.2.weight"]), _p(P["node_encoder.2.bias"]), _p(a1_ne), _p(a2_ne),
-                            _p(self._part_b), np_, s)
+        if self.node_enc_coop:
+            nb = self._nslabs_e   # one 8-wave block per CU (168 VGPRs)
+            self._t("node_enc_fwd", lib.pdg_node_enc_fwd, N, _p(x_in), _p(P["node_encoder.0.weight"]),
+                    _p(P["node_encoder.0.bias"]), _p(P["node_encoder.2.weight"]), _p(P["node_encoder.2.bias"]),
+                    _p(a1_ne), _p(a2_ne), _p(self._part_b), nb, s)
+            self._nparts.value = nb
+        else:
+            lib.pdg_encoder_fwd(N, 6, _p(x_in), _p(P["node_encoder.0.weight"]), _p(P["node_encoder.0.bias"]),
+                                _p(P["node_encoder.2.weight"]), _p(P["node_encoder.2.bias"]), _p(a1_ne), _p(a2_ne),
+                                _p(self._part_b), np_, s)
         # the node encoder's LayerNorm statistics are reduced inside step 0's node_pq (pdg_node_pq_rw_fin, as
         # every later step's; one launch fewer), its partials in _part_b until then (the edge encoder and the
         # first edge forward write _part_a / _part_b only after that node_pq)

@@ -77,6 +77,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
+    "pdg_node_enc_fwd": [I, P, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_node_bwd_coop": [I] + [P] * 14 + [I, I, P],
     "pdg_mlp2_bwd_coop": [I] + [P] * 10 + [I, P, P, I, P],

@@ -258,7 +258,12 @@ def test_isolated_node_and_ragged_batch():
 def test_fused_edge_weight_gradients_match_separate_passes(nmesh, ngraph, steps):
     """pdg_edge_bwd_w2 + pdg_edge_gout_wc (weight gradients fused into the edge backward,
     slabs accumulated over the steps) against pdg_edge_bwd + pdg_wgrad_segments: every
-    parameter gradient and the input-gradient chain agree to fp32 summation-order noise.
+    parameter gradient and the input-gradient chain agree to VARIANT_TOL.  The two variants also
+    run different edge-encoder forwards (pdg_edge_enc_fwd's bf16x6 W2 product vs pdg_encoder_fwd's
+    fp32 MFMAs, since the unfused backward needs the stored layer-1 output), so they are two fp32
+    evaluations that may differ in a relu bit within rounding of zero: with the bf16x6 node encoder
+    (round 5) one such bit moves node_encoder.0.weight's gradient by 1.8e-5 at (41, 3) (the golden and
+    oracle gates against fp64 are unchanged).
     (41, 3): ~15k edges, several 32-row rounds per block and a ragged last round;
     (9, 1): fewer edges than blocks x 32 (empty blocks)."""
     from gnn_local_stress import losses
@@ -276,7 +281,7 @@ def test_fused_edge_weight_gradients_match_separate_passes(nmesh, ngraph, steps)
         total.backward()
         grads[fused] = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
     for name, g in grads[True].items():
-        assert rel(g, grads[False][name]) < 1e-5, (name, rel(g, grads[False][name]))
+        assert rel(g, grads[False][name]) < VARIANT_TOL, (name, rel(g, grads[False][name]))
 
 
 @pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])

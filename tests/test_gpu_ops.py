@@ -886,6 +886,42 @@ def test_edge_enc_fwd_vs_fp64(env, E, nb):
     assert abs(float(p[1]) - float((ref * ref).sum())) <= 1e-6 * float((ref * ref).sum())
 
 
+@pytest.mark.parametrize("N,nb", [(7, 37), (1031, 37), (40328, 256), (100489, 256)])
+def test_node_enc_fwd_vs_encoder_fwd(env, N, nb):
+    """pdg_node_enc_fwd (node encoder, cooperative layout, unbiased bf16x6 W2 product) against pdg_encoder_fwd
+    (LDS weights, fp32 MFMAs) and fp64: a1 bitwise (the same fma order), a2 within 1e-6 of fp64, no less
+    accurate than the fp32 kernel, no mean bias beyond 3e-10 of the product scale; the LayerNorm partials'
+    totals to 1e-7.  Rows past a block's range (empty blocks when nb exceeds the 32-row rounds) write nothing."""
+    lib, sh, _ = env
+    s = sh()
+    x = rnd(N, 6)
+    w0, b0 = lin(L, 6)
+    W2, b2 = lin(L, L)
+    a1r, a2r = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda")
+    pr = torch.zeros(lib.pdg_max_blocks() * 2, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    assert lib.pdg_encoder_fwd(N, 6, x.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                               a1r.data_ptr(), a2r.data_ptr(), pr.data_ptr(), ctypes.byref(n), s) == 0
+    a1, a2 = (torch.full((N + 64, L), float("nan"), device="cuda") for _ in range(2))
+    part = torch.zeros(2 * nb, dtype=torch.float64, device="cuda")
+    assert lib.pdg_node_enc_fwd(N, x.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                                a1.data_ptr(), a2.data_ptr(), part.data_ptr(), nb, s) == 0
+    assert torch.isnan(a1[N:]).all() and torch.isnan(a2[N:]).all()
+    a1, a2 = a1[:N], a2[:N]
+    assert torch.equal(a1, a1r)
+    z = a1.double() @ W2.double().T + b2.double()
+    ref = torch.relu(z)
+    assert rel(a2, ref) < 1e-6 and rel(a2, ref) <= 1.05 * rel(a2r, ref) + 1e-9, (rel(a2, ref), rel(a2r, ref))
+    if N >= 1000:
+        scale = a1.double().abs() @ W2.double().abs().T + b2.double().abs()
+        pos = (a2 > 0) & (z > 0)
+        bias = float(((a2.double() - z) / scale.clamp_min(1e-30))[pos].mean())
+        assert abs(bias) < 3e-10, bias
+    p = part.view(nb, 2).sum(0).cpu()
+    a2d = a2.double().cpu()
+    assert rel(p, torch.stack([a2d.sum(), a2d.square().sum()])) < 1e-7
+
+
 @pytest.mark.parametrize("N,nb,res", [(7, 37, True), (1031, 37, False), (40328, 256, True)])
 def test_gemm_sum2_coop_vs_fp64(env, N, nb, res):
     """pdg_gemm_sum2_coop (bf16x6, register-stationary, cooperative layout) against an fp64
