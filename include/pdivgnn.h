@@ -172,6 +172,14 @@ int pdg_decoder_fwd_fin(int n_nodes, const float* a2_prev, const double* partial
                         pdg_ln_stat* st_out, const float* ln_g, const float* ln_b, const float* x_res,
                         float* x_out, const float* Wd1, const float* bd1, float* a1d, const float* Wd2,
                         const float* bd2, const float* stats8, int scale_output, float* y, void* stream);
+/* The decoder in the cooperative layout (pdg_ebw.hip): x_out bitwise pdg_decoder_fwd's, Wd1 x_S as an
+ * unbiased bf16x6 product from registers, a1d and y to fp32 rounding; partials != NULL: the statistics
+ * reduced in-kernel as pdg_decoder_fwd_fin does (st unused), else st.  nblocks blocks of 512 threads. */
+int pdg_decoder_fwd_coop(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const double* partials,
+                         int nparts, double count, pdg_ln_stat* st_out, const float* ln_g, const float* ln_b,
+                         const float* x_res, float* x_out, const float* Wd1, const float* bd1, float* a1d,
+                         const float* Wd2, const float* bd2, const float* stats8, int scale_output, float* y,
+                         int nblocks, void* stream);
 
 /* torch.any(x != 0) into *flag (int, device). models.py:294 */
 int pdg_any_nonzero(const float* x, int64_t n, int* flag, void* stream);

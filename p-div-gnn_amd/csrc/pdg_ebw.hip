@@ -1634,6 +1634,144 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void node_enc_fwd_kernel(
   }
 }
 
+// ============================================================================ decoder forward
+// The node decoder (models.py:316-321: x_S = LN(a2_prev) + x_prev, a1d = relu(Wd1 x_S + bd1),
+// y = Wd2 a1d + bd2, unscaled when asked) in the layout of node_enc_fwd_kernel: x_S element by element as
+// ln_res_frag forms it (bitwise), Wd1 x_S as an unbiased bf16x6 product from registers (decoder_kernel: fp32
+// MFMAs from an LDS weight copy), a1d rows through an fp32 tile, the 3 outputs of a row as fp32 dot products
+// over the tile (96 threads, features in order).  part != NULL: the last node LayerNorm's statistics reduced
+// in every block from the partials (pdg_ln_finalize's order), block 0 stores them to st_out.
+__global__ __launch_bounds__(EBW_THREADS, 1) void decoder_coop_kernel(
+    int N, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
+    const float* __restrict__ lb, const float* __restrict__ xres, float* __restrict__ xout,
+    const float* __restrict__ Wd1, const float* __restrict__ bd1, float* __restrict__ a1d,
+    const float* __restrict__ Wd2, const float* __restrict__ bd2, const float* __restrict__ st8, int scale,
+    float* __restrict__ y, const double* __restrict__ part, int nparts, double count, pdg_ln_stat* __restrict__ st_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img = sm;                                     // x_S (bf16x6)
+  float* t_a = reinterpret_cast<float*>(sm + EBW_IMG);         // a1d row tile
+  float* w2l = t_a + EFC_TILE;                                 // Wd2 (3 x 128)
+  __shared__ LNStat st_sh;
+  __shared__ double red_fin[2 * EBW_WAVES];
+  if (part) {
+    ln_stat_from_partials(part, nparts, count, &st_sh, red_fin);
+    __syncthreads();
+    if (blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_sh;
+  }
+  const LNStat st = part ? st_sh : *reinterpret_cast<const LNStat*>(stp);
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int oc = 16 * w + 4 * (l >> 4);
+  int r0, r1;
+  block_rows(N, r0, r1);
+  for (int i = threadIdx.x; i < 3 * L; i += blockDim.x) w2l[i] = Wd2[i];
+  const f32x4 gg = *reinterpret_cast<const f32x4*>(lg + 4 * cg), bb = *reinterpret_cast<const f32x4*>(lb + 4 * cg);
+  const f32x4 b1o = *reinterpret_cast<const f32x4*>(bd1 + oc);
+  f32x4 xa[2], xr[2];
+  auto issue = [&](int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
+      xa[u] = *reinterpret_cast<const f32x4*>(a2p + rc);
+      xr[u] = *reinterpret_cast<const f32x4*>(xres + rc);
+    }
+  };
+  const __amdgpu_buffer_rsrc_t rs_x = rows_rsrc(xout, r0, r1);
+  const __amdgpu_buffer_rsrc_t rs_a = rows_rsrc(a1d, r0, r1);
+  issue(r0);   // N > 0: an empty block reads row N - 1
+  WSlice ws;   // after the first rows' loads: the round trips overlap
+  load_wslice(ws, Wd1, w);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    pin_vgpr(xa[u]);
+    pin_vgpr(xr[u]);
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) pin_vgpr(ws.a[ks][q]);
+  pin_vgpr(b1o);
+  const int yo = threadIdx.x % 3, yr = threadIdx.x / 3;   // threads 0 .. 95: output yo of tile row yr
+  const float yb = bd2[yo];
+  const float ys = scale ? st8[5] : 1.f, yt = scale ? st8[4] : 0.f;
+  const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(y + (size_t)r0 * 3, (short)0, (r1 - r0) * 3 * 4,
+                                                                        0x00020000);
+  auto round = [&](const int base) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      f32x4 x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {   // ln_res_frag, element by element
+        float v = div_den(xa[u][j] - st.mean, st.den, st.rstd) * gg[j] + bb[j];
+        v += xr[u][j];
+        x[j] = v;
+      }
+      const bool ok = base + r < r1;
+      rows_store4_nt(rs_x, base + r - r0, 4 * cg, x);
+      img_store4(img, r, cg, ok ? x : f32x4{0.f, 0.f, 0.f, 0.f});
+    }
+    issue(base + X6_ROWS);
+    __syncthreads();   // the x_S image is complete
+    f32x4 d[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    gemm_x6f<2, X6_TERM, true>(d, ws, img);
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int r = 16 * nb + (l & 15);
+      f32x4 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = fmaxf(d[nb][j] + b1o[j], 0.f);
+      *reinterpret_cast<f32x4*>(t_a + r * OT_STRIDE + oc) = a;
+    }
+    __syncthreads();   // the a1d tile is complete; the image is free
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = rg + 16 * u;
+      rows_store4_nt(rs_a, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_a + r * OT_STRIDE + 4 * cg));
+    }
+    {   // y = Wd2 a1d + bd2 (features in order): threads 0 .. 95; the others compute a clamped row and their
+        // store falls outside the buffer range (every thread stores: no memory operation is conditional)
+      const float* ar = t_a + min(yr, X6_ROWS - 1) * OT_STRIDE;
+      const float* wr = w2l + yo * L;
+      float acc = 0.f;
+#pragma unroll 2
+      for (int k = 0; k < L; k += 4) {
+        const f32x4 av = *reinterpret_cast<const f32x4*>(ar + k), wv = *reinterpret_cast<const f32x4*>(wr + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = fmaf(wv[j], av[j], acc);
+      }
+      float out = acc + yb;
+      if (scale) out = out * ys + yt;
+      const int off = threadIdx.x < 3 * X6_ROWS ? ((base + yr - r0) * 3 + yo) * 4 : 0x7ffffff0;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, out), rs_y, off, 0, 0);
+    }
+    // (the next round writes the tile after its first barrier, which every thread reaches after these reads)
+  };
+  for (int base = r0; base < r1; base += X6_ROWS) round(base);
+}
+
+extern "C" int pdg_decoder_fwd_coop(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const double* partials,
+                                    int nparts, double count, pdg_ln_stat* st_out, const float* ln_g,
+                                    const float* ln_b, const float* x_res, float* x_out, const float* Wd1,
+                                    const float* bd1, float* a1d, const float* Wd2, const float* bd2,
+                                    const float* stats8, int scale_output, float* y, int nblocks, void* stream) {
+  PDG_CHECK_ARG(n_nodes > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_decoder_fwd_coop: bad sizes");
+  PDG_CHECK_ARG(a2_prev && x_res && x_out && a1d && Wd1 && bd1 && Wd2 && bd2 && y && ln_g && ln_b,
+                "pdg_decoder_fwd_coop: null argument");
+  PDG_CHECK_ARG(!scale_output || stats8 != nullptr, "pdg_decoder_fwd_coop: stats8 is NULL");
+  PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(x_res) && PDG_ALIGNED(x_out) && PDG_ALIGNED(a1d) &&
+                    PDG_ALIGNED(Wd1) && PDG_ALIGNED(bd1) && PDG_ALIGNED(ln_g) && PDG_ALIGNED(ln_b),
+                "pdg_decoder_fwd_coop: misaligned pointer");
+  PDG_CHECK_ARG(partials ? (nparts > 0 && count > 0 && st_out != nullptr) : st != nullptr,
+                "pdg_decoder_fwd_coop: statistics arguments");
+  const size_t shm = EBW_IMG + (size_t)(EFC_TILE + 3 * L) * sizeof(float);
+  hipLaunchKernelGGL(decoder_coop_kernel, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, n_nodes,
+                     a2_prev, st, ln_g, ln_b, x_res, x_out, Wd1, bd1, a1d, Wd2, bd2, stats8, scale_output, y,
+                     partials, nparts, count, st_out);
+  PDG_CHECK_LAUNCH("pdg_decoder_fwd_coop");
+  return PDG_OK;
+}
+
 // ============================================================================ node input gradient
 // pdg_gemm_sum2_rw in the cooperative layout: out = W0T in0 + W1T in1 + res (the input gradient of
 // x_t through P = Wa x, Q = Wb x plus the node_net path: in0 = gP, in1 = gQ, W0T = Wa^T, W1T = Wb^T)

@@ -92,6 +92,8 @@ VARIANTS = {
     # the node encoder in the cooperative layout with an unbiased bf16x6 W2 product (pdg_node_enc_fwd) instead of
     # the LDS-weight fp32-MFMA pdg_encoder_fwd
     "node_enc_coop": ("PDG_NODE_ENC_COOP", True),
+    # the decoder likewise (pdg_decoder_fwd_coop) instead of the LDS-weight pdg_decoder_fwd[_fin]
+    "decoder_coop": ("PDG_DECODER_COOP", True),
     # pdg_edge_enc_fwd blocks per CU (104 VGPRs, 41 KB LDS per 8-wave block)
     "enc_blocks_per_cu": ("PDG_ENC_BLOCKS_PER_CU", 2),
 }
@@ -203,6 +205,7 @@ class EPDEngine:
         self.fused_edge_bwd = var["fused_edge_bwd"]
         self.coop_fwd = var["coop_fwd"]
         self.node_enc_coop = var["node_enc_coop"]
+        self.decoder_coop = var["decoder_coop"]
         # the P / Q layout the library's node pre-pass writes and its cooperative edge forward reads
         self.pq_blocked = bool(lib.pdg_pq_layout())
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
@@ -406,7 +409,14 @@ class EPDEngine:
         x_S, a1d, y = self._empty(N, L), self._empty(N, L), self._empty(N, 3)
         if x_prev is None:
             raise ValueError("message_passing_steps must be >= 1")
-        if pend_n is not None:   # the last node LayerNorm's statistics reduced inside the decoder
+        if self.decoder_coop:   # (pend_n: the last node LayerNorm's statistics reduced inside the decoder)
+            self._t("decoder_fwd", lib.pdg_decoder_fwd_coop, N, _p(a2n_prev), None if pend_n is not None else stn_prev,
+                    pend_buf.data_ptr() if pend_n is not None else None, pend_n or 0, float(N * L),
+                    stn_prev if pend_n is not None else None, _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_S),
+                    _p(P["node_decoder.0.weight"]), _p(P["node_decoder.0.bias"]), _p(a1d),
+                    _p(P["node_decoder.2.weight"]), _p(P["node_decoder.2.bias"]), _p(stats8), int(scale_output),
+                    _p(y), self._nslabs_e, s)
+        elif pend_n is not None:   # the last node LayerNorm's statistics reduced inside the decoder
             lib.pdg_decoder_fwd_fin(N, _p(a2n_prev), pend_buf.data_ptr(), pend_n, float(N * L), stn_prev,
                                     _p(gn_prev), _p(bn_prev), _p(x_prev), _p(x_S), _p(P["node_decoder.0.weight"]),
                                     _p(P["node_decoder.0.bias"]), _p(a1d), _p(P["node_decoder.2.weight"]),

@@ -57,6 +57,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_node_net": [I, P, P, P, P, P, P, P, P, P, P, P],
     "pdg_decoder_fwd": [I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P],
     "pdg_decoder_fwd_fin": [I, P, P, I, c_double, P] + [P] * 10 + [I, P, P],
+    "pdg_decoder_fwd_coop": [I, P, P, P, I, c_double, P] + [P] * 10 + [I, P, I, P],
     "pdg_any_nonzero": [P, c_int64, P, P],
     "pdg_decoder_bwd": [I, P, P, P, P, P, P, P],
     "pdg_ln_colsum": [I, P, P, P, P, P, P, P, P, I, P],

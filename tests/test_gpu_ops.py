@@ -674,6 +674,60 @@ def test_decoder_fwd_fin_equals_finalize_then_decoder(env, N, nparts, scale):
         assert torch.equal(u, v)
 
 
+@pytest.mark.parametrize("N,nparts,scale,nb", [(7, 1, 1, 37), (1031, 37, 0, 37), (40328, 256, 1, 256),
+                                                (5000, 700, 0, 256)])
+def test_decoder_fwd_coop_vs_decoder_fwd(env, N, nparts, scale, nb):
+    """pdg_decoder_fwd_coop against pdg_decoder_fwd_fin on the same inputs: x_S and the stored statistics
+    bitwise (with the statistics reduced in-kernel, and given as st); a1d within 1e-6 of fp64 on x_S, no less
+    accurate than the fp32-MFMA kernel, no mean bias beyond 3e-10 of the product scale; y within 1e-6 of the
+    fp64 decoder on the kernel's own a1d and of the fp32 kernel's y; rows past N untouched."""
+    lib, sh, _ = env
+    s = sh()
+    a2 = torch.relu(rnd(N, L))
+    xr = rnd(N, L)
+    g, b = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
+    Wd1, bd1 = lin(L, L)
+    Wd2, bd2 = lin(3, L)
+    st8 = torch.tensor([0.1, 1.2, -0.3, 2.0, 0.25, 3.5, 0.05, 0.7], device="cuda")
+    edges = torch.linspace(0, N, nparts + 1).round().long().tolist()
+    a64 = a2.double()
+    part = torch.stack([torch.stack([a64[i:j].sum(), a64[i:j].square().sum()])
+                        for i, j in zip(edges[:-1], edges[1:])]).reshape(-1).cuda()
+    st_ref = torch.full((40,), 0xAB, dtype=torch.uint8, device="cuda")
+    xs0, a10, y0 = torch.empty(N, L, device="cuda"), torch.empty(N, L, device="cuda"), torch.empty(N, 3, device="cuda")
+    assert lib.pdg_decoder_fwd_fin(N, a2.data_ptr(), part.data_ptr(), nparts, float(N * L), st_ref.data_ptr(),
+                                   g.data_ptr(), b.data_ptr(), xr.data_ptr(), xs0.data_ptr(), Wd1.data_ptr(),
+                                   bd1.data_ptr(), a10.data_ptr(), Wd2.data_ptr(), bd2.data_ptr(), st8.data_ptr(),
+                                   scale, y0.data_ptr(), s) == 0
+    for fin in (True, False):
+        st_c = torch.full((40,), 0xCD, dtype=torch.uint8, device="cuda")
+        xs, a1, y = (torch.full((N + 40, c), float("nan"), device="cuda") for c in (L, L, 3))
+        assert lib.pdg_decoder_fwd_coop(N, a2.data_ptr(), None if fin else st_ref.data_ptr(),
+                                        part.data_ptr() if fin else None, nparts if fin else 0, float(N * L),
+                                        st_c.data_ptr() if fin else None, g.data_ptr(), b.data_ptr(), xr.data_ptr(),
+                                        xs.data_ptr(), Wd1.data_ptr(), bd1.data_ptr(), a1.data_ptr(), Wd2.data_ptr(),
+                                        bd2.data_ptr(), st8.data_ptr(), scale, y.data_ptr(), nb, s) == 0
+        torch.cuda.synchronize()
+        for t in (xs, a1, y):
+            assert torch.isnan(t[N:]).all()
+        xs, a1, y = xs[:N], a1[:N], y[:N]
+        if fin:
+            assert torch.equal(st_c, st_ref)
+        assert torch.equal(xs, xs0)
+        z = xs.double() @ Wd1.double().T + bd1.double()
+        h = torch.relu(z)
+        assert rel(a1, h) < 1e-6 and rel(a1, h) <= 1.05 * rel(a10, h) + 1e-9, (rel(a1, h), rel(a10, h))
+        if N >= 1000:
+            scale_ = xs.double().abs() @ Wd1.double().abs().T + bd1.double().abs()
+            pos = (a1 > 0) & (z > 0)
+            bias = float(((a1.double() - z) / scale_.clamp_min(1e-30))[pos].mean())
+            assert abs(bias) < 3e-10, bias
+        yr = a1.double() @ Wd2.double().T + bd2.double()
+        if scale:
+            yr = yr * float(st8[5]) + float(st8[4])
+        assert rel(y, yr) < 1e-6 and rel(y, y0) < 1e-5, (rel(y, yr), rel(y, y0))
+
+
 @pytest.mark.parametrize("slab_init", [0, 1])
 @pytest.mark.parametrize("E", [77, 5000])
 def test_edge_enc_bwd_vs_autograd(env, E, slab_init):
