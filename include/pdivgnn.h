@@ -349,7 +349,9 @@ int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, const float
  * before, pdg_wgrad_reduce layout) += gz2^T a1 and the b2 sums, gz1 = (W2T gz2) [a1 > 0], and per
  * block narrow_sums[b] = (sum gz1 e_in, sum gz1) as 2 x 128 doubles; a1 = relu(w0 e_in + b0) is
  * recomputed (pdg_encoder_fwd may skip storing it).  Replaces pdg_mlp2_bwd + the edge encoder's
- * pdg_wgrad_segments and pdg_wgrad_narrow passes.  lb / lb_pairs as pdg_mlp2_bwd. */
+ * pdg_wgrad_segments and pdg_wgrad_narrow passes.  lb / lb_pairs as pdg_mlp2_bwd.  Computed (default)
+ * as M = (gz2 e)^T mask and N = gz2^T mask with mask = [a1 > 0]: slab += w0 M + b0 N,
+ * narrow_sums = (sum_j W2[j][k] M[j][k], sum_j W2[j][k] N[j][k]) -- the same sums regrouped. */
 int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, const float* e_in, const float* w0,
                      const float* b0, const pdg_ln_stat* st, const pdg_ln_bwd* lb, const double* lb_pairs,
                      int lb_npairs, const float* ln_g, const float* W2T, float* slabs, double* narrow_sums,

@@ -2536,6 +2536,164 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
   return PDG_OK;
 }
 
+// Edge encoder backward without the W2^T product (PDG_EEB_MASK): the layer-1 input is one scalar e per edge,
+// so a1 = mask . (w0 e + b0) with mask = [a1 > 0], and every gradient of the encoder's first two layers is a
+// linear function of two products over the rows with the BINARY mask as operand:
+//   M = (gz2 . e)^T mask,  N = gz2^T mask       (128 x 128 each, per block, K = rows)
+//   dW2[j][k] = w0[k] M[j][k] + b0[k] N[j][k],  dw0[k] = sum_j W2[j][k] M[j][k],  db0[k] = sum_j W2[j][k] N[j][k]
+// (the same sums regrouped; a1 enters exactly instead of rounded to fp32).  The mask is exact in ONE bf16 term,
+// so each product costs 3 MFMAs per K step instead of bf16x6's 6, and the per-row W2^T product of the
+// two-deep kernel (another 6 per step, with its weight slice in registers) is gone: half the matrix time.
+// Structure, staging and the db2 / slab bookkeeping as edge_enc_bwd2_kernel; the block's slab gets its dW2
+// and its narrow-sum row its dw0 / db0 partials, so pdg_bwd_epilogue reduces them unchanged.
+// (round 5, A/B on one box: 89.5 / 88.9 -> 75.1 / 76.0 us per config-2 call, gradients within 7e-8 of the
+// two-deep kernel's; PDG_EEB_MASK=0 builds edge_enc_bwd2_kernel)
+#ifndef PDG_EEB_MASK
+#define PDG_EEB_MASK 1
+#endif
+constexpr int EEB3_BUF = 2 * IMG16 + T16;   // one round's gz2 and gz2.e images and the mask image
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd3_kernel(
+    const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ e_in,
+    const float* __restrict__ w0, const float* __restrict__ b0, const pdg_ln_stat* __restrict__ st_p,
+    const pdg_ln_bwd* __restrict__ lb_p, const double* __restrict__ pairs, int npairs,
+    const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ slabs,
+    double* __restrict__ nsums, int E, int slab_init) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const int l = lane_id(), w = wave_id(), h = l >> 5, c = l & 31;
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;    // the thread's staged row: rg (0..15)
+  const int ob = 32 * (w & 3), ib = 64 * (w >> 2);
+  const int lrow = 8 * h + ((l & 15) >> 2);
+  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
+  int r0, r1;
+  block_rows(E, r0, r1);
+  f32x16 accM[2], accN[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accM[b][r] = accN[b][r] = 0.f;
+  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 pg[2], pa2[2];
+  float pe[2];
+  auto issue = [&](const int s, int base) {   // clamped: E > 0 (an empty block reads row E - 1)
+    const int rc = clamp_row(base + rg, r1);
+    pg[s] = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + 4 * cg);
+    pa2[s] = *reinterpret_cast<const f32x4*>(a2 + (size_t)rc * L + 4 * cg);
+    pe[s] = e_in[rc];
+  };
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
+  const f32x4 w04 = *reinterpret_cast<const f32x4*>(w0 + 4 * cg);
+  const f32x4 b04 = *reinterpret_cast<const f32x4*>(b0 + 4 * cg);
+  const LNStat st = *reinterpret_cast<const LNStat*>(st_p);
+  issue(0, r0);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(1, r0 + R16);
+  __builtin_amdgcn_sched_barrier(0);
+  const pdg_ln_bwd lb = lnb_resolve(lb_p, pairs, npairs, st_p);
+  pin_vgpr(g4);
+  pin_vgpr(w04);
+  pin_vgpr(b04);
+  auto stage = [&](const int s, const int base) {
+    unsigned char* img_g = sm + s * EEB3_BUF;                  // gz2
+    unsigned char* img_e = img_g + IMG16;                      // gz2 . e
+    unsigned char* img_m = img_g + 2 * IMG16;                  // [a1 > 0] as bf16 0 / 1 (one term)
+    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool ok = base + rg < r1;
+    const f32x4 zr = ln_relu_bwd4(pg[s], pa2[s], st, lb, g4);
+    f32x4 zg, ze;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      zg[j] = ok ? zr[j] : 0.f;
+      ze[j] = zg[j] * pe[s];
+    }
+    bsum += zg;
+    img_store4<T16>(img_g, rg, cg, zg);
+    img_store4<T16>(img_e, rg, cg, ze);
+    unsigned mb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // encoder_kernel's a1 sign: fma(w0, e, 0) + b0 > 0
+      const float a = fmaf(w04[j], pe[s], 0.f) + b04[j];
+      mb[j] = (ok && a > 0.f) ? 0x3F80u : 0u;
+    }
+    *reinterpret_cast<u32x2*>(img_m + x6_addr(rg, 8 * cg)) = u32x2{mb[0] | (mb[1] << 16), mb[2] | (mb[3] << 16)};
+    issue(s, base + 2 * R16);   // the set is free: the round after next
+  };
+  auto compute = [&](const int s) {
+    const unsigned char* img_g = sm + s * EEB3_BUF;
+    const unsigned char* img_e = img_g + IMG16;
+    const unsigned char* img_m = img_g + 2 * IMG16;
+    bf16x8 Ag[3], Ae[3], Bm[2];
+    const int g0 = x6_addr(lrow, lcolb + 2 * ob), g1 = x6_addr(lrow + 4, lcolb + 2 * ob);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      Ag[p] = x6_operand(img_g + p * T16, g0, g1);
+      Ae[p] = x6_operand(img_e + p * T16, g0, g1);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int x0 = x6_addr(lrow, lcolb + 2 * (ib + 32 * b)), x1 = x6_addr(lrow + 4, lcolb + 2 * (ib + 32 * b));
+      Bm[b] = x6_operand(img_m, x0, x1);
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {   // the small terms first, as wgrad_round chains them
+      f32x16 t = accM[b];
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ae[2], Bm[b], t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ae[1], Bm[b], t, 0, 0, 0);
+      accM[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ae[0], Bm[b], t, 0, 0, 0);
+      f32x16 u = accN[b];
+      u = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ag[2], Bm[b], u, 0, 0, 0);
+      u = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ag[1], Bm[b], u, 0, 0, 0);
+      accN[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Ag[0], Bm[b], u, 0, 0, 0);
+    }
+  };
+  stage(0, r0);
+  __syncthreads();
+  for (int base = r0; base < r1; base += 2 * R16) {
+    compute(0);
+    stage(1, base + R16);
+    __syncthreads();
+    compute(1);
+    stage(0, base + 2 * R16);   // past r1 on the last step: zero rows nobody reads
+    __syncthreads();
+  }
+  __syncthreads();   // the last rounds' image reads precede the LDS reuse below
+  // dW2 into the block's slab; dw0 / db0 partials: per thread over its 16 rows o of each column i, then the
+  // two lane halves (h), then the four waves sharing ib, in order through LDS
+  f32x16 accD[2];
+  double dm[2], dn[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int i = ib + 32 * b + c;
+    const float wi = w0[i], bi = b0[i];
+    dm[b] = dn[b] = 0.;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h;
+      accD[b][r] = wi * accM[b][r] + bi * accN[b][r];
+      const double wt = (double)W2T[(size_t)i * L + o];
+      dm[b] += wt * (double)accM[b][r];
+      dn[b] += wt * (double)accN[b][r];
+    }
+    dm[b] += __shfl_xor(dm[b], 32);
+    dn[b] += __shfl_xor(dn[b], 32);
+  }
+  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, accD, bsum, reinterpret_cast<float*>(sm), slab_init);
+  double* red = reinterpret_cast<double*>(sm + 16 * L * 4);   // after slab_accumulate's 8 KB
+  if (h == 0) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int i = ib + 32 * b + c;
+      red[(w & 3) * 2 * L + i] = dm[b];
+      red[(w & 3) * 2 * L + L + i] = dn[b];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * L) {
+    const int e = threadIdx.x;
+    const double v = ((red[e] + red[2 * L + e]) + red[4 * L + e]) + red[6 * L + e];
+    nsums[(size_t)blockIdx.x * 2 * L + e] = v;
+  }
+}
+
 extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, const float* e_in, const float* w0,
                                 const float* b0, const pdg_ln_stat* st, const pdg_ln_bwd* lb, const double* lb_pairs,
                                 int lb_npairs, const float* ln_g, const float* W2T, float* slabs, double* narrow_sums,
@@ -2547,6 +2705,13 @@ extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, c
   PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2) && PDG_ALIGNED(w0) && PDG_ALIGNED(b0) && PDG_ALIGNED(ln_g) &&
                     PDG_ALIGNED(W2T) && PDG_ALIGNED(slabs),
                 "pdg_edge_enc_bwd: misaligned pointer");
+  if (PDG_EEB_MASK) {
+    const size_t shm3 = 2 * EEB3_BUF > 16 * L * 4 + 8 * L * 8 ? 2 * EEB3_BUF : 16 * L * 4 + 8 * L * 8;
+    hipLaunchKernelGGL(edge_enc_bwd3_kernel, dim3(nslabs), dim3(EBW_THREADS), shm3, (hipStream_t)stream, gy, a2, e_in,
+                       w0, b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs, narrow_sums, n_edges, slab_init);
+    PDG_CHECK_LAUNCH("pdg_edge_enc_bwd");
+    return PDG_OK;
+  }
   const size_t shm = PDG_EEB_2DEEP ? 2 * EEB2_BUF : 2 * EBW_IMG + EBW_MASK + X6_ROWS * sizeof(float);
   hipLaunchKernelGGL(PDG_EEB_2DEEP ? edge_enc_bwd2_kernel : edge_enc_bwd_kernel, dim3(nslabs), dim3(EBW_THREADS), shm,
                      (hipStream_t)stream, gy, a2, e_in, w0, b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs,
