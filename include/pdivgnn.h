@@ -290,6 +290,17 @@ int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* 
  * LayerNorm partials of a2 (nblocks pairs).  a1 is not stored (pdg_edge_enc_bwd recomputes it). */
 int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0, const float* b0, const float* W2,
                      const float* b2, float* a2, double* partials, int nblocks, void* stream);
+/* The same outputs from the piecewise-linear form of the encoder (engine A/B variant): with one scalar
+ * input, a1 = relu(w0 e + b0) has a kink at each knot -b0[k] / w0[k], and between consecutive knots
+ * a2 = relu(e U_i + V_i) with U_i = W2 (w0 . m_i), V_i = b2 + W2 (b0 . m_i) for the interval's fixed relu
+ * mask m_i.  One launch forms the 129 (U_i, V_i) rows in fp64 into `table` (pdg_edge_enc_knots_floats()
+ * floats, 16-byte aligned, device scratch), a second streams a2 (one knot search and one fma per output)
+ * and the LayerNorm partials (nblocks pairs; one block per CU: the table and a chunk of rows occupy
+ * 148.6 KB of LDS). */
+int pdg_edge_enc_fwd_knots(int n_edges, const float* e_in, const float* w0, const float* b0,
+                           const float* W2, const float* b2, float* table, float* a2, double* partials,
+                           int nblocks, void* stream);
+int pdg_edge_enc_knots_floats(void);
 /* pdg_gemm_sum2_rw in the block-cooperative layout (nblocks blocks of 512 threads, contiguous row
  * ranges): out = W0T in0 + W1T in1 [+ res], both products in bf16x6 with the weights stationary in
  * registers; partials != NULL: the LayerNorm column partials and pairs as pdg_gemm_sum2_rw (nblocks

@@ -1531,6 +1531,183 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_fwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------- edge encoder forward by knots
+// The first layer has ONE scalar input, so a1 = relu(w0 e + b0) is piecewise linear in e with a kink at each
+// knot t_k = -b0[k] / w0[k]: between two consecutive knots the set of active features A is fixed and
+//   a2 = relu(W2 a1 + b2) = relu(e U_i + V_i),  U_i = sum_{k in A_i} W2[:, k] w0[k],  V_i = b2 + sum_{k in A_i} W2[:, k] b0[k]
+// (w0[k] = 0: feature k is active on every interval iff b0[k] > 0, contributing to V only).  The 129 interval
+// rows (U_i, V_i) are formed once per forward in fp64 and rounded once (edge_knots_kernel), so the per-edge
+// work is a binary search over the 128 sorted knots and one fma per output: no matrix product is left and the
+// kernel only streams a2 out.  An edge within an ulp of a knot may take the neighbouring interval; feature k
+// is then ~0 either way (|w0 e + b0| at the ulp level), so the output moves by that much only.
+// Table layout (EK_TAB floats): the sorted knots [128], then interval i's U [128] and V [128] at 128 + 256 i.
+constexpr int EK_KNOTS = 128;
+constexpr int EK_TAB = EK_KNOTS + (EK_KNOTS + 1) * 2 * L;   // 33,152 floats (132.6 KB)
+__global__ __launch_bounds__(EBW_THREADS) void edge_knots_kernel(const float* __restrict__ w0,
+                                                                  const float* __restrict__ b0,
+                                                                  const float* __restrict__ W2,
+                                                                  const float* __restrict__ b2,
+                                                                  float* __restrict__ tab) {
+  __shared__ float sw[L * (L + 1)];   // W2, row stride L + 1 (thread j reads row j: no bank conflicts)
+  __shared__ float tau[L], sw0[L], sb0[L];
+  __shared__ int rank[L];
+  __shared__ double red[4][2][L];
+  const int t = threadIdx.x, i = blockIdx.x;
+  {   // W2 into LDS: every load issued before the first store (one round trip)
+    f32x4 v[L * L / 4 / EBW_THREADS];
+#pragma unroll
+    for (int q = 0; q < L * L / 4 / EBW_THREADS; ++q)
+      v[q] = *reinterpret_cast<const f32x4*>(W2 + 4 * (t + q * EBW_THREADS));
+#pragma unroll
+    for (int q = 0; q < L * L / 4 / EBW_THREADS; ++q) {
+      const int x = 4 * (t + q * EBW_THREADS), row = x / L, col = x % L;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) sw[row * (L + 1) + col + c] = v[q][c];
+    }
+  }
+  float tk = 0.f;
+  if (t < L) {
+    const float wk = w0[t], bk = b0[t];
+    tk = wk != 0.f ? -bk / wk : __FLT_MAX__;   // w0 = 0: no kink (sorted last, never below an edge)
+    tau[t] = tk;
+    sw0[t] = wk;
+    sb0[t] = bk;
+  }
+  __syncthreads();
+  {   // rank of knot k: four quarter counts over 32 knots each
+    const int k = t & (L - 1), p = t >> 7;
+    const float tq = tau[k];
+    int r = 0;
+#pragma unroll
+    for (int q = 32 * p; q < 32 * p + 32; ++q) r += (tau[q] < tq || (tau[q] == tq && q < k)) ? 1 : 0;
+    reinterpret_cast<int*>(red)[t] = r;
+  }
+  __syncthreads();
+  if (t < L) {
+    const int* cnt = reinterpret_cast<const int*>(red);
+    const int r = cnt[t] + cnt[L + t] + cnt[2 * L + t] + cnt[3 * L + t];
+    rank[t] = r;
+    if (i == 0) tab[r] = tk;
+  }
+  __syncthreads();
+  // interval i: the edges with exactly i knots below them; output j, features [32 p, 32 p + 32)
+  const int j = t & (L - 1), p = t >> 7;
+  double u = 0., v = 0.;
+#pragma unroll
+  for (int q = 32 * p; q < 32 * p + 32; ++q) {
+    const float wq = sw0[q], bq = sb0[q];
+    const bool act = wq > 0.f ? rank[q] < i : (wq < 0.f ? rank[q] >= i : bq > 0.f);
+    const double a = act ? (double)sw[j * (L + 1) + q] : 0.;
+    u += a * (double)wq;
+    v += a * (double)bq;
+  }
+  red[p][0][j] = u;
+  red[p][1][j] = v;
+  __syncthreads();
+  if (t < L) {
+    const double uu = ((red[0][0][t] + red[1][0][t]) + red[2][0][t]) + red[3][0][t];
+    const double vv = (double)b2[t] + (((red[0][1][t] + red[1][1][t]) + red[2][1][t]) + red[3][1][t]);
+    tab[EK_KNOTS + 2 * L * i + t] = (float)uu;
+    tab[EK_KNOTS + 2 * L * i + L + t] = (float)vv;
+  }
+}
+
+// The edges' a2 rows from the knot table (in LDS): 32 threads per row, 4 features each, 16 rows per block pass.
+// The block's inputs come in chunks of EK_CH rows through LDS with each row's interval, searched once per row by
+// one lane: searched by all 32 lanes of the row in the write loop, the compiler serialised the rows' chains of
+// dependent LDS reads (30.5 us per config-2 call).  The LayerNorm partials as edge_enc_fwd_kernel.
+// Plain (not nontemporal) row stores: 27.3 -> 23.6 us per config-2 call, the step-0 edge forward that reads the
+// rows no slower (PDG_EK_NT=1: nontemporal, the policy of the other row stores)
+#ifndef PDG_EK_NT
+#define PDG_EK_NT 0
+#endif
+constexpr int EK_U = 4;
+constexpr int EK_CH = 2048;                              // rows per input chunk
+constexpr int EK_SHM = (EK_TAB + 2 * EK_CH) * 4;         // 148.6 KB
+__global__ __launch_bounds__(EBW_THREADS) void edge_enc_fwd_knots_kernel(int E, const float* __restrict__ e_in,
+                                                                           const float* __restrict__ tab,
+                                                                           float* __restrict__ a2,
+                                                                           double* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  float* st = reinterpret_cast<float*>(sm);
+  float* se = st + EK_TAB;
+  int* sp = reinterpret_cast<int*>(se + EK_CH);
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  int r0, r1;
+  block_rows(E, r0, r1);
+  constexpr int NE = EK_CH / EBW_THREADS;
+  float ve[NE];
+  auto load_chunk = [&](int c0) {   // clamped: E > 0 (an empty block reads row E - 1)
+#pragma unroll
+    for (int q = 0; q < NE; ++q) ve[q] = e_in[clamp_row(c0 + threadIdx.x + q * EBW_THREADS, r1)];
+  };
+  // the chunk's inputs and their intervals (knots below e: one branch-free search per row, by one lane)
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int q = 0; q < NE; ++q) {
+      const float e = ve[q];
+      int pos = 0;
+#pragma unroll
+      for (int h = EK_KNOTS / 2; h >= 1; h >>= 1) pos += st[pos + h - 1] < e ? h : 0;
+      pos += st[pos] < e ? 1 : 0;
+      se[threadIdx.x + q * EBW_THREADS] = e;
+      sp[threadIdx.x + q * EBW_THREADS] = pos;
+    }
+  };
+  load_chunk(r0);
+  {   // the table into LDS: every load issued before the first store (one L2 round trip, not 17)
+    constexpr int NV = (EK_TAB / 4 + EBW_THREADS - 1) / EBW_THREADS;
+    f32x4 v[NV];
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int x = 4 * (threadIdx.x + q * EBW_THREADS);
+      v[q] = *reinterpret_cast<const f32x4*>(tab + (x < EK_TAB ? x : 0));
+    }
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int x = 4 * (threadIdx.x + q * EBW_THREADS);
+      if (x < EK_TAB) *reinterpret_cast<f32x4*>(st + x) = v[q];
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rs_a2 = rows_rsrc(a2, r0, r1);
+  double s1 = 0, s2 = 0;
+  __syncthreads();   // the table in LDS
+  for (int c0 = r0; c0 < r1; c0 += EK_CH) {
+    store_chunk();
+    __syncthreads();   // the chunk in LDS
+    if (c0 + EK_CH < r1) load_chunk(c0 + EK_CH);   // in flight while this chunk's rows are written
+    const int n = min(EK_CH, r1 - c0);
+    for (int b = 0; b < n; b += 16 * EK_U) {
+#pragma unroll
+      for (int u = 0; u < EK_U; ++u) {
+        const int rr = b + rg + 16 * u;
+        const float e = se[rr];
+        const int pos = sp[rr];
+        const f32x4 U = *reinterpret_cast<const f32x4*>(st + EK_KNOTS + 2 * L * pos + 4 * cg);
+        const f32x4 V = *reinterpret_cast<const f32x4*>(st + EK_KNOTS + 2 * L * pos + L + 4 * cg);
+        f32x4 a;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = fmaxf(fmaf(e, U[q], V[q]), 0.f);
+        if (PDG_EK_NT)
+          rows_store4_nt(rs_a2, c0 - r0 + rr, 4 * cg, a);   // rows past r1 dropped
+        else
+          rows_store4(rs_a2, c0 - r0 + rr, 4 * cg, a);
+        const float k = rr < n ? 1.f : 0.f;   // branch-free: a branch here split the rows' code apart
+        s1 += (double)(k * ((a[0] + a[1]) + (a[2] + a[3])));
+        s2 += (double)(k * ((a[0] * a[0] + a[1] * a[1]) + (a[2] * a[2] + a[3] * a[3])));
+      }
+    }
+    __syncthreads();   // the chunk is read
+  }
+  double* red = reinterpret_cast<double*>(sm);
+  __syncthreads();
+  block_sum2(s1, s2, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s1;
+    part[2 * blockIdx.x + 1] = s2;
+  }
+}
+
 // ============================================================================ node encoder forward
 // The node encoder (models.py:260-274, 6 inputs -> 128 -> 128 + the LayerNorm partials of the output) in
 // the layout of edge_enc_fwd_kernel: a1 = relu(W0 x + b0) per element in encoder_kernel's order (bitwise
@@ -2552,6 +2729,13 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
 #define PDG_EEB_MASK 1
 #endif
 constexpr int EEB3_BUF = 2 * IMG16 + T16;   // one round's gz2 and gz2.e images and the mask image
+// NS register sets of row loads: set s holds round n's rows (n = s mod NS) from its issue NS - 1 stages ahead
+// until its stage; the two LDS buffers alternate by round parity.  Four sets (64 KB of loads in flight per CU)
+// measured the same as two (69.7 / 70.4 vs 70.3 / 69.0 us per config-2 call): the kernel is not waiting on rows.
+#ifndef PDG_EEB_SETS
+#define PDG_EEB_SETS 2
+#endif
+template <int NS>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd3_kernel(
     const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ e_in,
     const float* __restrict__ w0, const float* __restrict__ b0, const pdg_ln_stat* __restrict__ st_p,
@@ -2572,8 +2756,8 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd3_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) accM[b][r] = accN[b][r] = 0.f;
   f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 pg[2], pa2[2];
-  float pe[2];
+  f32x4 pg[NS], pa2[NS];
+  float pe[NS];
   auto issue = [&](const int s, int base) {   // clamped: E > 0 (an empty block reads row E - 1)
     const int rc = clamp_row(base + rg, r1);
     pg[s] = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + 4 * cg);
@@ -2584,16 +2768,17 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd3_kernel(
   const f32x4 w04 = *reinterpret_cast<const f32x4*>(w0 + 4 * cg);
   const f32x4 b04 = *reinterpret_cast<const f32x4*>(b0 + 4 * cg);
   const LNStat st = *reinterpret_cast<const LNStat*>(st_p);
-  issue(0, r0);
-  __builtin_amdgcn_sched_barrier(0);
-  issue(1, r0 + R16);
-  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    issue(q, r0 + q * R16);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   const pdg_ln_bwd lb = lnb_resolve(lb_p, pairs, npairs, st_p);
   pin_vgpr(g4);
   pin_vgpr(w04);
   pin_vgpr(b04);
-  auto stage = [&](const int s, const int base) {
-    unsigned char* img_g = sm + s * EEB3_BUF;                  // gz2
+  auto stage = [&](const int s, const int base) {   // set s into LDS buffer s & 1
+    unsigned char* img_g = sm + (s & 1) * EEB3_BUF;            // gz2
     unsigned char* img_e = img_g + IMG16;                      // gz2 . e
     unsigned char* img_m = img_g + 2 * IMG16;                  // [a1 > 0] as bf16 0 / 1 (one term)
     const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2615,7 +2800,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd3_kernel(
       mb[j] = (ok && a > 0.f) ? 0x3F80u : 0u;
     }
     *reinterpret_cast<u32x2*>(img_m + x6_addr(rg, 8 * cg)) = u32x2{mb[0] | (mb[1] << 16), mb[2] | (mb[3] << 16)};
-    issue(s, base + 2 * R16);   // the set is free: the round after next
+    issue(s, base + NS * R16);   // the set is free: NS rounds on
   };
   auto compute = [&](const int s) {
     const unsigned char* img_g = sm + s * EEB3_BUF;
@@ -2647,13 +2832,14 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd3_kernel(
   };
   stage(0, r0);
   __syncthreads();
-  for (int base = r0; base < r1; base += 2 * R16) {
-    compute(0);
-    stage(1, base + R16);
-    __syncthreads();
-    compute(1);
-    stage(0, base + 2 * R16);   // past r1 on the last step: zero rows nobody reads
-    __syncthreads();
+  for (int base = r0; base < r1; base += NS * R16) {
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      compute(q & 1);
+      if (q + 1 < NS && base + (q + 1) * R16 >= r1) break;   // block-uniform
+      stage((q + 1) % NS, base + (q + 1) * R16);   // past r1 on the last step: zero rows nobody reads
+      __syncthreads();
+    }
   }
   __syncthreads();   // the last rounds' image reads precede the LDS reuse below
   // dW2 into the block's slab; dw0 / db0 partials: per thread over its 16 rows o of each column i, then the
@@ -2707,7 +2893,7 @@ extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, c
                 "pdg_edge_enc_bwd: misaligned pointer");
   if (PDG_EEB_MASK) {
     const size_t shm3 = 2 * EEB3_BUF > 16 * L * 4 + 8 * L * 8 ? 2 * EEB3_BUF : 16 * L * 4 + 8 * L * 8;
-    hipLaunchKernelGGL(edge_enc_bwd3_kernel, dim3(nslabs), dim3(EBW_THREADS), shm3, (hipStream_t)stream, gy, a2, e_in,
+    hipLaunchKernelGGL(edge_enc_bwd3_kernel<PDG_EEB_SETS>, dim3(nslabs), dim3(EBW_THREADS), shm3, (hipStream_t)stream, gy, a2, e_in,
                        w0, b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs, narrow_sums, n_edges, slab_init);
     PDG_CHECK_LAUNCH("pdg_edge_enc_bwd");
     return PDG_OK;
@@ -2817,6 +3003,22 @@ extern "C" int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0,
   PDG_CHECK_LAUNCH("pdg_edge_enc_fwd");
   return PDG_OK;
 }
+
+extern "C" int pdg_edge_enc_fwd_knots(int n_edges, const float* e_in, const float* w0, const float* b0,
+                                      const float* W2, const float* b2, float* table, float* a2, double* partials,
+                                      int nblocks, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_enc_fwd_knots: bad sizes");
+  PDG_CHECK_ARG(e_in && w0 && b0 && W2 && b2 && table && a2 && partials, "pdg_edge_enc_fwd_knots: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(table) && PDG_ALIGNED(a2), "pdg_edge_enc_fwd_knots: misaligned pointer");
+  hipLaunchKernelGGL(edge_knots_kernel, dim3(EK_KNOTS + 1), dim3(EBW_THREADS), 0, (hipStream_t)stream, w0, b0, W2, b2, table);
+  PDG_CHECK_LAUNCH("pdg_edge_enc_fwd_knots");
+  hipLaunchKernelGGL(edge_enc_fwd_knots_kernel, dim3(nblocks), dim3(EBW_THREADS), (size_t)EK_SHM,
+                     (hipStream_t)stream, n_edges, e_in, table, a2, partials);
+  PDG_CHECK_LAUNCH("pdg_edge_enc_fwd_knots");
+  return PDG_OK;
+}
+
+extern "C" int pdg_edge_enc_knots_floats(void) { return EK_TAB; }
 
 extern "C" int pdg_gemm_sum2_coop(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
                                   const float* res, float* out, const float* ln_a2, const pdg_ln_stat* ln_st,

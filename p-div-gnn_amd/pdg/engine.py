@@ -94,6 +94,12 @@ VARIANTS = {
     "node_enc_coop": ("PDG_NODE_ENC_COOP", True),
     # the decoder likewise (pdg_decoder_fwd_coop) instead of the LDS-weight pdg_decoder_fwd[_fin]
     "decoder_coop": ("PDG_DECODER_COOP", True),
+    # the edge encoder forward from its knot table (pdg_edge_enc_fwd_knots: one fma per output, no W2 product)
+    # instead of pdg_edge_enc_fwd: 33.6 vs 48.3 us per config-2 step and closer to fp64, but off: its rounding
+    # differs in kind from the reference's fp32 products, and after the resumed Adam step of
+    # tests/test_gpu_checkpoint.py the LayerNorm biases (gradient components at noise level, which Adam
+    # normalises) sit 1.03e-5 from the reference's instead of 1.0e-7 (EXPERIMENTS.md section 4)
+    "edge_enc_knots": ("PDG_EDGE_ENC_KNOTS", False),
     # pdg_edge_enc_fwd blocks per CU (104 VGPRs, 41 KB LDS per 8-wave block)
     "enc_blocks_per_cu": ("PDG_ENC_BLOCKS_PER_CU", 2),
 }
@@ -206,6 +212,8 @@ class EPDEngine:
         self.coop_fwd = var["coop_fwd"]
         self.node_enc_coop = var["node_enc_coop"]
         self.decoder_coop = var["decoder_coop"]
+        self.edge_enc_knots = var["edge_enc_knots"]
+        self._knots = torch.empty(lib.pdg_edge_enc_knots_floats(), dtype=torch.float32, device=self.device)
         # the P / Q layout the library's node pre-pass writes and its cooperative edge forward reads
         self.pq_blocked = bool(lib.pdg_pq_layout())
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
@@ -304,7 +312,14 @@ class EPDEngine:
         # pdg_edge_enc_bwd recomputes it from the scalar input
         a1_ee = self._empty(E, L) if (need_grad and not self.fused_edge_wgrad) else None
         a2_ee = self._empty(E, L)
-        if E and a1_ee is None:   # bf16x6 W2 product, register-stationary (pdg_edge_enc_fwd)
+        if E and a1_ee is None and self.edge_enc_knots:   # piecewise-linear form (pdg_edge_enc_fwd_knots)
+            nb = self._nslabs_e   # one block per CU (the table and a row chunk take 148.6 KB of LDS)
+            self._t("edge_enc_fwd", lib.pdg_edge_enc_fwd_knots, E, _p(e_in), _p(P["edge_encoder.0.weight"]),
+                    _p(P["edge_encoder.0.bias"]), _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]),
+                    _p(self._knots), _p(a2_ee), _p(self._part_a), nb, s)
+            self._nparts.value = nb
+            self._finalize(self._part_a, E * L, st[1], s, True)
+        elif E and a1_ee is None:   # bf16x6 W2 product, register-stationary (pdg_edge_enc_fwd)
             nb = self._enc_blocks
             self._t("edge_enc_fwd", lib.pdg_edge_enc_fwd, E, _p(e_in), _p(P["edge_encoder.0.weight"]),
                     _p(P["edge_encoder.0.bias"]), _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]),

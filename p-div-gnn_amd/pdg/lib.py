@@ -78,6 +78,8 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
+    "pdg_edge_enc_fwd_knots": [I, P, P, P, P, P, P, P, P, I, P],
+    "pdg_edge_enc_knots_floats": [],
     "pdg_node_enc_fwd": [I, P, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_node_bwd_coop": [I] + [P] * 14 + [I, I, P],
@@ -147,7 +149,8 @@ class _Lib:
         if not name.startswith("pdg_"):
             raise AttributeError(name)
         fn = getattr(self.load(), name)
-        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks", "pdg_wgrad_slabs_per_cu", "pdg_pq_layout"):
+        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks", "pdg_wgrad_slabs_per_cu", "pdg_pq_layout",
+                                                  "pdg_edge_enc_knots_floats"):
             return fn
 
         def call(*args):

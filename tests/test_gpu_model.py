@@ -312,7 +312,8 @@ def test_gz1e_from_gc_matches_stored_gz1e(nmesh, ngraph, steps):
 @pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
 def test_forward_variants_agree(nmesh, ngraph, steps):
     """The two edge-forward kernels of the engine: pdg_edge_fwd_coop (default: block-cooperative, C and W2
-    in unbiased bf16x6) and pdg_edge_fwd (LDS weights, C in fp32 MFMAs).  Output (training and inference)
+    in unbiased bf16x6) and pdg_edge_fwd (LDS weights, C in fp32 MFMAs), with the two edge-encoder forwards
+    (pdg_edge_enc_fwd's bf16x6 W2 product, default, and the knot-table pdg_edge_enc_fwd_knots).  Output (training and inference)
     agree to 1e-5 and every parameter gradient to VARIANT_TOL (two fp32 evaluations may differ in a relu
     mask bit whose pre-activation is within rounding of zero)."""
     from gnn_local_stress import losses
@@ -325,6 +326,7 @@ def test_forward_variants_agree(nmesh, ngraph, steps):
         model = _model(steps, stats)
         eng = model._engine_for(batch.pos.device)
         eng.coop_fwd = coop
+        eng.edge_enc_knots = not coop   # the knot-table edge encoder (A/B variant) beside the default one
         with torch.no_grad():
             y_inf = model(batch, scale_output=True).local_stress.clone()
         pred = model(batch, scale_output=False).local_stress

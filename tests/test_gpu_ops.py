@@ -919,25 +919,67 @@ def test_wgrad_reduce_batch_matches_single(env):
             assert rel(outs["batch"][1][i].double().cpu() - gb0[i].double().cpu(), ref[L * L:]) < 1e-5
 
 
+@pytest.mark.parametrize("kind", ["knots", "x6"])
 @pytest.mark.parametrize("E,nb", [(77, 37), (4099, 37), (20000, 512)])
-def test_edge_enc_fwd_vs_fp64(env, E, nb):
-    """pdg_edge_enc_fwd (edge encoder, W2 product in bf16x6, register-stationary) against an fp64
-    restatement: a2 to fp32 rounding, the LayerNorm partials' (sum, sum of squares) to 1e-6."""
+def test_edge_enc_fwd_vs_fp64(env, E, nb, kind):
+    """pdg_edge_enc_fwd (default: W2 product in bf16x6, register-stationary) and pdg_edge_enc_fwd_knots
+    (A/B variant: piecewise-linear form, knot table) against an fp64 restatement: a2 to fp32 rounding, the LayerNorm partials'
+    (sum, sum of squares) to 1e-6.  Rows past the edges are not written (the NaN fill survives nowhere)."""
     lib, sh, _ = env
     s = sh()
     e_in = rnd(E)
     w0, b0 = lin(L, 1)
     W2, b2 = lin(L, L)
-    a2 = torch.full((E, L), float("nan"), device="cuda")
+    a2 = torch.full((E + 5, L), float("nan"), device="cuda")
     part = torch.zeros(2 * nb, dtype=torch.float64, device="cuda")
-    lib.pdg_edge_enc_fwd(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
-                         a2.data_ptr(), part.data_ptr(), nb, s)
+    if kind == "knots":
+        tab = torch.empty(lib.pdg_edge_enc_knots_floats(), device="cuda")
+        lib.pdg_edge_enc_fwd_knots(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                                   tab.data_ptr(), a2.data_ptr(), part.data_ptr(), nb, s)
+    else:
+        lib.pdg_edge_enc_fwd(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                             a2.data_ptr(), part.data_ptr(), nb, s)
+    assert bool(a2[E:].isnan().all())
+    a2 = a2[:E]
     a1 = torch.relu(e_in.double()[:, None] * w0.double()[:, 0][None, :] + b0.double())
     ref = torch.relu(a1 @ W2.double().T + b2.double())
     assert rel(a2, ref) < TOL
     p = part.view(nb, 2).sum(0).cpu()
     assert abs(float(p[0]) - float(ref.sum())) <= 1e-6 * float(ref.abs().sum())
     assert abs(float(p[1]) - float((ref * ref).sum())) <= 1e-6 * float((ref * ref).sum())
+
+
+def test_edge_enc_fwd_knots_edge_cases(env):
+    """pdg_edge_enc_fwd_knots on the cases the knot table must get right: zero first-layer weights (a feature
+    active everywhere or nowhere, no knot), repeated knots (two features with the same w0, b0), inputs exactly
+    at knots and beyond every knot on both sides, and one edge: a2 within fp32 rounding of fp64."""
+    lib, sh, _ = env
+    s = sh()
+    w0, b0 = lin(L, 1)
+    W2, b2 = lin(L, L)
+    w0[:8] = 0.0
+    b0[:4] = 0.3
+    b0[4:8] = -0.2
+    w0[20], b0[20] = w0[21], b0[21]
+    w0[30], b0[30] = w0[31], b0[31]
+    knots = (-b0[8:] / w0[8:, 0]).float()
+    e_in = torch.cat([knots, knots * (1 + 1e-7), torch.tensor([-1e30, 1e30, 0.0, -0.0], device="cuda"),
+                      rnd(500, scale=5.0)]).contiguous()
+    tab = torch.empty(lib.pdg_edge_enc_knots_floats(), device="cuda")
+    for E in (1, e_in.numel()):
+        a2 = torch.full((E, L), float("nan"), device="cuda")
+        part = torch.zeros(2 * 37, dtype=torch.float64, device="cuda")
+        lib.pdg_edge_enc_fwd_knots(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                                   tab.data_ptr(), a2.data_ptr(), part.data_ptr(), 37, s)
+        a1 = torch.relu(e_in[:E].double()[:, None] * w0.double()[:, 0][None, :] + b0.double())
+        ref = torch.relu(a1 @ W2.double().T + b2.double())
+        mid = ref.abs().amax(1) < 1e20   # the +-1e30 rows: compare relative to their own scale
+        assert rel(a2[mid], ref[mid]) < TOL, rel(a2[mid], ref[mid])
+        if (~mid).any():
+            assert rel(a2[~mid], ref[~mid]) < TOL
+        p = part.view(37, 2).sum(0).cpu()
+        if E == 1:
+            assert abs(float(p[0]) - float(ref.sum())) <= 1e-6 * float(ref.abs().sum())
 
 
 @pytest.mark.parametrize("N,nb", [(7, 37), (1031, 37), (40328, 256), (100489, 256)])
