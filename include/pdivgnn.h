@@ -184,6 +184,11 @@ int pdg_decoder_fwd_coop(int n_nodes, const float* a2_prev, const pdg_ln_stat* s
 /* torch.any(x != 0) into *flag (int, device). models.py:294 */
 int pdg_any_nonzero(const float* x, int64_t n, int* flag, void* stream);
 
+/* y[i] = 0 for every i < n unless *flag (device int) is set: the zero-stress guard of models.py:294-299
+ * ("return zeros_like(mean_stress)") decided on the device, for a forward replayed from a HIP graph
+ * (pdg/serve.py) where the reference's host-side torch.any would cost a synchronisation per call. */
+int pdg_zero_unless(const int* flag, float* y, int64_t n, void* stream);
+
 /* ---------------------------------------------------------------- backward */
 
 /* Decoder backward: gz1d = (Wd2^T gy) * [a1d > 0]; gx = Wd1^T gz1d. */

@@ -865,6 +865,11 @@ extern "C" int pdg_decoder_fwd_fin(int n_nodes, const float* a2_prev, const doub
 }
 
 // ============================================================================ any-nonzero guard
+// The flag is cleared by a one-thread kernel, not hipMemsetAsync: captured into a HIP graph
+// (pdg/serve.py), a 4-byte memset node was replayed on the test box with a garbage byte value (the flag
+// read 0x7c7c7c7c on one replay, 0 on the next; tests/test_gpu_published.py), kernel nodes are exact.
+__global__ void flag_clear_kernel(int* __restrict__ flag) { *flag = 0; }
+
 __global__ void any_nonzero_kernel(const float* __restrict__ x, long n, int* __restrict__ flag) {
   int found = 0;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
@@ -874,16 +879,29 @@ __global__ void any_nonzero_kernel(const float* __restrict__ x, long n, int* __r
 
 extern "C" int pdg_any_nonzero(const float* x, int64_t n, int* flag, void* stream) {
   PDG_CHECK_ARG(n >= 0 && flag != nullptr, "pdg_any_nonzero: bad args");
-  if (hipMemsetAsync(flag, 0, sizeof(int), (hipStream_t)stream) != hipSuccess) {
-    set_error("pdg_any_nonzero: memset failed");
-    return PDG_ERR_HIP;
-  }
+  hipLaunchKernelGGL(flag_clear_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, flag);
+  PDG_CHECK_LAUNCH("pdg_any_nonzero");
   if (n == 0) return PDG_OK;
   long blocks = (n + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(any_nonzero_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x, (long)n,
                      flag);
   PDG_CHECK_LAUNCH("pdg_any_nonzero");
+  return PDG_OK;
+}
+
+__global__ void zero_unless_kernel(const int* __restrict__ flag, float* __restrict__ y, long n) {
+  if (*flag) return;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) y[i] = 0.f;
+}
+
+extern "C" int pdg_zero_unless(const int* flag, float* y, int64_t n, void* stream) {
+  PDG_CHECK_ARG(n >= 0 && flag != nullptr && (n == 0 || y != nullptr), "pdg_zero_unless: bad args");
+  if (n == 0) return PDG_OK;
+  long blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(zero_unless_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, flag, y, (long)n);
+  PDG_CHECK_LAUNCH("pdg_zero_unless");
   return PDG_OK;
 }
 

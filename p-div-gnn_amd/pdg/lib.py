@@ -59,6 +59,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_decoder_fwd_fin": [I, P, P, I, c_double, P] + [P] * 10 + [I, P, P],
     "pdg_decoder_fwd_coop": [I, P, P, P, I, c_double, P] + [P] * 10 + [I, P, I, P],
     "pdg_any_nonzero": [P, c_int64, P, P],
+    "pdg_zero_unless": [P, P, c_int64, P],
     "pdg_decoder_bwd": [I, P, P, P, P, P, P, P],
     "pdg_ln_colsum": [I, P, P, P, P, P, P, P, P, I, P],
     "pdg_ln_colsum_nodes": [I, P, P, P, P, P, P, P, I, P],
@@ -124,6 +125,8 @@ class PdgError(RuntimeError):
 class _Lib:
     def __init__(self) -> None:
         self._dll = None
+        self.calls = 0   # status-returning entry points called (launch counts: pdg/serve.py, bench.py)
+        self.hook = None  # optional callable(name) run after every such call (fault localisation tools)
 
     def load(self) -> ctypes.CDLL:
         if self._dll is None:
@@ -154,10 +157,13 @@ class _Lib:
             return fn
 
         def call(*args):
+            self.calls += 1
             rc = fn(*args)
             if rc != 0:
                 msg = self.load().pdg_last_error().decode(errors="replace")
                 raise PdgError(f"{name} failed ({rc}): {msg}")
+            if self.hook is not None:
+                self.hook(name)
             if _DEBUG_SYNC:   # fault localisation: every launch completes before the next (stderr names it)
                 import sys
                 print(f"[pdg] {name}", file=sys.stderr, flush=True)

@@ -86,4 +86,43 @@ def test_compulsory_bytes_of_the_edge_forward_at_config_2():
     assert comp["edge_bwd"] == work["edge_bwd"][1] - (E - N) * 512
     assert comp["node_net"] == work["node_net"][1]
     r = bench.roofline("edge_fwd", work, {"edge_fwd": 2e-4}, {"edge_fwd": 2e-3}, 8e-3, {}, {"edge_fwd": 10}, None, comp)
-    assert r["frac_compulsory"] == round(comp["edge_fwd"] / 2e-4 / bench.PEAK_HBM, 4) < r["frac"]
+    assert r["frac_compulsory"] == round(comp["edge_fwd"] / 2e-4 / bench.PEAK_HBM, 4) < r["frac_gather_priced"]
+
+
+def test_headline_frac_is_the_compulsory_fraction():
+    """roofline.frac = bytes_compulsory_per_launch / avg_launch / 8 TB/s (0.61 at
+    config 2's 192.5 us launches), the per-edge-priced figure only as frac_gather_priced (0.88) and
+    SURVEY §8(d)'s reads-only formula (24 L E + 8 E = 740 MB) as frac_reads_only; with PMC bytes of the
+    same tree, frac_pmc and their ratio to the compulsory bytes."""
+    N, E, S, slab = 40328, 239744, 10, 256 * (128 * 128 + 128) * 4
+    work = bench.kernel_work(False, N, E, S, slab, True, e_sum=True)
+    comp = bench.compulsory_bytes(work, N, E)
+    t = 192.5e-6
+    ro = bench.reads_only_bytes("edge_fwd", E)
+    assert round(ro / 1e6, 1) == 738.4
+    assert bench.reads_only_bytes("segment_sum", E) is None
+    pmc = {"edge_fwd": 905_200_000}
+    r = bench.roofline("edge_fwd", work, {"edge_fwd": t}, {"edge_fwd": 8 * t}, 8e-3, pmc, {"edge_fwd": 24}, None,
+                       comp, ro)
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s"
+    assert r["frac"] == round(comp["edge_fwd"] / t / 8e12, 4) == r["frac_compulsory"]
+    assert abs(r["frac"] - 0.6129) < 2e-4
+    assert r["bytes_per_launch"] == r["bytes_compulsory_per_launch"] == comp["edge_fwd"]
+    assert r["achieved"] == round(comp["edge_fwd"] / t / 1e9, 2)
+    assert r["frac_gather_priced"] == round(work["edge_fwd"][1] / t / 8e12, 4) > r["frac"]
+    assert r["frac_reads_only"] == round(ro / t / 8e12, 4) < r["frac"]
+    assert r["frac_pmc"] == round(905_200_000 / t / 8e12, 4)
+    assert r["pmc_over_compulsory"] == round(905_200_000 / comp["edge_fwd"], 4)
+
+
+def test_counter_files_are_per_config(tmp_path, monkeypatch):
+    """Configs 3-5 take their counters from profiles/rNN_pmc_traffic_cC.json / rNN_sq_cC.json of the same
+    tree; the main line's (config 2) file never prices another config's launches."""
+    monkeypatch.setattr(bench, "ROOT", tmp_path)
+    main = _write(tmp_path, "r06_pmc_traffic.json", "aaaa", 1.0e9)
+    c5 = _write(tmp_path, "r06_pmc_traffic_c5.json", "aaaa", 3.0e9)
+    assert bench.pmc_file("aaaa", config=2) == (main, None)
+    assert bench.pmc_file("aaaa", config=5) == (c5, None)
+    path, reason = bench.pmc_file("aaaa", config=3)
+    assert path is None and "_c3" in reason
+    assert bench.load_pmc(True, c5)["edge_fwd"] == 3_000_000_000
