@@ -68,7 +68,6 @@ PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd
              "wgrad_W2": "wgrad_x6_kernel",
              # the edge-update instantiations
              "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
-             "edge_bwd_fused": "void edge_bwd_fused_kernel<true>",
              "edge_gout": "void edge_gout_wc_kernel<true>",
              "node_bwd": "node_bwd_coop_kernel", "node_pq": "void node_pq_x6_kernel<true>",
              "gemm_sum2": "void gemm_sum2_coop_kernel<true>", "wgrad_pairs": "void wgrad_x6_pair2_kernel"}
@@ -241,8 +240,7 @@ def cpu_baseline(cfg, samples, full_graphs: int, reps: int = 5, one_thread: bool
 
 
 # ---------------------------------------------------------------------------------- roofline
-def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, e_sum: bool = True,
-                one_pass: bool = False) -> dict:
+def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bool, e_sum: bool = True) -> dict:
     """Algorithmic work per launch (DESIGN.md "Kernels"): executed MFMA flops with the peak of their
     instruction type, and the bytes the kernel must read/write (inputs once, outputs once, int32
     indices).  An fp32-accurate 128x128 product per row costs 2*L*L fp32 flops on the fp32 MFMA,
@@ -273,10 +271,6 @@ def kernel_work(infer: bool, N: int, E: int, S: int, nslab_bytes: int, fused: bo
                      2 * 4 * L * N + (1 if infer else 2) * 4 * L * N),
         "pq_scatter_bwd": ([], 2 * 4 * L * E + 4 * E + 8 * (N + 1) + 2 * 4 * L * N),
     }
-    if one_pass:   # pdg_edge_bwd_fused: the W2 and Wc work of both kernels (6 bf16x6 products per edge);
-        # reads gaggr[dst], a2m, a1m, ge_next, a2e, a1e, e, a2ln, dst; writes gz1m, gC, ge_out; two slab sets
-        out["edge_bwd"] = ([(E * 6 * g * X6, PEAK_BF16_MFMA)], E * (11 * 4 * L + 4) + 4 * nslab_bytes)
-        out.pop("edge_gout")
     return out
 
 
@@ -321,7 +315,7 @@ def pmc_tree() -> str | None:
     return json.loads(f.read_text())["_meta"]["tree"] if f else None
 
 
-def load_pmc(fused: bool, path=None, one_pass: bool = False) -> dict:
+def load_pmc(fused: bool, path=None) -> dict:
     """Per-launch PMC bytes by kernel from `path` (a pmc_file() result; {} when None)."""
     pmc = {}
     if path is not None and Path(path).exists():
@@ -329,7 +323,7 @@ def load_pmc(fused: bool, path=None, one_pass: bool = False) -> dict:
         data.pop("_meta", None)
         for k, prefix in PMC_NAMES.items():
             if fused and k == "edge_bwd":
-                prefix = PMC_NAMES["edge_bwd_fused" if one_pass else "edge_bwd_w2"]
+                prefix = PMC_NAMES["edge_bwd_w2"]
             hit = [v for name, v in data.items() if name.startswith(prefix if isinstance(prefix, tuple) else (prefix,))]
             if hit:
                 pmc[k] = round(hit[0]["total"])
@@ -543,12 +537,10 @@ def time_config(cid: int, args, rank: int, world: int, pg, device) -> tuple[dict
     ktot = {k: sum(a.elapsed_time(b) for a, b in v) * 1e-3 for k, v in ev.items()}
     fused = eng.fused_edge_wgrad
     nslab_bytes = getattr(eng, "_nslabs_e", 256) * (L * L + L) * 4
-    one_pass = fused and getattr(eng, "fused_edge_bwd", False)
-    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, fused and getattr(eng, "gz1e_from_gc", False),
-                       one_pass)
+    work = kernel_work(infer, N, E, cfg["steps"], nslab_bytes, fused, fused and getattr(eng, "gz1e_from_gc", False))
     comp = compulsory_bytes(work, N, E)
     pmc_path, pmc_reason = pmc_file(config=cid)
-    pmc = load_pmc(fused, pmc_path, one_pass)
+    pmc = load_pmc(fused, pmc_path)
     sq_path, sq_reason = sq_file(config=cid)
     sq = load_sq(sq_path)
     step_s = el * ev_steps / args.steps

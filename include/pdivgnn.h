@@ -295,17 +295,6 @@ int pdg_gemm_sum2_rw(int rows, const float* in0, const float* in1, const float* 
  * LayerNorm partials of a2 (nblocks pairs).  a1 is not stored (pdg_edge_enc_bwd recomputes it). */
 int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0, const float* b0, const float* W2,
                      const float* b2, float* a2, double* partials, int nblocks, void* stream);
-/* The same outputs from the piecewise-linear form of the encoder (engine A/B variant): with one scalar
- * input, a1 = relu(w0 e + b0) has a kink at each knot -b0[k] / w0[k], and between consecutive knots
- * a2 = relu(e U_i + V_i) with U_i = W2 (w0 . m_i), V_i = b2 + W2 (b0 . m_i) for the interval's fixed relu
- * mask m_i.  One launch forms the 129 (U_i, V_i) rows in fp64 into `table` (pdg_edge_enc_knots_floats()
- * floats, 16-byte aligned, device scratch), a second streams a2 (one knot search and one fma per output)
- * and the LayerNorm partials (nblocks pairs; one block per CU: the table and a chunk of rows occupy
- * 148.6 KB of LDS). */
-int pdg_edge_enc_fwd_knots(int n_edges, const float* e_in, const float* w0, const float* b0,
-                           const float* W2, const float* b2, float* table, float* a2, double* partials,
-                           int nblocks, void* stream);
-int pdg_edge_enc_knots_floats(void);
 /* pdg_gemm_sum2_rw in the block-cooperative layout (nblocks blocks of 512 threads, contiguous row
  * ranges): out = W0T in0 + W1T in1 [+ res], both products in bf16x6 with the weights stationary in
  * registers; partials != NULL: the LayerNorm column partials and pairs as pdg_gemm_sum2_rw (nblocks
@@ -378,22 +367,6 @@ int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* 
                      const float* WcT, float* ge_out, float* slabs, int nslabs, const float* a2ln,
                      const pdg_ln_stat* st_ln, double* ln_partials, const float* ln_g, double* pairs,
                      int accumulate, int slab_init, void* stream);
-/* pdg_edge_bwd_w2 + pdg_edge_gout_wc in one pass (the backward of both edge_net evaluations of one
- * message-passing step, models.py:219-225 / :233-238): gz1m, gC (= gz1m + gz1e; gz1e is not stored),
- * ge_out = [ge_next +] WcT gC, slabs_w2 += the dW2 / db2 sums, slabs_wc += the dWc / db1 sums, and the
- * column sums / pairs of the LayerNorm that produced e (a2ln, st_ln, ln_g_e -> ln_partials, ln_pairs,
- * accumulate) as pdg_edge_gout_wc.  ln_g_msg: the edge_net LayerNorm weight (both branches' gz2).
- * ge_next == NULL: the message branch only; gC must then be the gz1m pointer.  gz1m / gC / ge_out equal
- * the split pair's bit for bit; the slab weight sums too, the bias and column sums add in another order.
- * A weight-specialised block per slab (4 waves on W2, 4 on Wc; pdg_ebw.hip), 157 KB of LDS. */
-int pdg_edge_bwd_fused(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
-                       const float* a2m, const float* a1m, const float* a2e, const float* a1e,
-                       const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
-                       const pdg_ln_bwd* lb_e, const float* ln_g_msg, const float* W2T, const float* WcT,
-                       const float* e, const float* a2ln, const pdg_ln_stat* st_ln, const float* ln_g_e,
-                       float* gz1m, float* gC, float* ge_out, float* slabs_w2, float* slabs_wc, int nslabs,
-                       double* ln_partials, double* ln_pairs, const double* pairs_m, int npairs_m,
-                       const double* pairs_e, int npairs_e, int slab_init, int accumulate, void* stream);
 
 /* Mesh graph on the device (pdg_graph.hip): FaceToEdge of a triangle
  * mesh (convert_utils.py:47-60), edge lengths (datasets.py:182-188) and, when `periodic`,

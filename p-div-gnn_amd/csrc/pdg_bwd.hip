@@ -480,9 +480,6 @@ extern "C" int pdg_gemm_sum2(int rows, const float* in0, const float* in1, const
 #define PDG_EDGE_BWD_WAVES PDG_EDGE_WAVES
 #endif
 constexpr int EB_WAVES = PDG_EDGE_BWD_WAVES;
-#ifndef PDG_EB_EARLY_A1E
-#define PDG_EB_EARLY_A1E 0
-#endif
 
 template <bool EU>
 __global__ __launch_bounds__(64 * EB_WAVES, EB_WAVES / 4) void edge_bwd_kernel(
@@ -494,18 +491,11 @@ __global__ __launch_bounds__(64 * EB_WAVES, EB_WAVES / 4) void edge_bwd_kernel(
     float* __restrict__ gz1m, float* __restrict__ gz2e, float* __restrict__ gz1e, float* __restrict__ gC,
     float* __restrict__ ge_out, const double* __restrict__ pm, int npm, const double* __restrict__ pe, int npe) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-#if PDG_EDGE_X6
   load_wblock_swz(lds, WcT, L, 0);                                   // Wc^T (fp32)
   unsigned char* w2p = reinterpret_cast<unsigned char*>(lds + 128 * 128);
   load_wplanes(w2p, W2T, L, 0);                                      // W2^T as bf16 term planes
 #define PDG_GEMM_2(acc, v) gemm128_x6(acc, w2p, v)
 #define PDG_GEMM_C(acc, v) gemm128_swz(acc, lds, v)
-#else
-  load_wblock(lds, W2T, L, 0);
-  load_wblock(lds + WBLK, WcT, L, 0);
-#define PDG_GEMM_2(acc, v) PDG_GEMM_W2(acc, lds, v)
-#define PDG_GEMM_C(acc, v) gemm128(acc, lds + WBLK, v)
-#endif
   const FeatVec fg = load_featvec(lg);
   __syncthreads();
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
@@ -549,17 +539,10 @@ __global__ __launch_bounds__(64 * EB_WAVES, EB_WAVES / 4) void edge_bwd_kernel(
       load_frag(A, a2e + (size_t)rc * L);
       if (valid) store_frag(gz1m + (size_t)row * L, v);
       ln_relu_bwd_fv(G, A, ste, lbe, fg);                  // G := gz2e
-#if PDG_EB_EARLY_A1E
-      load_frag(A, a1e + (size_t)rc * L);
-      if (valid) store_frag(gz2e + (size_t)row * L, G);
-      zero_acc(Z);
-      PDG_GEMM_2(Z, G);
-#else
       zero_acc(Z);
       PDG_GEMM_2(Z, G);
       load_frag(A, a1e + (size_t)rc * L);
       if (valid) store_frag(gz2e + (size_t)row * L, G);
-#endif
       relu_mask_acc(G, Z, A);                              // G := gz1e
       // ge_out = ge_next + Wc^T gC: the accumulator starts as ge_next
       {
@@ -612,7 +595,7 @@ extern "C" int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, con
                 "pdg_edge_bwd: edge-update arguments missing or misaligned");
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd: ge_out must not alias ge_next");
   const int grid = persistent_grid(n_edges, EB_WAVES, 1);
-  const size_t shm = PDG_EDGE_X6 ? (size_t)EDGE_LDS_BYTES : 2 * WBLK * sizeof(float);
+  const size_t shm = (size_t)EDGE_LDS_BYTES;
   if (ge_next)
     hipLaunchKernelGGL(edge_bwd_kernel<true>, dim3(grid), dim3(64 * EB_WAVES), shm, (hipStream_t)stream,
                        n_edges, dst, gaggr, ge_next, a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g, W2T, WcT, gz2m,
@@ -724,6 +707,8 @@ extern "C" int pdg_pq_scatter_bwd(int n_nodes, const int* rowptr_dst, const int*
                                   const float* gz1m, const float* gz1e, int e_is_sum, float* gP, float* gQ,
                                   void* stream) {
   PDG_CHECK_ARG(n_nodes > 0, "pdg_pq_scatter_bwd: n_nodes must be > 0");
+  PDG_CHECK_ARG(rowptr_dst && rowptr_src && perm_src && gz1m && gP && gQ, "pdg_pq_scatter_bwd: null argument");
+  PDG_CHECK_ARG(!e_is_sum || gz1e, "pdg_pq_scatter_bwd: e_is_sum needs the gC rows");
   PDG_CHECK_ARG(PDG_ALIGNED(gz1m) && (!gz1e || PDG_ALIGNED(gz1e)) && PDG_ALIGNED(gP) && PDG_ALIGNED(gQ),
                 "pdg_pq_scatter_bwd: misaligned pointer");
   long want = (n_nodes + 7) / 8;

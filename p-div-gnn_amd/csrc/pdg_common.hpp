@@ -38,9 +38,6 @@ constexpr int WBLK = 128 * WPAD;        // floats per weight block in LDS (69,63
 #define PDG_EDGE_WAVES 12
 #endif
 constexpr int EDGE_WAVES = PDG_EDGE_WAVES;
-#ifndef PDG_EDGE_X6
-#define PDG_EDGE_X6 1   // edge kernels: W2 GEMMs as bf16x6 (0: fp32 MFMA, padded LDS images)
-#endif  // waves per block of the fused edge kernels (one block per CU)
 constexpr float LN_EPS = 1e-5f;         // torch_geometric LayerNorm default eps
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -68,12 +65,8 @@ __device__ __forceinline__ int opaque(int x) {
 // dst-sorted and mesh-local, so the P/Q rows one XCD gathers for its range stay
 // in that XCD's L2.  Speed only: any order is correct.
 __device__ __forceinline__ int xcd_block() {
-#ifdef PDG_NO_XCD_REMAP
-  return blockIdx.x;
-#else
   const int g = gridDim.x, b = blockIdx.x;
   return (g & 7) ? b : (b & 7) * (g >> 3) + (b >> 3);
-#endif
 }
 
 // Persistent wave-tile loop over tiles_of(M) tiles of 16 rows.
@@ -92,28 +85,14 @@ __device__ __forceinline__ f32x4 ld4(const float* __restrict__ p, int T) {
 // Row stores are nontemporal (streamed past the caches' normal allocation): measured -0.08 ms per
 // config-2 step, all from pdg_segment_sum re-reading the edge forward's a2m rows; nontemporal
 // LOADS of whole rows made pdg_edge_fwd 4 % slower and are off.
-#ifndef PDG_NT_ST
-#define PDG_NT_ST 1
-#endif
 __device__ __forceinline__ void st4(float* __restrict__ p, int T, const f32x4& x) {
-#if PDG_NT_ST
   __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p + 16 * T));
-#else
-  *reinterpret_cast<f32x4*>(p + 16 * T) = x;
-#endif
 }
-// A 16-byte row store outside the fragment helpers (nontemporal with PDG_NT_ROWS: measured +0.2 ms
+// A 16-byte row store outside the fragment helpers (nontemporal: measured +0.2 ms
 // per config-2 step, the P / Q rows the edge forward gathers and the gaggr rows the edge backward
-// gathers then miss the caches; off).
-#ifndef PDG_NT_ROWS
-#define PDG_NT_ROWS 0
-#endif
+// gathers then miss the caches; plain stores).
 __device__ __forceinline__ void stg4(float* __restrict__ p, const f32x4& x) {
-#if PDG_NT_ROWS
-  __builtin_nontemporal_store(x, reinterpret_cast<f32x4*>(p));
-#else
   *reinterpret_cast<f32x4*>(p) = x;
-#endif
 }
 // A 16-byte load through a global-address-space pointer: for row pointers the compiler cannot
 // place (read from an LDS table), which it would otherwise load with FLAT instructions; those
@@ -155,16 +134,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(float* base, int r0,
 __device__ __forceinline__ void rows_store4(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, 0);
 }
-// The same, nontemporal (aux nt: the policy of stnt4 / PDG_NT_ST).
+// The same, nontemporal (aux nt: the policy of stnt4).
 __device__ __forceinline__ void rows_store4_nt(__amdgpu_buffer_rsrc_t rs, int r, int c, const f32x4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, PDG_NT_ST ? 2 : 0);
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, (r * L + c) * 4, 0, 2);
 }
 
-// A 16-byte row store with the fragment stores' policy (nontemporal with PDG_NT_ST).
+// A 16-byte row store with the fragment stores' policy (nontemporal).
 __device__ __forceinline__ void stnt4(float* __restrict__ p, const f32x4& x) { st4(p, 0, x); }
-// Feature index of fragment element s in lane quarter q.
-__device__ __forceinline__ int frag_feature(int s, int q) { return 16 * (s >> 2) + 4 * q + (s & 3); }
-
 // x / den as the reference computes it (models.py LayerNorm: out = x / (std + eps)),
 // via the reciprocal and one Newton correction: 3 instructions instead of the
 // ~10-instruction IEEE division sequence, within 1 ulp of the quotient.
@@ -218,12 +194,6 @@ __device__ __forceinline__ f32x4 featvec_chunk(const FeatVec& fv, int T) {
   for (int j = 0; j < 4; ++j) r[j] = __int_as_float(__builtin_amdgcn_ds_bpermute(addr + 4 * j, src));
   return r;
 }
-// acc = per-feature bias (the accumulator is then the bias plus the GEMM).
-__device__ __forceinline__ void bias_acc(Acc& acc, const FeatVec& b) {
-#pragma unroll
-  for (int ob = 0; ob < 8; ++ob) acc.b[ob] = featvec_chunk(b, ob);
-}
-
 // acc += W * v over K = 128: 8 input groups t x 4 output-block pairs x 8 MFMAs
 // (256 MFMAs).  The A fragments of the next (t, pair) are read from LDS while
 // the current pair's 8 MFMAs issue; the two accumulators of a pair alternate so
@@ -417,11 +387,7 @@ __device__ __forceinline__ void load_frag(float (&v)[FRAG], const float* __restr
   const float* p = row + lane_col();
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
-#if PDG_NT_LD
-    const f32x4 x = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 16 * t));
-#else
     const f32x4 x = ld4(p, t);
-#endif
     v[4 * t + 0] = x[0]; v[4 * t + 1] = x[1]; v[4 * t + 2] = x[2]; v[4 * t + 3] = x[3];
   }
 }

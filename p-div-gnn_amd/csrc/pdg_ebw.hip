@@ -38,15 +38,9 @@ constexpr int EBW_IMG = 3 * X6_TERM;        // one bf16x6 image of 32 rows (24 K
 // from 16 rows at a time, which a 128-B stride put on 2 of the 32 banks of a ds_read_b32 lane
 // group (16-way conflicts); 136 B (34 words) spreads them over all 32.  The staging writes (32
 // consecutive words of a row per lane group) stay conflict free.
-#ifndef PDG_EFWD_X6F   // 1: the edge forward's W2 products in gemm_x6f's unbiased form (A/B only)
-#define PDG_EFWD_X6F 0
-#endif
 // the cooperative edge forward's C = Wc e as an unbiased bf16x6 product (gemm_x6f, the lo terms of Wc's
 // K chunks 0-1 in LDS) instead of fp32 MFMAs (0: A/B only).  Round 5: edge_fwd 211.4-212.9 -> 205.3-206.3 us
 // per config-2 call, the step -0.07 ms in two same-box pairs; every parity gate green (EXPERIMENTS §4).
-#ifndef PDG_EFWD_CX6
-#define PDG_EFWD_CX6 1
-#endif
 #ifndef PDG_MSK_STRIDE
 #define PDG_MSK_STRIDE 136
 #endif
@@ -198,9 +192,6 @@ __device__ __forceinline__ void row_schedule(bool xi, int M, int& r0, int& r1, i
 // XCD-interleaved units in the edge backward kernels (pdg_edge_bwd_w2, pdg_edge_gout_wc; the grid of
 // XCD_GRID blocks).  Off: 195-198 vs 195-198 us per edge_bwd_w2 call (no gather whose reuse it could
 // help: gaggr[dst] is read in dst order), and the slab sums change order.
-#ifndef PDG_EBW_XCD
-#define PDG_EBW_XCD 0
-#endif
 
 // slab += acc (the block's own slab, fixed block -> slab map) and the bias sums:
 // thread (cg, rg) holds column sums of columns 4cg .. 4cg+3 over its rows; reduced over
@@ -270,7 +261,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;    // the thread's staged row: rg (0..15)
   const int oc = 16 * w + 4 * (l >> 4);
   int r0, r1, first, stride;   // 32-row units: rounds base and base + 16, the next unit stride rows on
-  row_schedule(PDG_EBW_XCD, E, r0, r1, first, stride);
+  row_schedule(0, E, r0, r1, first, stride);
   WSlice ws;
   const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
   const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
@@ -424,7 +415,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
   int r0, r1, first, stride;
-  row_schedule(PDG_EBW_XCD, E, r0, r1, first, stride);
+  row_schedule(0, E, r0, r1, first, stride);
   WSlice ws;
   f32x16 acc[2];
 #pragma unroll
@@ -524,593 +515,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
   }
 }
 
-// ============================================================================ fused edge backward
-// pdg_edge_bwd_fused: pdg_edge_bwd_w2 + pdg_edge_gout_wc in one pass over the edge rows, as a weight-
-// specialised block.  The split pair re-read gC and ge_next from HBM in
-// the Wc pass (13 E-row passes per call); here the Wc work takes gC from an LDS image the W2 work just
-// wrote, and ge_next from an LDS tile the W2 work's staging filled: 11 passes (reads gaggr[dst], a2m, a1m,
-// ge_next, a2e, a1e, e, a2ln; writes gz1m, gC, ge_out).
-//
-// No wave holds both 128x128 weights: waves 0-3 (group A) own W2^T output features 32 wl + [0, 32) (hi /
-// mid bf16 terms in registers, the lo term in LDS) and the dW2 slab rows 32 wl + [0, 32); waves 4-7
-// (group B) own Wc^T and dWc likewise (all three terms in registers) and the column sums of the
-// LayerNorm that produced e.  Per 16-row round k, two barriers:
-//   phase 1  A: dW2 += gz2m^T a1m + gz2e^T a1e; gz1 = (W2^T gz2) [a1 > 0]; gC = gz1m + gz1e -> HBM and
-//               the gC image                                  (4 product units)
-//            B: stage round k's e image and xhat(a2ln) tile; issue round k+1's e / a2ln loads
-//   phase 2  B: dWc += gC^T e; ge_out = ge_next + Wc^T gC -> HBM; LayerNorm column sums   (2 units)
-//            A: stage round k+1 (gz2 = LN_bwd(gy) [a2 > 0], a1 images, masks, ge_next tile); issue
-//               round k+2's loads
-// so each SIMD runs one wave of each group, the matrix work of one overlapping the other's staging.
-// Per-element MFMA order as in the split pair: gz1m / gC / ge_out and the dW2 / dWc weight sums are
-// bitwise theirs; the bias and LayerNorm column sums add in another order.
-namespace {
-
-constexpr int EBF_LO = 4 * 4 * 2 * 64 * 16;   // lo terms of one weight's four wave slices in LDS (32 KB)
-// LDS: A images + masks, the gC and e images, the ge_next tiles (2) and the xhat tile, the W2^T lo terms
-constexpr int EBF_SHM = 4 * IMG16 + 2 * MSK16 + 2 * IMG16 + 2 * R16 * OT_STRIDE * 4 + 2 * EBF_LO;   // 156.75 KB
-
-// dW += G^T X over one 16-row image pair for a 4-wave group: wave wl owns o in 32 wl + [0, 32) and all
-// 128 i as four 32x32 accumulators (wgrad_round's operand reads and per-accumulator MFMA order).
-__device__ __forceinline__ void wgrad_round_g4(f32x16 (&acc)[4], const unsigned char* gimg, const unsigned char* ximg,
-                                               int wl) {
-  const int l = lane_id(), h = l >> 5;
-  const int lrow = 8 * h + ((l & 15) >> 2);
-  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
-  bf16x8 A[3];
-  const int g0 = x6_addr(lrow, lcolb + 64 * wl), g1 = x6_addr(lrow + 4, lcolb + 64 * wl);
-#pragma unroll
-  for (int p = 0; p < 3; ++p) A[p] = x6_operand(gimg + p * T16, g0, g1);
-#pragma unroll
-  for (int b = 0; b < 4; ++b) {
-    bf16x8 B[3];
-    const int x0 = x6_addr(lrow, lcolb + 64 * b), x1 = x6_addr(lrow + 4, lcolb + 64 * b);
-#pragma unroll
-    for (int p = 0; p < 3; ++p) B[p] = x6_operand(ximg + p * T16, x0, x1);
-    f32x16 t = acc[b];
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[2], B[0], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[1], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[2], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[1], B[0], t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[1], t, 0, 0, 0);
-    acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[0], B[0], t, 0, 0, 0);
-  }
-}
-
-// Two 16-feature W^T slices (output blocks 2 wl, 2 wl + 1); lo terms either in `a[..][2]` or in LDS.
-struct WSlice2 {
-  bf16x8 a[2][4][3];
-};
-
-// d[u][b] = W^T block (2 wl + b) x image u (16 rows): gemm_round<NI, 1, T16>'s chain per output block.
-// LO: the lo-term A operands come from LDS (lo + ((ks * 2 + b) * 64 + lane) * 16), not from ws.
-template <int NI, bool LO>
-__device__ __forceinline__ void gemm_round_g4(f32x4 (&d)[NI][2], const WSlice2& ws, const unsigned char* lo,
-                                              const unsigned char* const (&img)[NI]) {
-  const int l = lane_id(), n = l & 15, kg = l >> 4;
-#pragma unroll
-  for (int u = 0; u < NI; ++u)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) d[u][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    bf16x8 wl2[2];
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-      wl2[b] = LO ? *reinterpret_cast<const bf16x8*>(lo + ((ks * 2 + b) * 64 + l) * 16) : ws.a[b][ks][2];
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      const int off = x6_addr(n, 64 * ks + 16 * kg);
-      bf16x8 B[3];
-#pragma unroll
-      for (int p = 0; p < 3; ++p) B[p] = *reinterpret_cast<const bf16x8*>(img[u] + p * T16 + off);
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        f32x4 t = d[u][b];
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl2[b], B[0], t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][1], B[1], t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][0], B[2], t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][1], B[0], t, 0, 0, 0);
-        t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][0], B[1], t, 0, 0, 0);
-        d[u][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws.a[b][ks][0], B[0], t, 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);   // one image operand live at a time (register bound)
-    }
-  }
-}
-
-// The two slices of output blocks 2 wl, 2 wl + 1 of W^T (row-major, out x in); with LO the lo terms go
-// to this wave's part of the LDS array instead (read back by gemm_round_g4<.., true>).
-template <bool LO>
-__device__ __forceinline__ void load_wslice2(WSlice2& ws, const float* __restrict__ WT, int wl, unsigned char* lo) {
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    WSlice s;
-    load_wslice(s, WT, 2 * wl + b);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      ws.a[b][ks][0] = s.a[ks][0];
-      ws.a[b][ks][1] = s.a[ks][1];
-      if (LO)
-        *reinterpret_cast<bf16x8*>(lo + ((ks * 2 + b) * 64 + lane_id()) * 16) = s.a[ks][2];
-      else
-        ws.a[b][ks][2] = s.a[ks][2];
-    }
-  }
-}
-
-// slab rows 32 wl + [0, 32), all 128 columns, += acc (init: =) — slab_accumulate's element map for a
-// 4-wave group (ib = 0, four column blocks); every load before any store.
-__device__ __forceinline__ void slab_accumulate_g4(float* __restrict__ slab, const f32x16 (&acc)[4], int wl, int init) {
-  const int l = lane_id(), h = l >> 5, c = l & 31;
-  const int ob = 32 * wl;
-  float old[4][16];
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h, i = 32 * b + c;
-      old[b][r] = init ? 0.f : slab[o * L + i];
-    }
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int o = ob + (r & 3) + 8 * (r >> 2) + 4 * h, i = 32 * b + c;
-      slab[o * L + i] = old[b][r] + acc[b][r];
-    }
-}
-
-}  // namespace
-
-// LDS map of the fused kernel (EBF_SHM): A images gz2m, a1m, gz2e, a1e (16-row bf16x6), the masks, the gC
-// and e images, the ge_next tiles (by round parity), the lo terms of W2^T (group A) and Wc^T (group B)
-struct EbfLds {
-  unsigned char *img_gm, *img_am, *img_ge, *img_ae, *msk_m, *msk_e, *img_c, *img_e;
-  float* t_gn;
-  unsigned char *lo_a, *lo_b;
-  __device__ explicit EbfLds(unsigned char* sm) {
-    img_gm = sm;
-    img_am = sm + IMG16;
-    img_ge = sm + 2 * IMG16;
-    img_ae = sm + 3 * IMG16;
-    msk_m = sm + 4 * IMG16;
-    msk_e = msk_m + MSK16;
-    img_c = msk_e + MSK16;
-    img_e = img_c + IMG16;
-    t_gn = reinterpret_cast<float*>(img_e + IMG16);
-    lo_a = reinterpret_cast<unsigned char*>(t_gn + 2 * R16 * OT_STRIDE);
-    lo_b = lo_a + EBF_LO;
-  }
-};
-
-// Reduce-scatter of per-lane values over the lanes that differ in the lane-index bits of MASKS (a
-// butterfly; each step sends half of the values still held to the partner and keeps the other half):
-// afterwards v[0 .. N >> steps) of a lane hold the sums of the entries whose index's high bits equal the
-// lane's bits, in order (step s keeps the upper half where the lane's s-th mask bit is set).
-template <int N, int M, int SZ>
-__device__ __forceinline__ void rs_step(float (&v)[SZ], int l) {
-  static_assert(N <= SZ, "rs_step: more entries than the array holds");
-  const bool up = (l & M) != 0;
-#pragma unroll
-  for (int i = 0; i < N / 2; ++i) {
-    const float keep = up ? v[i + N / 2] : v[i], send = up ? v[i] : v[i + N / 2];
-    v[i] = keep + __shfl_xor(send, M);
-  }
-}
-
-// Group A (waves 0-3): the message branch and the W2 side.  Its own function, so that none of its values
-// is live in group B's code (one body holding both groups' loops made the register allocation the union of
-// both).  Stages gz2m = LN_bwd(gaggr[dst]) [a2m > 0], a1m and its mask; in phase 1 the dW2 and W2^T
-// products for both branches.
-template <bool EU>
-__device__ __forceinline__ void ebf_group_a(
-    const EbfLds& S, int r0, int r1, int nr, const int* __restrict__ dst, const float* __restrict__ gaggr,
-    const float* __restrict__ a2m, const float* __restrict__ a1m, const pdg_ln_stat* __restrict__ stm_p,
-    const pdg_ln_bwd* __restrict__ lbm_p, const float* __restrict__ lg, const float* __restrict__ W2T,
-    float* __restrict__ gz1m, float* __restrict__ gC, float* __restrict__ slab, const double* __restrict__ pm, int npm,
-    int slab_init, float* red_b2, float* red_b1) {
-  const int l = lane_id(), wl = wave_id() & 3;
-  const int srow = (threadIdx.x & 255) >> 4, sc = threadIdx.x & 15;   // staged row, columns 8 sc .. +7
-  unsigned char* lo = S.lo_a + wl * (EBF_LO / 4);
-  const LNStat stm = *reinterpret_cast<const LNStat*>(stm_p);
-  WSlice2 ws;
-  f32x16 acc[4];
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-  f32x4 pg[2], pa2[2], pa1[2];   // one prefetched round
-  int dn;
-  // bias sums, reduce-scattered every round: db2 part of features 8 sc + 4 bit5(l) + 2 bit4(l) + {0, 1}
-  // over this wave's 4 staged rows (the split pair's message + edge-update gz2 rows; B adds gz2e's); db1
-  // entry (l & 15) >> 1 of the product layout's 8 (block b = idx >> 2, feature 4 (l >> 4) + (idx & 3))
-  float b2s[2] = {0.f, 0.f}, b1s = 0.f;
-  const __amdgpu_buffer_rsrc_t out_m = rows_rsrc(gz1m, r0, r1);
-  const __amdgpu_buffer_rsrc_t out_c = rows_rsrc(EU || gC != gz1m ? gC : nullptr, r0, r1);
-  auto issue = [&](int base) {
-    const size_t rc = (size_t)clamp_row(base + srow, r1) * L + 8 * sc;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      pg[h] = *reinterpret_cast<const f32x4*>(gaggr + (size_t)dn * L + 8 * sc + 4 * h);
-      pa2[h] = *reinterpret_cast<const f32x4*>(a2m + rc + 4 * h);
-      pa1[h] = *reinterpret_cast<const f32x4*>(a1m + rc + 4 * h);
-    }
-  };
-  // the round at `base` from the prefetch set; rows past r1 get gz2 = 0, which zeroes every product they enter
-  auto stage = [&](int base, const pdg_ln_bwd& lbm) {
-    const bool ok = base + srow < r1;
-    float v[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cg = 2 * sc + h;
-      const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
-      const f32x4 zm = ok ? ln_relu_bwd4(pg[h], pa2[h], stm, lbm, g4) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[4 * h + j] = zm[j];
-      img_store4<T16>(S.img_gm, srow, cg, zm);
-      img_store4<T16>(S.img_am, srow, cg, pa1[h]);
-      *reinterpret_cast<unsigned*>(S.msk_m + srow * MSK_STRIDE + 4 * cg) = relu_mask4(pa1[h]);
-    }
-    rs_step<8, 32>(v, l);
-    rs_step<4, 16>(v, l);
-    b2s[0] += v[0];
-    b2s[1] += v[1];
-  };
-  dn = dst[clamp_row(r0 + srow, r1)];   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
-  issue(r0);
-  dn = dst[clamp_row(r0 + R16 + srow, r1)];
-  load_wslice2<true>(ws, W2T, wl, lo);
-  const pdg_ln_bwd lbm = lnb_resolve(lbm_p, pm, npm, stm_p);
-  stage(r0, lbm);
-  issue(r0 + R16);
-  dn = dst[clamp_row(r0 + 2 * R16 + srow, r1)];
-  __syncthreads();   // round 0's images (B stages the edge-update ones) complete
-  for (int k = 0; k < nr; ++k) {
-    const int base = r0 + k * R16, r = l & 15, row = base + r;
-    // ---- phase 1: dW2, the W2^T products, gz1m / gC to HBM and gC into the image
-    wgrad_round_g4(acc, S.img_gm, S.img_am, wl);
-    if (EU) wgrad_round_g4(acc, S.img_ge, S.img_ae, wl);
-    constexpr int NI = EU ? 2 : 1;
-    f32x4 d[NI][2];
-    const unsigned char* imgs[NI];
-    imgs[0] = S.img_gm;
-    if (EU) imgs[NI - 1] = S.img_ge;
-    gemm_round_g4<NI, true>(d, ws, lo, imgs);
-    float v[8];
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int oc = 32 * wl + 16 * b + 4 * (l >> 4);
-      const unsigned mm = *reinterpret_cast<const unsigned*>(S.msk_m + r * MSK_STRIDE + oc);
-      f32x4 zm;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) zm[j] = (mm >> (8 * j)) & 1u ? d[0][b][j] : 0.f;
-      f32x4 c = zm;
-      if (EU) {
-        const unsigned me = *reinterpret_cast<const unsigned*>(S.msk_e + r * MSK_STRIDE + oc);
-        f32x4 ze;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) ze[j] = (me >> (8 * j)) & 1u ? d[NI - 1][b][j] : 0.f;
-        c = zm + ze;
-      }
-      rows_store4(out_m, row - r0, oc, zm);
-      rows_store4(out_c, row - r0, oc, c);
-      img_store4<T16>(S.img_c, r, oc >> 2, c);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[4 * b + j] = c[j];   // rows past r1: c = 0 (their gz2 rows are zero)
-    }
-    rs_step<8, 8>(v, l);
-    rs_step<4, 4>(v, l);
-    rs_step<2, 2>(v, l);
-    b1s += v[0] + __shfl_xor(v[0], 1);
-    __syncthreads();   // gC image complete (B reads it in phase 2); the A images are read
-    // ---- phase 2: the next round's message images (its rows have had phase 1 to land), the round after's loads
-    if (k + 1 < nr) {
-      stage(base + R16, lbm);
-      issue(base + 2 * R16);
-      dn = dst[clamp_row(base + 3 * R16 + srow, r1)];
-    }
-    __syncthreads();   // the next round's images complete
-  }
-  slab_accumulate_g4(slab, acc, wl, slab_init);
-  // db2 parts: [wave][128] (B adds its own rows below: [4 + wave]); db1: one entry per feature
-  red_b2[wl * L + 8 * sc + 4 * ((l >> 5) & 1) + 2 * ((l >> 4) & 1)] = b2s[0];
-  red_b2[wl * L + 8 * sc + 4 * ((l >> 5) & 1) + 2 * ((l >> 4) & 1) + 1] = b2s[1];
-  if ((l & 1) == 0) {
-    const int idx = (l & 15) >> 1;
-    red_b1[32 * wl + 16 * (idx >> 2) + 4 * (l >> 4) + (idx & 3)] = b1s;
-  }
-}
-
-// Group B (waves 4-7): the edge-update branch and the Wc side.  Stages gz2e = LN_bwd(ge_next) [a2e > 0],
-// a1e and its mask, the ge_next tile and the e image; in phase 2 dWc, Wc^T gC, ge_out = ge_next + Wc^T gC
-// and the column sums of the LayerNorm that produced e (its input a2ln read in the product layout, xhat
-// formed per element; the sums reduce-scattered over the 16 row lanes every round, fp64 across rounds).
-template <bool EU>
-__device__ __forceinline__ void ebf_group_b(
-    const EbfLds& S, int r0, int r1, int nr, const float* __restrict__ ge_next, const float* __restrict__ a2e,
-    const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ ste_p, const pdg_ln_bwd* __restrict__ lbe_p,
-    const float* __restrict__ lg, const double* __restrict__ pe, int npe, const float* __restrict__ WcT,
-    const float* __restrict__ e, const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p,
-    float* __restrict__ ge_out, float* __restrict__ slab, int slab_init, float* red_b2, double* ln_row) {
-  const int l = lane_id(), wl = wave_id() & 3;
-  const int srow = (threadIdx.x & 255) >> 4, sc = threadIdx.x & 15;
-  unsigned char* lo = S.lo_b + wl * (EBF_LO / 4);
-  const LNStat stln = *reinterpret_cast<const LNStat*>(stln_p);
-  WSlice2 ws;
-  f32x16 acc[4];
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-  f32x4 pge[2], pa2e[2], pa1e[2], pe_[2], pl[2];
-  float b2s[2] = {0.f, 0.f};   // gz2e's db2 part (as group A's)
-  double cs = 0.0;             // LayerNorm column sum entry (l & 15) of this lane's 16: see below
-  const __amdgpu_buffer_rsrc_t out_g = rows_rsrc(ge_out, r0, r1);
-  auto issue_u = [&](int base) {   // the edge-update rows (whole rows, staged for A's next round)
-    const size_t rc = (size_t)clamp_row(base + srow, r1) * L + 8 * sc;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      pge[h] = *reinterpret_cast<const f32x4*>(ge_next + rc + 4 * h);
-      pa2e[h] = *reinterpret_cast<const f32x4*>(a2e + rc + 4 * h);
-      pa1e[h] = *reinterpret_cast<const f32x4*>(a1e + rc + 4 * h);
-    }
-  };
-  auto issue_e = [&](int base) {   // e (whole rows, for the image) and a2ln (this lane's product-layout rows)
-    const size_t rc = (size_t)clamp_row(base + srow, r1) * L + 8 * sc;
-    const size_t rp = (size_t)clamp_row(base + (l & 15), r1) * L + 32 * wl + 4 * (l >> 4);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      pe_[h] = *reinterpret_cast<const f32x4*>(e + rc + 4 * h);
-      pl[h] = *reinterpret_cast<const f32x4*>(a2ln + rp + 16 * h);
-    }
-  };
-  auto stage_u = [&](int base, int par, const LNStat& ste, const pdg_ln_bwd& lbe) {
-    const bool ok = base + srow < r1;
-    float v[8];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int cg = 2 * sc + h;
-      const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
-      const f32x4 ze = ok ? ln_relu_bwd4(pge[h], pa2e[h], ste, lbe, g4) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) v[4 * h + j] = ze[j];
-      img_store4<T16>(S.img_ge, srow, cg, ze);
-      img_store4<T16>(S.img_ae, srow, cg, pa1e[h]);
-      *reinterpret_cast<unsigned*>(S.msk_e + srow * MSK_STRIDE + 4 * cg) = relu_mask4(pa1e[h]);
-      *reinterpret_cast<f32x4*>(S.t_gn + (par * R16 + srow) * OT_STRIDE + 4 * cg) = pge[h];
-    }
-    rs_step<8, 32>(v, l);
-    rs_step<4, 16>(v, l);
-    b2s[0] += v[0];
-    b2s[1] += v[1];
-  };
-  const LNStat ste = EU ? *reinterpret_cast<const LNStat*>(ste_p) : stln;
-  pdg_ln_bwd lbe;
-  if (EU) issue_u(r0);
-  issue_e(r0);
-  load_wslice2<true>(ws, WcT, wl, lo);
-  if (EU) {
-    lbe = lnb_resolve(lbe_p, pe, npe, ste_p);
-    stage_u(r0, 0, ste, lbe);
-    issue_u(r0 + R16);
-  }
-  __syncthreads();   // round 0's images complete
-  for (int k = 0; k < nr; ++k) {
-    const int base = r0 + k * R16, r = l & 15, row = base + r;
-    // ---- phase 1: this round's e image (rows past r1 zero, as the split Wc pass)
-    {
-      const bool ok = base + srow < r1;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        img_store4<T16>(S.img_e, srow, 2 * sc + h, ok ? pe_[h] : f32x4{0.f, 0.f, 0.f, 0.f});
-    }
-    __syncthreads();   // gC and e images complete; A's edge-update images and masks are read
-    // ---- phase 2: dWc, Wc^T gC, ge_out = ge_next + Wc^T gC, LayerNorm column sums
-    wgrad_round_g4(acc, S.img_c, S.img_e, wl);
-    f32x4 d[1][2];
-    const unsigned char* imgs[1] = {S.img_c};
-    gemm_round_g4<1, true>(d, ws, lo, imgs);
-    const bool ok = row < r1;
-    float v[16];   // entry 8 b + 2 j + {0: go, 1: go xhat}
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int oc = 32 * wl + 16 * b + 4 * (l >> 4);
-      f32x4 go = d[0][b];
-      if (EU) go = *reinterpret_cast<const f32x4*>(S.t_gn + ((k & 1) * R16 + r) * OT_STRIDE + oc) + d[0][b];
-      rows_store4(out_g, row - r0, oc, go);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float xv = div_den(pl[b][j] - stln.mean, stln.den, stln.rstd);
-        v[8 * b + 2 * j] = ok ? go[j] : 0.f;
-        v[8 * b + 2 * j + 1] = ok ? go[j] * xv : 0.f;
-      }
-    }
-    rs_step<16, 8>(v, l);
-    rs_step<8, 4>(v, l);
-    rs_step<4, 2>(v, l);
-    rs_step<2, 1>(v, l);
-    cs += (double)v[0];
-    // the next rounds' rows: e / a2ln now; the edge-update images of A's next round, their loads two ahead
-    issue_e(base + R16);
-    if (EU && k + 1 < nr) {
-      stage_u(base + R16, (k + 1) & 1, ste, lbe);
-      issue_u(base + 2 * R16);
-    }
-    __syncthreads();   // A's next images complete; gC / e images and the ge_next tile are read
-  }
-  slab_accumulate_g4(slab, acc, wl, slab_init);
-  red_b2[(4 + wl) * L + 8 * sc + 4 * ((l >> 5) & 1) + 2 * ((l >> 4) & 1)] = b2s[0];
-  red_b2[(4 + wl) * L + 8 * sc + 4 * ((l >> 5) & 1) + 2 * ((l >> 4) & 1) + 1] = b2s[1];
-  {   // lane entry (l & 15) = 8 b + 2 j + gx of feature 32 wl + 16 b + 4 (l >> 4) + j
-    const int idx = l & 15, b = idx >> 3, j = (idx >> 1) & 3, gx = idx & 1;
-    ln_row[gx * L + 32 * wl + 16 * b + 4 * (l >> 4) + j] = cs;
-  }
-}
-
-template <bool EU>
-__global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_fused_kernel(
-    const int* __restrict__ dst, const float* __restrict__ gaggr, const float* __restrict__ ge_next,
-    const float* __restrict__ a2m, const float* __restrict__ a1m, const float* __restrict__ a2e,
-    const float* __restrict__ a1e, const pdg_ln_stat* __restrict__ stm_p, const pdg_ln_stat* __restrict__ ste_p,
-    const pdg_ln_bwd* __restrict__ lbm_p, const pdg_ln_bwd* __restrict__ lbe_p, const float* __restrict__ lg,
-    const float* __restrict__ W2T, const float* __restrict__ WcT, const float* __restrict__ e,
-    const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, const float* __restrict__ ln_g,
-    float* __restrict__ gz1m, float* __restrict__ gC, float* __restrict__ ge_out, float* __restrict__ slabs_w2,
-    float* __restrict__ slabs_wc, double* __restrict__ ln_part, double* __restrict__ ln_pairs, int E,
-    const double* __restrict__ pm, int npm, const double* __restrict__ pe, int npe, int slab_init, int accumulate) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  int r0, r1;
-  block_rows(E, r0, r1);
-  const int nr = (r1 - r0 + R16 - 1) / R16;
-  // end-of-kernel reduction space (the images are dead by then)
-  float* red_b2 = reinterpret_cast<float*>(sm);                 // [8 waves][128]: db2 parts
-  float* red_b1 = red_b2 + 8 * L;                               // [128]: db1
-  double* ln_row = reinterpret_cast<double*>(red_b1 + L);       // [256] column-sum row + lnb_emit's scratch [256]
-#ifndef PDG_EBF_ONLY   // register-pressure probe builds: 1 compiles only group A's code, 2 only B's
-#define PDG_EBF_ONLY 0
-#endif
-  const EbfLds S(sm);
-  if (PDG_EBF_ONLY != 2 && (PDG_EBF_ONLY == 1 || wave_id() < 4))
-    ebf_group_a<EU>(S, r0, r1, nr, dst, gaggr, a2m, a1m, stm_p, lbm_p, lg, W2T, gz1m, gC,
-                    slabs_w2 + (size_t)blockIdx.x * WSLAB, pm, npm, slab_init, red_b2, red_b1);
-  else if (PDG_EBF_ONLY != 1)
-    ebf_group_b<EU>(S, r0, r1, nr, ge_next, a2e, a1e, ste_p, lbe_p, lg, pe, npe, WcT, e, a2ln, stln_p, ge_out,
-                    slabs_wc + (size_t)blockIdx.x * WSLAB, slab_init, red_b2, ln_row);
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (t < L) {   // db2: the 8 waves' parts in order (message rows: waves 0-3, edge-update rows: 4-7)
-    float s = 0.f;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) s += red_b2[g * L + t];
-    float* bp = slabs_w2 + (size_t)blockIdx.x * WSLAB + L * L + t;
-    *bp = (slab_init ? 0.f : *bp) + s;
-  } else if (t < 2 * L) {   // db1
-    const int f = t - L;
-    float* bp = slabs_wc + (size_t)blockIdx.x * WSLAB + L * L + f;
-    *bp = (slab_init ? 0.f : *bp) + red_b1[f];
-  }
-  __syncthreads();
-  lnb_emit(ln_row, ln_g, ln_part, accumulate, ln_pairs, ln_row + 2 * L);
-}
-
-// ============================================================================ edge encoder backward
-// Backward of edge_encoder = Lin(1 -> 128) ReLU Lin(128 -> 128) ReLU LN (models.py:268-274) over the
-// E scalar inputs e_in, upstream gradient gy = d loss / d e_0 (ge_out of the first step):
-//   gz2 = LN_bwd(gy) [a2 > 0];   dW2 += gz2^T a1,  db2 += sum gz2   (slab, as edge_bwd_w2)
-//   gz1 = (W2^T gz2) [a1 > 0];   dw0 += sum gz1 e, db0 += sum gz1   (fp64 per block)
-// a1 = relu(w0 e + b0) is recomputed from the scalar input exactly as encoder_kernel forms it (so
-// the forward keeps no a1), and neither gz2 nor gz1 is written: this reads two E-row arrays where
-// pdg_mlp2_bwd + the ee2 weight-gradient pass + pdg_wgrad_narrow moved eight.
-__global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd_kernel(
-    const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ e_in,
-    const float* __restrict__ w0, const float* __restrict__ b0, const pdg_ln_stat* __restrict__ st_p,
-    const pdg_ln_bwd* __restrict__ lb_p, const double* __restrict__ pairs, int npairs,
-    const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ slabs,
-    double* __restrict__ nsums, int E, int slab_init) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  unsigned char* img_g = sm;                                   // gz2
-  unsigned char* img_a = sm + EBW_IMG;                         // a1
-  unsigned char* msk = sm + 2 * EBW_IMG;                       // [a1 > 0]
-  float* ev = reinterpret_cast<float*>(msk + EBW_MASK);        // the round's 32 inputs
-  const int l = lane_id(), w = wave_id();
-  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int oc = 16 * w + 4 * (l >> 4);
-  int r0, r1;
-  block_rows(E, r0, r1);
-  WSlice ws;
-  load_wslice(ws, W2T, w);
-  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
-  const f32x4 w04 = *reinterpret_cast<const f32x4*>(w0 + 4 * cg);
-  const f32x4 b04 = *reinterpret_cast<const f32x4*>(b0 + 4 * cg);
-  const LNStat st = *reinterpret_cast<const LNStat*>(st_p);
-  const pdg_ln_bwd lb = lnb_resolve(lb_p, pairs, npairs, st_p);
-  f32x16 acc[2];
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  double sw[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};   // narrow sums of features oc .. oc+3
-  f32x4 pg[2], pa2[2];
-  float pe[2];
-  auto issue = [&](int base) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int rc = clamp_row(base + rg + 16 * u, r1);
-      pg[u] = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + 4 * cg);
-      pa2[u] = *reinterpret_cast<const f32x4*>(a2 + (size_t)rc * L + 4 * cg);
-      pe[u] = e_in[rc];
-    }
-  };
-  // loads unconditional (clamped) and issued before the barrier; the first round's complete before
-  // the loop (pending at the loop head they set every stage's wait to vmcnt(0))
-  issue(r0);   // E > 0: an empty block (r0 = r1 = E) reads row E - 1
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    pin_vgpr(pg[u]);
-    pin_vgpr(pa2[u]);
-    pin_vgpr(pe[u]);
-  }
-  // the first round peeled off (unconditional: an empty block stages zero rows), so the loop is
-  // entered in its steady state
-  auto round = [&](const int base) {
-    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int r = rg + 16 * u;
-      const bool ok = base + r < r1;
-      const f32x4 zg = ok ? ln_relu_bwd4(pg[u], pa2[u], st, lb, g4) : zero;
-      bsum += zg;
-      img_store4(img_g, r, cg, zg);
-      f32x4 a;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] = fmaxf(fmaf(w04[j], pe[u], 0.f) + b04[j], 0.f);   // encoder_kernel's a1
-      a = ok ? a : zero;
-      img_store4(img_a, r, cg, a);
-      *reinterpret_cast<unsigned*>(msk + r * MSK_STRIDE + 4 * cg) = relu_mask4(a);
-      if (cg == 0) ev[r] = ok ? pe[u] : 0.f;
-    }
-    issue(base + X6_ROWS);
-    __syncthreads();
-    wgrad_round(acc, img_g, img_a);                        // dW2 += gz2^T a1
-    f32x4 d[1][2];
-    const unsigned char* imgs[1] = {img_g};
-    gemm_round<1>(d, ws, imgs);                            // W2^T gz2, features oc .. oc+3
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int r = 16 * nb + (l & 15);
-      const unsigned mm = *reinterpret_cast<const unsigned*>(msk + r * MSK_STRIDE + oc);
-      const double e = (double)ev[r];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float z = (mm >> (8 * j)) & 1u ? d[0][nb][j] : 0.f;
-        sw[j] += (double)z * e;
-        sb[j] += (double)z;
-      }
-    }
-    __syncthreads();   // the images are rewritten by the next round
-  };
-  round(r0);
-  for (int base = r0 + X6_ROWS; base < r1; base += X6_ROWS) round(base);
-  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
-  // the 16 lanes holding the same features (different rows): fixed xor butterfly
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      sw[j] += __shfl_xor(sw[j], off);
-      sb[j] += __shfl_xor(sb[j], off);
-    }
-  if ((l & 15) == 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      nsums[(size_t)blockIdx.x * 2 * L + oc + j] = sw[j];
-      nsums[(size_t)blockIdx.x * 2 * L + L + oc + j] = sb[j];
-    }
-  }
-}
-
+// ============================================================================ edge encoder narrow reduction
 // grad_w0 += sum over blocks of the dw0 sums, grad_b0 += the db0 sums.  Block c (of 2) owns columns
 // 128 c .. 128 c + 127; its 4 thread groups sum every 4th slab row with 4 loads in flight each, then
 // the 4 partial sums are added in group order (deterministic).
@@ -1150,20 +555,21 @@ __global__ __launch_bounds__(512) void enc_narrow_reduce_kernel(const double* __
 //   product  a2 = relu(W2 a1 + b2) -> LayerNorm partials, row tiles
 //   | barrier | a2 rows stored; the next round's stage
 // C = Wc e is an UNBIASED bf16x6 product (gemm_x6f from an e image; Wc as bf16 terms, the lo terms of
-// its first two K chunks in LDS), round 5.  Rounds 2-4 kept C an exact fp32 product (v_mfma_f32_16x16x4_f32,
-// still the -DPDG_EFWD_CX6=0 build): C in the BIASED bf16x6 chain had shifted the LayerNorm statistics the
+// its first two K chunks in LDS), round 5.  Rounds 2-4 kept C an exact fp32 product (v_mfma_f32_16x16x4_f32):
+// C in the BIASED bf16x6 chain had shifted the LayerNorm statistics the
 // way bf16x6 node_net did (parameter gradients 2e-4 from fp64 instead of 2.5e-6), a bias gemm_x6f does not
 // have (rms error 3.6x below the fp32 MFMA chain's).  The fp32 C was half of this kernel's matrix time.
 constexpr int EFC_TILE = X6_ROWS * OT_STRIDE;   // floats per fp32 row tile
 constexpr int EFC_ES = L + 8;                    // e tile row stride: the C operand reads are conflict free
 
 
-// D (deferred a2 stores): a2 goes into two tiles of its own
+// Deferred a2 stores: a2 goes into two tiles of its own
 // and its rows are stored after the NEXT round's first barrier, behind that round's gathers and row
 // loads, so a round has two barriers instead of four (the barrier that freed the a1 tiles for a2 and
 // the one that completed the a2 tiles go: the loop-top barrier completes both the e tile and the
 // previous round's a2 tiles), and the C product's wait for its gathers no longer covers the previous
-// round's a2 stores.  Bitwise the same outputs; 32 KB more LDS (131 KB).
+// round's a2 stores.  Bitwise the same outputs as storing each round's a2 at once; 32 KB more LDS (131 KB;
+// 216 -> 210.5 us per config-2 call with X, the step -0.05 ms, in two same-box A/B pairs, round 3).
 //
 // X (XCD-interleaved rounds): the blocks that share an XCD's L2 (b and b + 8; the grid
 // a multiple of 8) sweep one contiguous eighth of the rows together, taking its 32-row rounds
@@ -1171,7 +577,7 @@ constexpr int EFC_ES = L + 8;                    // e tile row stride: the C ope
 // reused by the edges of the mesh neighbours of its nodes, about +-13 rounds away in dst order: with
 // per-block ranges every block of an XCD keeps such a window live (32 x ~280 KB, over the 4 MiB L2, so
 // the reuse was served by the Infinity Cache), with interleaved rounds the XCD has one window.
-template <bool RES, bool EU, bool D = false, bool X = false>
+template <bool RES, bool EU, bool X = false>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
     const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
@@ -1185,14 +591,14 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   float* t_m = reinterpret_cast<float*>(sm + 2 * EBW_IMG);     // fp32 row tiles: a1m / a2m
   float* t_x = t_m + EFC_TILE;                                 //                 a1e / a2e
   float* t_e = t_x + EFC_TILE;                                 //                 e_t
-  // PDG_EFWD_CX6: e as a bf16x6 image in the tile's place (24 instead of 17 KB)
+  // e as a bf16x6 image (24 KB)
   unsigned char* img_e = reinterpret_cast<unsigned char*>(t_e);
-  constexpr int E_BYTES = PDG_EFWD_CX6 ? EBW_IMG : X6_ROWS * EFC_ES * 4;
-  float* t_am = reinterpret_cast<float*>(img_e + E_BYTES);     // D: a2m / a2e tiles
+  constexpr int E_BYTES = EBW_IMG;
+  float* t_am = reinterpret_cast<float*>(img_e + E_BYTES);     // deferred a2m / a2e tiles
   float* t_ae = t_am + EFC_TILE;
-  // PDG_EFWD_CX6: the lo bf16 terms of Wc's K chunks 0 and 1 in LDS, after every region (with all 12 terms
+  // the lo bf16 terms of Wc's K chunks 0 and 1 in LDS, after every region (with all 12 terms
   // in registers the main instantiation spilled 5 VGPRs and was no faster than fp32 MFMAs)
-  unsigned char* wlo = reinterpret_cast<unsigned char*>(t_am) + (D ? 2 * EFC_TILE * 4 : 0);
+  unsigned char* wlo = reinterpret_cast<unsigned char*>(t_am) + 2 * EFC_TILE * 4;
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
@@ -1202,11 +608,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   row_schedule(X, E, r0, r1, first, stride);
   // the weights as A operands, rows = output features 16w .. 16w + 15 (W is out x in, row-major):
   // Wc = W1[:, 256:384] (row stride 384), W2
-#if PDG_EFWD_CX6
   WSlice wsc;     // Wc as bf16 terms (gemm_x6f's A operand)
-#else
-  f32x4 wcf[8];   // Wc rows 16w + (l & 15), inputs 16T + 4(l >> 4) .. +3 (node_pq_rw's A fragments)
-#endif
   WSlice ws2;     // both loaded after the first round's row loads (the round trips overlap)
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
   const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg), bb4 = *reinterpret_cast<const f32x4*>(lb + 4 * cg);
@@ -1247,40 +649,23 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         e[j] = y;
       }
       rows_store4_nt(rs_e, base + r - r0, 4 * cg, e);
-#if PDG_EFWD_CX6
       img_store4(img_e, r, cg, ok ? e : f32x4{0.f, 0.f, 0.f, 0.f});
-#else
-      *reinterpret_cast<f32x4*>(t_e + r * EFC_ES + 4 * cg) = ok ? e : f32x4{0.f, 0.f, 0.f, 0.f};
-#endif
     }
   };
   issue(first);   // E > 0: an empty block (first = r1 = E) reads row E - 1
-#if PDG_EFWD_CX6
   load_wslice(wsc, W1 + 2 * L, w, 3 * L);
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) *reinterpret_cast<bf16x8*>(wlo + ((2 * w + ks) * 64 + l) * 16) = wsc.a[ks][2];
-#else
-  {
-    const float* pc = W1 + (size_t)(16 * w + (l & 15)) * (3 * L) + 2 * L + 4 * (l >> 4);
-#pragma unroll
-    for (int T = 0; T < 8; ++T) wcf[T] = *reinterpret_cast<const f32x4*>(pc + 16 * T);
-  }
-#endif
   load_wslice(ws2, W2, w);
   // the loop-invariant weights and biases are in registers before the loop (an empty asm using them
   // here): left to the compiler, their loads were sunk to the loop's preheader, still in flight at
   // the loop head, and the count merged there made every round's C product wait for the previous
   // round's stores (vmcnt 23 .. 16)
-#if PDG_EFWD_CX6
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
     for (int p = 0; p < 3; ++p)
       if (p < 2 || ks >= 2) pin_vgpr(wsc.a[ks][p]);
-#else
-#pragma unroll
-  for (int T = 0; T < 8; ++T) pin_vgpr(wcf[T]);
-#endif
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
@@ -1314,7 +699,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     __builtin_amdgcn_sched_barrier(0);
     issue(base + stride);   // clamped past r1: unconditional
     __builtin_amdgcn_sched_barrier(0);
-    if (D) {   // the previous round's a2 rows (tiles completed by the barrier above; none before the first
+    {   // the previous round's a2 rows (tiles completed by the barrier above; none before the first
                // round: base - stride lies below the range and its stores are dropped)
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
@@ -1325,7 +710,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
     }
     // ---- C = Wc e + b1 and the two first layers at this wave's 16 features
     f32x4 d[2];
-#if PDG_EFWD_CX6   // C = Wc e as an unbiased bf16x6 product (gemm_x6f), 2.7x less matrix time than fp32 MFMAs
     d[0] = d[1] = f32x4{0.f, 0.f, 0.f, 0.f};
     {
       WSlice wc = wsc;   // the lo terms of K chunks 0-1 from LDS
@@ -1333,20 +717,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       for (int ks = 0; ks < 2; ++ks) wc.a[ks][2] = *reinterpret_cast<const bf16x8*>(wlo + ((2 * w + ks) * 64 + l) * 16);
       gemm_x6f<2, X6_TERM, true>(d, wc, img_e);
     }
-#else
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {   // the MFMA order of gemm128: step (T, jj) sums inputs 16T + 4k + jj
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* er = t_e + (16 * nb + (l & 15)) * EFC_ES + 4 * (l >> 4);
-#pragma unroll
-      for (int T = 0; T < 8; ++T) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(er + 16 * T);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wcf[T][jj], bv[jj], acc, 0, 0, 0);
-      }
-      d[nb] = acc;
-    }
-#endif
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
       const int r = 16 * nb + (l & 15);
@@ -1372,23 +742,14 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
       if (EU) rows_store4_nt(rs_a1e, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
     }
     // ---- a2 = relu(W2 a1 + b2) for both evaluations
-    float* t_a2 = D ? t_am : t_m;
-    float* t_a2e = D ? t_ae : t_x;
+    float* t_a2 = t_am;
+    float* t_a2e = t_ae;
     constexpr int NI = EU ? 2 : 1;
     f32x4 d2[NI][2];
     const unsigned char* ia[NI];
     ia[0] = img_m;
     if (EU) ia[NI - 1] = img_x;
-#if PDG_EFWD_X6F   // A/B build (tools/grad_err_stages.py): the W2 products in gemm_x6f's unbiased form
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-      d2[u][0] = d2[u][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      gemm_x6f<2, X6_TERM, true>(d2[u], ws2, ia[u]);
-    }
-#else
     gemm_round<NI>(d2, ws2, ia);
-#endif
-    if (!D) __syncthreads();   // the a1 tiles are read; reuse them for a2
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
       const int r = 16 * nb + (l & 15);
@@ -1406,18 +767,9 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
         }
       }
     }
-    if (!D) {
-      __syncthreads();   // a2 tiles complete
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int r = rg + 16 * u;
-        rows_store4_nt(rs_a2m, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_a2 + r * OT_STRIDE + 4 * cg));
-        if (EU) rows_store4_nt(rs_a2e, base + r - r0, 4 * cg, *reinterpret_cast<const f32x4*>(t_x + r * OT_STRIDE + 4 * cg));
-      }
-    }
     stage(base + stride);   // past r1: stores dropped, the tile unused; the e tile was last read before the second barrier
   }
-  if (D) {   // the last round's a2 rows
+  {   // the last round's a2 rows
     __syncthreads();
     const int last = first < r1 ? first + (r1 - 1 - first) / stride * stride : first;
 #pragma unroll
@@ -1522,183 +874,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_fwd_kernel(
   };
   round(r0);
   for (int base = r0 + X6_ROWS; base < r1; base += X6_ROWS) round(base);
-  double* red = reinterpret_cast<double*>(sm);
-  __syncthreads();
-  block_sum2(s1, s2, red);
-  if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = s1;
-    part[2 * blockIdx.x + 1] = s2;
-  }
-}
-
-// ---------------------------------------------------------------------------- edge encoder forward by knots
-// The first layer has ONE scalar input, so a1 = relu(w0 e + b0) is piecewise linear in e with a kink at each
-// knot t_k = -b0[k] / w0[k]: between two consecutive knots the set of active features A is fixed and
-//   a2 = relu(W2 a1 + b2) = relu(e U_i + V_i),  U_i = sum_{k in A_i} W2[:, k] w0[k],  V_i = b2 + sum_{k in A_i} W2[:, k] b0[k]
-// (w0[k] = 0: feature k is active on every interval iff b0[k] > 0, contributing to V only).  The 129 interval
-// rows (U_i, V_i) are formed once per forward in fp64 and rounded once (edge_knots_kernel), so the per-edge
-// work is a binary search over the 128 sorted knots and one fma per output: no matrix product is left and the
-// kernel only streams a2 out.  An edge within an ulp of a knot may take the neighbouring interval; feature k
-// is then ~0 either way (|w0 e + b0| at the ulp level), so the output moves by that much only.
-// Table layout (EK_TAB floats): the sorted knots [128], then interval i's U [128] and V [128] at 128 + 256 i.
-constexpr int EK_KNOTS = 128;
-constexpr int EK_TAB = EK_KNOTS + (EK_KNOTS + 1) * 2 * L;   // 33,152 floats (132.6 KB)
-__global__ __launch_bounds__(EBW_THREADS) void edge_knots_kernel(const float* __restrict__ w0,
-                                                                  const float* __restrict__ b0,
-                                                                  const float* __restrict__ W2,
-                                                                  const float* __restrict__ b2,
-                                                                  float* __restrict__ tab) {
-  __shared__ float sw[L * (L + 1)];   // W2, row stride L + 1 (thread j reads row j: no bank conflicts)
-  __shared__ float tau[L], sw0[L], sb0[L];
-  __shared__ int rank[L];
-  __shared__ double red[4][2][L];
-  const int t = threadIdx.x, i = blockIdx.x;
-  {   // W2 into LDS: every load issued before the first store (one round trip)
-    f32x4 v[L * L / 4 / EBW_THREADS];
-#pragma unroll
-    for (int q = 0; q < L * L / 4 / EBW_THREADS; ++q)
-      v[q] = *reinterpret_cast<const f32x4*>(W2 + 4 * (t + q * EBW_THREADS));
-#pragma unroll
-    for (int q = 0; q < L * L / 4 / EBW_THREADS; ++q) {
-      const int x = 4 * (t + q * EBW_THREADS), row = x / L, col = x % L;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) sw[row * (L + 1) + col + c] = v[q][c];
-    }
-  }
-  float tk = 0.f;
-  if (t < L) {
-    const float wk = w0[t], bk = b0[t];
-    tk = wk != 0.f ? -bk / wk : __FLT_MAX__;   // w0 = 0: no kink (sorted last, never below an edge)
-    tau[t] = tk;
-    sw0[t] = wk;
-    sb0[t] = bk;
-  }
-  __syncthreads();
-  {   // rank of knot k: four quarter counts over 32 knots each
-    const int k = t & (L - 1), p = t >> 7;
-    const float tq = tau[k];
-    int r = 0;
-#pragma unroll
-    for (int q = 32 * p; q < 32 * p + 32; ++q) r += (tau[q] < tq || (tau[q] == tq && q < k)) ? 1 : 0;
-    reinterpret_cast<int*>(red)[t] = r;
-  }
-  __syncthreads();
-  if (t < L) {
-    const int* cnt = reinterpret_cast<const int*>(red);
-    const int r = cnt[t] + cnt[L + t] + cnt[2 * L + t] + cnt[3 * L + t];
-    rank[t] = r;
-    if (i == 0) tab[r] = tk;
-  }
-  __syncthreads();
-  // interval i: the edges with exactly i knots below them; output j, features [32 p, 32 p + 32)
-  const int j = t & (L - 1), p = t >> 7;
-  double u = 0., v = 0.;
-#pragma unroll
-  for (int q = 32 * p; q < 32 * p + 32; ++q) {
-    const float wq = sw0[q], bq = sb0[q];
-    const bool act = wq > 0.f ? rank[q] < i : (wq < 0.f ? rank[q] >= i : bq > 0.f);
-    const double a = act ? (double)sw[j * (L + 1) + q] : 0.;
-    u += a * (double)wq;
-    v += a * (double)bq;
-  }
-  red[p][0][j] = u;
-  red[p][1][j] = v;
-  __syncthreads();
-  if (t < L) {
-    const double uu = ((red[0][0][t] + red[1][0][t]) + red[2][0][t]) + red[3][0][t];
-    const double vv = (double)b2[t] + (((red[0][1][t] + red[1][1][t]) + red[2][1][t]) + red[3][1][t]);
-    tab[EK_KNOTS + 2 * L * i + t] = (float)uu;
-    tab[EK_KNOTS + 2 * L * i + L + t] = (float)vv;
-  }
-}
-
-// The edges' a2 rows from the knot table (in LDS): 32 threads per row, 4 features each, 16 rows per block pass.
-// The block's inputs come in chunks of EK_CH rows through LDS with each row's interval, searched once per row by
-// one lane: searched by all 32 lanes of the row in the write loop, the compiler serialised the rows' chains of
-// dependent LDS reads (30.5 us per config-2 call).  The LayerNorm partials as edge_enc_fwd_kernel.
-// Plain (not nontemporal) row stores: 27.3 -> 23.6 us per config-2 call, the step-0 edge forward that reads the
-// rows no slower (PDG_EK_NT=1: nontemporal, the policy of the other row stores)
-#ifndef PDG_EK_NT
-#define PDG_EK_NT 0
-#endif
-constexpr int EK_U = 4;
-constexpr int EK_CH = 2048;                              // rows per input chunk
-constexpr int EK_SHM = (EK_TAB + 2 * EK_CH) * 4;         // 148.6 KB
-__global__ __launch_bounds__(EBW_THREADS) void edge_enc_fwd_knots_kernel(int E, const float* __restrict__ e_in,
-                                                                           const float* __restrict__ tab,
-                                                                           float* __restrict__ a2,
-                                                                           double* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  float* st = reinterpret_cast<float*>(sm);
-  float* se = st + EK_TAB;
-  int* sp = reinterpret_cast<int*>(se + EK_CH);
-  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  int r0, r1;
-  block_rows(E, r0, r1);
-  constexpr int NE = EK_CH / EBW_THREADS;
-  float ve[NE];
-  auto load_chunk = [&](int c0) {   // clamped: E > 0 (an empty block reads row E - 1)
-#pragma unroll
-    for (int q = 0; q < NE; ++q) ve[q] = e_in[clamp_row(c0 + threadIdx.x + q * EBW_THREADS, r1)];
-  };
-  // the chunk's inputs and their intervals (knots below e: one branch-free search per row, by one lane)
-  auto store_chunk = [&]() {
-#pragma unroll
-    for (int q = 0; q < NE; ++q) {
-      const float e = ve[q];
-      int pos = 0;
-#pragma unroll
-      for (int h = EK_KNOTS / 2; h >= 1; h >>= 1) pos += st[pos + h - 1] < e ? h : 0;
-      pos += st[pos] < e ? 1 : 0;
-      se[threadIdx.x + q * EBW_THREADS] = e;
-      sp[threadIdx.x + q * EBW_THREADS] = pos;
-    }
-  };
-  load_chunk(r0);
-  {   // the table into LDS: every load issued before the first store (one L2 round trip, not 17)
-    constexpr int NV = (EK_TAB / 4 + EBW_THREADS - 1) / EBW_THREADS;
-    f32x4 v[NV];
-#pragma unroll
-    for (int q = 0; q < NV; ++q) {
-      const int x = 4 * (threadIdx.x + q * EBW_THREADS);
-      v[q] = *reinterpret_cast<const f32x4*>(tab + (x < EK_TAB ? x : 0));
-    }
-#pragma unroll
-    for (int q = 0; q < NV; ++q) {
-      const int x = 4 * (threadIdx.x + q * EBW_THREADS);
-      if (x < EK_TAB) *reinterpret_cast<f32x4*>(st + x) = v[q];
-    }
-  }
-  const __amdgpu_buffer_rsrc_t rs_a2 = rows_rsrc(a2, r0, r1);
-  double s1 = 0, s2 = 0;
-  __syncthreads();   // the table in LDS
-  for (int c0 = r0; c0 < r1; c0 += EK_CH) {
-    store_chunk();
-    __syncthreads();   // the chunk in LDS
-    if (c0 + EK_CH < r1) load_chunk(c0 + EK_CH);   // in flight while this chunk's rows are written
-    const int n = min(EK_CH, r1 - c0);
-    for (int b = 0; b < n; b += 16 * EK_U) {
-#pragma unroll
-      for (int u = 0; u < EK_U; ++u) {
-        const int rr = b + rg + 16 * u;
-        const float e = se[rr];
-        const int pos = sp[rr];
-        const f32x4 U = *reinterpret_cast<const f32x4*>(st + EK_KNOTS + 2 * L * pos + 4 * cg);
-        const f32x4 V = *reinterpret_cast<const f32x4*>(st + EK_KNOTS + 2 * L * pos + L + 4 * cg);
-        f32x4 a;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) a[q] = fmaxf(fmaf(e, U[q], V[q]), 0.f);
-        if (PDG_EK_NT)
-          rows_store4_nt(rs_a2, c0 - r0 + rr, 4 * cg, a);   // rows past r1 dropped
-        else
-          rows_store4(rs_a2, c0 - r0 + rr, 4 * cg, a);
-        const float k = rr < n ? 1.f : 0.f;   // branch-free: a branch here split the rows' code apart
-        s1 += (double)(k * ((a[0] + a[1]) + (a[2] + a[3])));
-        s2 += (double)(k * ((a[0] * a[0] + a[1] * a[1]) + (a[2] * a[2] + a[3] * a[3])));
-      }
-    }
-    __syncthreads();   // the chunk is read
-  }
   double* red = reinterpret_cast<double*>(sm);
   __syncthreads();
   block_sum2(s1, s2, red);
@@ -2216,146 +1391,6 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void node_bwd_coop_kernel(
   }
 }
 
-// Edge encoder backward, two-deep (default; edge_bwd_w2_kernel's form): 16-row rounds with two rounds
-// of row loads in flight in two register sets (round parity), double-buffered images / masks / inputs,
-// one barrier per round.  Every output is bitwise edge_enc_bwd_kernel's: the weight-gradient K steps,
-// the per-lane narrow sums and the per-thread bias sums visit the same rows in the same order.
-#ifndef PDG_EEB_2DEEP
-#define PDG_EEB_2DEEP 1
-#endif
-constexpr int EEB2_BUF = 2 * IMG16 + MSK16 + R16 * 4;   // one round's images, mask and inputs
-
-__global__ __launch_bounds__(EBW_THREADS, 1) void edge_enc_bwd2_kernel(
-    const float* __restrict__ gy, const float* __restrict__ a2, const float* __restrict__ e_in,
-    const float* __restrict__ w0, const float* __restrict__ b0, const pdg_ln_stat* __restrict__ st_p,
-    const pdg_ln_bwd* __restrict__ lb_p, const double* __restrict__ pairs, int npairs,
-    const float* __restrict__ lg, const float* __restrict__ W2T, float* __restrict__ slabs,
-    double* __restrict__ nsums, int E, int slab_init) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  const int l = lane_id(), w = wave_id();
-  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;    // the thread's staged row: rg (0..15)
-  const int oc = 16 * w + 4 * (l >> 4);
-  int r0, r1;
-  block_rows(E, r0, r1);
-  f32x16 acc[2];
-#pragma unroll
-  for (int b = 0; b < 2; ++b)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
-  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  double sw[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};   // narrow sums of features oc .. oc+3
-  f32x4 pg[2], pa2[2];
-  float pe[2];
-  auto issue = [&](const int s, int base) {   // clamped: E > 0 (an empty block reads row E - 1)
-    const int rc = clamp_row(base + rg, r1);
-    pg[s] = *reinterpret_cast<const f32x4*>(gy + (size_t)rc * L + 4 * cg);
-    pa2[s] = *reinterpret_cast<const f32x4*>(a2 + (size_t)rc * L + 4 * cg);
-    pe[s] = e_in[rc];
-  };
-  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg);
-  const f32x4 w04 = *reinterpret_cast<const f32x4*>(w0 + 4 * cg);
-  const f32x4 b04 = *reinterpret_cast<const f32x4*>(b0 + 4 * cg);
-  const LNStat st = *reinterpret_cast<const LNStat*>(st_p);
-  issue(0, r0);
-  __builtin_amdgcn_sched_barrier(0);
-  issue(1, r0 + R16);
-  __builtin_amdgcn_sched_barrier(0);
-  // the weights and the LayerNorm scalars after the first rounds' row loads: the round trips overlap
-  WSlice ws;
-  load_wslice(ws, W2T, w);
-  const pdg_ln_bwd lb = lnb_resolve(lb_p, pairs, npairs, st_p);
-  // the loop-invariant vectors in registers before the loop (pending at the loop head, their loads
-  // made the stage wait for every row load in flight)
-  pin_vgpr(g4);
-  pin_vgpr(w04);
-  pin_vgpr(b04);
-  auto stage = [&](const int s, const int base) {
-    unsigned char* img_g = sm + s * EEB2_BUF;                  // gz2
-    unsigned char* img_a = img_g + IMG16;                      // a1
-    unsigned char* msk = img_g + 2 * IMG16;                    // [a1 > 0]
-    float* ev = reinterpret_cast<float*>(msk + MSK16);         // the round's 16 inputs
-    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bool ok = base + rg < r1;
-    // computed for every row (a row past r1 is a clamped, finite row) and selected: a conditional
-    // call here became a branch, which splits the round into two scheduling regions
-    const f32x4 zr = ln_relu_bwd4(pg[s], pa2[s], st, lb, g4);
-    f32x4 zg;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) zg[j] = ok ? zr[j] : 0.f;
-    bsum += zg;
-    img_store4<T16>(img_g, rg, cg, zg);
-    f32x4 a;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) a[j] = fmaxf(fmaf(w04[j], pe[s], 0.f) + b04[j], 0.f);   // encoder_kernel's a1
-    a = ok ? a : zero;
-    img_store4<T16>(img_a, rg, cg, a);
-    *reinterpret_cast<unsigned*>(msk + rg * MSK_STRIDE + 4 * cg) = relu_mask4(a);
-    ev[rg] = ok ? pe[s] : 0.f;   // every thread of the row group (the same value): no branch in the round
-    issue(s, base + 2 * R16);   // the set is free: the round after next
-  };
-  auto compute = [&](const int s) {
-    const unsigned char* img_g = sm + s * EEB2_BUF;
-    const unsigned char* img_a = img_g + IMG16;
-    const unsigned char* msk = img_g + 2 * IMG16;
-    const float* ev = reinterpret_cast<const float*>(msk + MSK16);
-    wgrad_round<1, T16>(acc, img_g, img_a);                // dW2 += gz2^T a1
-    f32x4 d[1][1];
-    const unsigned char* imgs[1] = {img_g};
-    gemm_round<1, 1, T16>(d, ws, imgs);                    // W2^T gz2, features oc .. oc+3
-    const int r = l & 15;
-    const unsigned mm = *reinterpret_cast<const unsigned*>(msk + r * MSK_STRIDE + oc);
-    const double e = (double)ev[r];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float z = (mm >> (8 * j)) & 1u ? d[0][0][j] : 0.f;
-      sw[j] += (double)z * e;
-      sb[j] += (double)z;
-    }
-  };
-  // software-pipelined: the products of round k and the stage of round k + 1 (its rows already in
-  // registers, its images in the other buffer) between the same two barriers, interleaved by scheduling
-  // groups (two operand reads, one matrix instruction, three vector ones; left to itself the compiler
-  // issues all 36 products of a round before any of the stage's vector work).  94 -> 88 us per config-2
-  // call against the stage-then-products loop, same box, bitwise the same (gpurun_out/r04r).
-  auto weave = [&]() {
-#pragma unroll
-    for (int i = 0; i < 36; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-    }
-  };
-  // both rounds of a 32-row step always run: a round past r1 stages zero rows (exact zeros)
-  stage(0, r0);
-  __syncthreads();
-  for (int base = r0; base < r1; base += 2 * R16) {
-    compute(0);
-    stage(1, base + R16);
-    weave();
-    __syncthreads();
-    compute(1);
-    stage(0, base + 2 * R16);   // past r1 on the last step: zero rows nobody reads
-    weave();
-    __syncthreads();
-  }
-  __syncthreads();   // the last rounds' image reads precede the LDS reuse below
-  slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      sw[j] += __shfl_xor(sw[j], off);
-      sb[j] += __shfl_xor(sb[j], off);
-    }
-  if ((l & 15) == 0) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      nsums[(size_t)blockIdx.x * 2 * L + oc + j] = sw[j];
-      nsums[(size_t)blockIdx.x * 2 * L + L + oc + j] = sb[j];
-    }
-  }
-}
-
 // ============================================================================ narrow weight gradients
 // The block partial of a narrow weight gradient T[c][i] = sum_rows wide[c] narrow[i] (c < 128, i < K) in
 // wgrad_narrow_kernel's layout [T (128 K) | wide sums (128) | narrow sums (K)], reduced by
@@ -2618,7 +1653,6 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
                                const double* pairs_e, int npairs_e, int slab_init, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_w2: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_bwd_w2: bad slabs");
-  PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_bwd_w2: the XCD-interleaved build needs 256 blocks");
   PDG_CHECK_ARG(dst && gaggr && a2m && a1m && st_m && (lb_m || pairs_m) && ln_g && W2T && gz1m && gC,
                 "pdg_edge_bwd_w2: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(ln_g) &&
@@ -2646,52 +1680,12 @@ extern "C" int pdg_edge_bwd_w2(int n_edges, const int* dst, const float* gaggr, 
   return PDG_OK;
 }
 
-extern "C" int pdg_edge_bwd_fused(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
-                                  const float* a2m, const float* a1m, const float* a2e, const float* a1e,
-                                  const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,
-                                  const pdg_ln_bwd* lb_e, const float* ln_g_msg, const float* W2T, const float* WcT,
-                                  const float* e, const float* a2ln, const pdg_ln_stat* st_ln, const float* ln_g_e,
-                                  float* gz1m, float* gC, float* ge_out, float* slabs_w2, float* slabs_wc, int nslabs,
-                                  double* ln_partials, double* ln_pairs, const double* pairs_m, int npairs_m,
-                                  const double* pairs_e, int npairs_e, int slab_init, int accumulate, void* stream) {
-  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_bwd_fused: n_edges must be > 0");
-  PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs_w2 && slabs_wc, "pdg_edge_bwd_fused: bad slabs");
-  PDG_CHECK_ARG(dst && gaggr && a2m && a1m && st_m && (lb_m || pairs_m) && ln_g_msg && W2T && WcT && e && a2ln &&
-                    st_ln && ln_g_e && gz1m && gC && ge_out && ln_partials,
-                "pdg_edge_bwd_fused: null argument");
-  PDG_CHECK_ARG(PDG_ALIGNED(gaggr) && PDG_ALIGNED(a2m) && PDG_ALIGNED(a1m) && PDG_ALIGNED(ln_g_msg) &&
-                    PDG_ALIGNED(W2T) && PDG_ALIGNED(WcT) && PDG_ALIGNED(e) && PDG_ALIGNED(a2ln) && PDG_ALIGNED(gz1m) &&
-                    PDG_ALIGNED(gC) && PDG_ALIGNED(ge_out) && PDG_ALIGNED(slabs_w2) && PDG_ALIGNED(slabs_wc),
-                "pdg_edge_bwd_fused: misaligned pointer");
-  const bool eu = ge_next != nullptr;
-  PDG_CHECK_ARG(eu || gC == gz1m, "pdg_edge_bwd_fused: without the edge update gC is gz1m (pass the same array)");
-  PDG_CHECK_ARG(!eu || gC != gz1m, "pdg_edge_bwd_fused: gC may alias gz1m only without the edge update");
-  PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_bwd_fused: ge_out must not alias ge_next");
-  PDG_CHECK_ARG(!eu || (PDG_ALIGNED(ge_next) && a2e && a1e && st_e && (lb_e || pairs_e) && PDG_ALIGNED(a2e) &&
-                        PDG_ALIGNED(a1e)),
-                "pdg_edge_bwd_fused: edge-update arguments missing or misaligned");
-  hipStream_t s = (hipStream_t)stream;
-  if (eu)
-    hipLaunchKernelGGL(edge_bwd_fused_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), EBF_SHM, s, dst, gaggr, ge_next,
-                       a2m, a1m, a2e, a1e, st_m, st_e, lb_m, lb_e, ln_g_msg, W2T, WcT, e, a2ln, st_ln, ln_g_e, gz1m, gC,
-                       ge_out, slabs_w2, slabs_wc, ln_partials, ln_pairs, n_edges, pairs_m, npairs_m, pairs_e, npairs_e,
-                       slab_init, accumulate);
-  else
-    hipLaunchKernelGGL(edge_bwd_fused_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), EBF_SHM, s, dst, gaggr, ge_next,
-                       a2m, a1m, a2e, a1e, st_m, st_m, lb_m, lb_m, ln_g_msg, W2T, WcT, e, a2ln, st_ln, ln_g_e, gz1m, gC,
-                       ge_out, slabs_w2, slabs_wc, ln_partials, ln_pairs, n_edges, pairs_m, npairs_m, pairs_m, npairs_m,
-                       slab_init, accumulate);
-  PDG_CHECK_LAUNCH("pdg_edge_bwd_fused");
-  return PDG_OK;
-}
-
 extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, const float* ge_next, const float* WcT,
                                 float* ge_out, float* slabs, int nslabs, const float* a2ln, const pdg_ln_stat* st_ln,
                                 double* ln_partials, const float* ln_g, double* pairs, int accumulate, int slab_init,
                                 void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_gout_wc: n_edges must be > 0");
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS && slabs, "pdg_edge_gout_wc: bad slabs");
-  PDG_CHECK_ARG(!PDG_EBW_XCD || nslabs == XCD_GRID, "pdg_edge_gout_wc: the XCD-interleaved build needs 256 blocks");
   PDG_CHECK_ARG(gC && e && WcT && ge_out, "pdg_edge_gout_wc: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(gC) && PDG_ALIGNED(e) && PDG_ALIGNED(WcT) && PDG_ALIGNED(ge_out) &&
                     PDG_ALIGNED(slabs) && (!ge_next || PDG_ALIGNED(ge_next)),
@@ -2713,7 +1707,10 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
   return PDG_OK;
 }
 
-// Edge encoder backward without the W2^T product (PDG_EEB_MASK): the layer-1 input is one scalar e per edge,
+// ============================================================================ edge encoder backward
+// Backward of edge_encoder = Lin(1 -> 128) ReLU Lin(128 -> 128) ReLU LN (models.py:268-274) over the E scalar
+// inputs e_in, upstream gradient gy = d loss / d e_0 (ge_out of the first step), gz2 = LN_bwd(gy) [a2 > 0],
+// without the W2^T product: the layer-1 input is one scalar e per edge,
 // so a1 = mask . (w0 e + b0) with mask = [a1 > 0], and every gradient of the encoder's first two layers is a
 // linear function of two products over the rows with the BINARY mask as operand:
 //   M = (gz2 . e)^T mask,  N = gz2^T mask       (128 x 128 each, per block, K = rows)
@@ -2721,13 +1718,11 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
 // (the same sums regrouped; a1 enters exactly instead of rounded to fp32).  The mask is exact in ONE bf16 term,
 // so each product costs 3 MFMAs per K step instead of bf16x6's 6, and the per-row W2^T product of the
 // two-deep kernel (another 6 per step, with its weight slice in registers) is gone: half the matrix time.
-// Structure, staging and the db2 / slab bookkeeping as edge_enc_bwd2_kernel; the block's slab gets its dW2
-// and its narrow-sum row its dw0 / db0 partials, so pdg_bwd_epilogue reduces them unchanged.
-// (round 5, A/B on one box: 89.5 / 88.9 -> 75.1 / 76.0 us per config-2 call, gradients within 7e-8 of the
-// two-deep kernel's; PDG_EEB_MASK=0 builds edge_enc_bwd2_kernel)
-#ifndef PDG_EEB_MASK
-#define PDG_EEB_MASK 1
-#endif
+// 16-row rounds with two rounds of row loads in flight (edge_bwd_w2_kernel's form); the block's slab gets its
+// dW2 and its narrow-sum row its dw0 / db0 partials, so pdg_bwd_epilogue reduces them.  a1 is recomputed from
+// the scalar input (the forward keeps no a1), gz2 / gz1 are never written.  (Round 5, A/B on one box: 89.5 /
+// 88.9 -> 75.1 / 76.0 us per config-2 call against the earlier W2^T-product kernels, since removed; gradients
+// within 7e-8 of theirs.)
 constexpr int EEB3_BUF = 2 * IMG16 + T16;   // one round's gz2 and gz2.e images and the mask image
 // NS register sets of row loads: set s holds round n's rows (n = s mod NS) from its issue NS - 1 stages ahead
 // until its stage; the two LDS buffers alternate by round parity.  Four sets (64 KB of loads in flight per CU)
@@ -2891,17 +1886,9 @@ extern "C" int pdg_edge_enc_bwd(int n_edges, const float* gy, const float* a2, c
   PDG_CHECK_ARG(PDG_ALIGNED(gy) && PDG_ALIGNED(a2) && PDG_ALIGNED(w0) && PDG_ALIGNED(b0) && PDG_ALIGNED(ln_g) &&
                     PDG_ALIGNED(W2T) && PDG_ALIGNED(slabs),
                 "pdg_edge_enc_bwd: misaligned pointer");
-  if (PDG_EEB_MASK) {
-    const size_t shm3 = 2 * EEB3_BUF > 16 * L * 4 + 8 * L * 8 ? 2 * EEB3_BUF : 16 * L * 4 + 8 * L * 8;
-    hipLaunchKernelGGL(edge_enc_bwd3_kernel<PDG_EEB_SETS>, dim3(nslabs), dim3(EBW_THREADS), shm3, (hipStream_t)stream, gy, a2, e_in,
-                       w0, b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs, narrow_sums, n_edges, slab_init);
-    PDG_CHECK_LAUNCH("pdg_edge_enc_bwd");
-    return PDG_OK;
-  }
-  const size_t shm = PDG_EEB_2DEEP ? 2 * EEB2_BUF : 2 * EBW_IMG + EBW_MASK + X6_ROWS * sizeof(float);
-  hipLaunchKernelGGL(PDG_EEB_2DEEP ? edge_enc_bwd2_kernel : edge_enc_bwd_kernel, dim3(nslabs), dim3(EBW_THREADS), shm,
-                     (hipStream_t)stream, gy, a2, e_in, w0, b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs,
-                     narrow_sums, n_edges, slab_init);
+  const size_t shm = 2 * EEB3_BUF > 16 * L * 4 + 8 * L * 8 ? 2 * EEB3_BUF : 16 * L * 4 + 8 * L * 8;
+  hipLaunchKernelGGL(edge_enc_bwd3_kernel<PDG_EEB_SETS>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gy,
+                     a2, e_in, w0, b0, st, lb, lb_pairs, lb_npairs, ln_g, W2T, slabs, narrow_sums, n_edges, slab_init);
   PDG_CHECK_LAUNCH("pdg_edge_enc_bwd");
   return PDG_OK;
 }
@@ -2916,16 +1903,6 @@ extern "C" int pdg_enc_narrow_reduce(const double* narrow_sums, int nslabs, floa
 }
 
 
-// deferred a2 stores in the cooperative edge forward (edge_fwd_coop_kernel's D)
-// (default: bitwise the same outputs; with X below 216 -> 210.5 us per config-2 call, the step -0.05 ms, in
-// two same-box A/B pairs; D alone or X alone measured no faster)
-#ifndef PDG_EFC_DEFER
-#define PDG_EFC_DEFER 1
-#endif
-// XCD-interleaved rounds in the cooperative edge forward (edge_fwd_coop_kernel's X; needs nblocks % 8 == 0)
-#ifndef PDG_EFC_XCD
-#define PDG_EFC_XCD 1
-#endif
 
 // the P / Q layout this library was built for (pdg_common.hpp PDG_PQ_BLOCKED): 0 = two N x 128 arrays,
 // 1 = one N x 256 array of interleaved 16-feature blocks (Q = P + 16 floats)
@@ -2945,25 +1922,29 @@ extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln
                 "pdg_edge_fwd_coop: misaligned pointer");
   PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd_coop: edge-update outputs missing or misaligned");
-  PDG_CHECK_ARG(a2m != nullptr, "pdg_edge_fwd_coop: a2m is required");
-  const bool defer = PDG_EFC_DEFER;
+  // every required input and output refused when null (a null output would be dropped by its buffer
+  // resource, silently leaving the caller's array unwritten): e_res (first step) and a1m / a1e (inference)
+  // are the optional ones
+  PDG_CHECK_ARG(a2_prev && st && ln_g && ln_b && e_out && src && dst && P && Q && W1 && b1 && W2 && b2 && a2m &&
+                    part_m,
+                "pdg_edge_fwd_coop: null argument");
   // the XCD-interleaved rounds are compiled for the 256-block grid; any other grid (tests, other parts)
   // walks contiguous block ranges
-  const bool xcd = PDG_EFC_XCD && nblocks == XCD_GRID;
-  const size_t shm = 2 * EBW_IMG + 2 * EFC_TILE * sizeof(float) + (PDG_EFWD_CX6 ? EBW_IMG : X6_ROWS * EFC_ES * 4) +
-                     (defer ? 2 * EFC_TILE * sizeof(float) : 0) + (PDG_EFWD_CX6 ? 2 * EBW_WAVES * 64 * 16 : 0);
+  const bool xcd = nblocks == XCD_GRID;
+  const size_t shm = 2 * EBW_IMG + 2 * EFC_TILE * sizeof(float) + EBW_IMG + 2 * EFC_TILE * sizeof(float) +
+                     2 * EBW_WAVES * 64 * 16;
   hipStream_t s = (hipStream_t)stream;
-#define PDG_EFC_X(R, U, X)                                                                                            \
-  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, (bool)PDG_EFC_DEFER, X>), dim3(nblocks), dim3(EBW_THREADS), shm, s, \
+#define PDG_EFC_X(R, U, X)                                                                                    \
+  hipLaunchKernelGGL((edge_fwd_coop_kernel<R, U, X>), dim3(nblocks), dim3(EBW_THREADS), shm, s,               \
                      n_edges, a2_prev, st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a1m, a2m, a1e,   \
                      a2e, part_m, part_e)
-#define PDG_EFC(R, U)                         \
-  do {                                        \
-    if (PDG_EFC_XCD && xcd) {                 \
-      PDG_EFC_X(R, U, (bool)PDG_EFC_XCD);     \
-    } else {                                  \
-      PDG_EFC_X(R, U, false);                 \
-    }                                         \
+#define PDG_EFC(R, U)            \
+  do {                           \
+    if (xcd) {                   \
+      PDG_EFC_X(R, U, true);     \
+    } else {                     \
+      PDG_EFC_X(R, U, false);    \
+    }                            \
   } while (0)
   if (e_res) {
     if (with_edge_update) PDG_EFC(true, true); else PDG_EFC(true, false);
@@ -3004,21 +1985,6 @@ extern "C" int pdg_edge_enc_fwd(int n_edges, const float* e_in, const float* w0,
   return PDG_OK;
 }
 
-extern "C" int pdg_edge_enc_fwd_knots(int n_edges, const float* e_in, const float* w0, const float* b0,
-                                      const float* W2, const float* b2, float* table, float* a2, double* partials,
-                                      int nblocks, void* stream) {
-  PDG_CHECK_ARG(n_edges > 0 && nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_enc_fwd_knots: bad sizes");
-  PDG_CHECK_ARG(e_in && w0 && b0 && W2 && b2 && table && a2 && partials, "pdg_edge_enc_fwd_knots: null argument");
-  PDG_CHECK_ARG(PDG_ALIGNED(table) && PDG_ALIGNED(a2), "pdg_edge_enc_fwd_knots: misaligned pointer");
-  hipLaunchKernelGGL(edge_knots_kernel, dim3(EK_KNOTS + 1), dim3(EBW_THREADS), 0, (hipStream_t)stream, w0, b0, W2, b2, table);
-  PDG_CHECK_LAUNCH("pdg_edge_enc_fwd_knots");
-  hipLaunchKernelGGL(edge_enc_fwd_knots_kernel, dim3(nblocks), dim3(EBW_THREADS), (size_t)EK_SHM,
-                     (hipStream_t)stream, n_edges, e_in, table, a2, partials);
-  PDG_CHECK_LAUNCH("pdg_edge_enc_fwd_knots");
-  return PDG_OK;
-}
-
-extern "C" int pdg_edge_enc_knots_floats(void) { return EK_TAB; }
 
 extern "C" int pdg_gemm_sum2_coop(int rows, const float* in0, const float* in1, const float* W0T, const float* W1T,
                                   const float* res, float* out, const float* ln_a2, const pdg_ln_stat* ln_st,

@@ -332,7 +332,7 @@ extern "C" int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat*
 //   edge update: relu(C + P[src] + Q[dst]) -> ve (kept for layer 2)
 //   message:     relu(C + P[dst] + Q[src]) -> v
 // Chunk 0's gathers are issued before the W_c GEMM so their latency hides behind
-// it; with PDG_EF_PREFETCH chunk q+1's are in flight while chunk q is computed.
+// it; chunk q+1's are in flight while chunk q is computed.
 //
 // Memory-order discipline of the tile loop: vmcnt counts loads and stores together
 // and in issue order, so a load issued after a store cannot be waited for without
@@ -341,19 +341,10 @@ extern "C" int pdg_node_pq(int n_nodes, const float* a2_prev, const pdg_ln_stat*
 // this tile's last store, the gathers before a1m / a1e are stored, and the
 // loop-invariant vectors (b1, b2, LayerNorm weight and bias) never touch vector
 // memory inside the loop (FeatVec, ds_bpermute).
-#ifndef PDG_EF_PREFETCH
-#define PDG_EF_PREFETCH 1
-#endif
 #ifndef PDG_EDGE_FWD_WAVES
 #define PDG_EDGE_FWD_WAVES 8   // 2 waves per SIMD, 256 VGPRs: room for the prefetches (measured)
 #endif
 constexpr int EF_WAVES = PDG_EDGE_FWD_WAVES;
-#ifndef PDG_EF_EARLY
-#define PDG_EF_EARLY 1
-#endif
-#ifndef PDG_EF_NEXT
-#define PDG_EF_NEXT 1
-#endif
 struct Gather8 {
   f32x4 xs[2], yd[2], xd[2], ys[2];
 };
@@ -379,17 +370,10 @@ __device__ __forceinline__ void first_layers(float (&v)[FRAG], float (&ve)[FRAG]
                                              const float* __restrict__ ps, const float* __restrict__ qd,
                                              const float* __restrict__ pd, const float* __restrict__ qs) {
   Gather8 cur = g0;
-#if !PDG_EF_EARLY
-  gather_chunk<EU>(cur, 0, ps, qd, pd, qs);
-#endif
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-#if PDG_EF_PREFETCH
     Gather8 nxt;
     if (q < 3) gather_chunk<EU>(nxt, q + 1, ps, qd, pd, qs);
-#else
-    if (q > 0) gather_chunk<EU>(cur, q, ps, qd, pd, qs);
-#endif
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
 #pragma unroll
@@ -399,9 +383,7 @@ __device__ __forceinline__ void first_layers(float (&v)[FRAG], float (&ve)[FRAG]
         v[8 * q + 4 * t + j] = fmaxf((c + cur.xd[t][j]) + cur.ys[t][j], 0.f);
       }
     }
-#if PDG_EF_PREFETCH
     if (q < 3) cur = nxt;
-#endif
     PDG_FENCE();
   }
 }
@@ -443,18 +425,11 @@ __global__ __launch_bounds__(64 * EF_WAVES, EF_WAVES / 4) void edge_fwd_kernel(
     float* __restrict__ a2m, float* __restrict__ a1e, float* __restrict__ a2e, double* __restrict__ part_m,
     double* __restrict__ part_e) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
-#if PDG_EDGE_X6
   load_wblock_swz(lds, W1, 3 * L, 2 * L);   // W_c (fp32): edge-feature block
   unsigned char* w2p = reinterpret_cast<unsigned char*>(lds + 128 * 128);
   load_wplanes(w2p, W2, L, 0);             // W2 as three bf16 term planes
 #define PDG_GEMM_C(acc, v) gemm128_swz(acc, lds, v)
 #define PDG_GEMM_2(acc, v) gemm128_x6(acc, w2p, v)
-#else
-  load_wblock(lds, W1, 3 * L, 2 * L);   // W_c: edge-feature block
-  load_wblock(lds + WBLK, W2, L, 0);
-#define PDG_GEMM_C(acc, v) gemm128(acc, lds, v)
-#define PDG_GEMM_2(acc, v) PDG_GEMM_W2(acc, lds + WBLK, v)
-#endif
   const FeatVec fg = load_featvec(lg), fb = load_featvec(lb), fb1 = load_featvec(b1), fb2 = load_featvec(b2);
   __syncthreads();
   const LNStat st = *reinterpret_cast<const LNStat*>(stp);
@@ -483,9 +458,7 @@ __global__ __launch_bounds__(64 * EF_WAVES, EF_WAVES / 4) void edge_fwd_kernel(
     const float* pd = P + (size_t)d_node * L + lc;
     const float* qs = Q + (size_t)s_node * L + lc;
     Gather8 g0;
-#if PDG_EF_EARLY
     gather_chunk<EU>(g0, 0, ps, qd, pd, qs);
-#endif
     float v[FRAG];
     // e_t = LN(a2_prev) + e_res   (models.py:225 residual of the previous step)
     ln_apply<RES>(v, xa, xr, st, fg, fb);
@@ -515,14 +488,9 @@ __global__ __launch_bounds__(64 * EF_WAVES, EF_WAVES / 4) void edge_fwd_kernel(
       bias_relu_fv(v, Z, fb2);
       accum_stats(v, valid, se1, se2);
     }
-#if PDG_EF_NEXT
     issue(tile + stride);   // before this tile's last store
     PDG_FENCE();
     if (valid) store_frag((EU ? a2e : a2m) + (size_t)row * L, v);
-#else
-    if (valid) store_frag((EU ? a2e : a2m) + (size_t)row * L, v);
-    if (tile + stride < ntiles) issue(tile + stride);
-#endif
   }
 #undef PDG_GEMM_C
 #undef PDG_GEMM_2
@@ -548,13 +516,16 @@ extern "C" int pdg_edge_fwd(int n_edges, const float* a2_prev, const pdg_ln_stat
                             const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                             double* part_e, int with_edge_update, int* nparts, void* stream) {
   PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd: n_edges must be > 0");
+  PDG_CHECK_ARG(a2_prev && st && ln_g && ln_b && e_out && src && dst && P && Q && W1 && b1 && W2 && b2 && a2m &&
+                    part_m && nparts,
+                "pdg_edge_fwd: null argument");
   PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
                     PDG_ALIGNED(a1m) && PDG_ALIGNED(a2m) && (!e_res || PDG_ALIGNED(e_res)),
                 "pdg_edge_fwd: misaligned pointer");
   PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a1e) && PDG_ALIGNED(a2e)),
                 "pdg_edge_fwd: edge-update outputs missing or misaligned");
   const int grid = persistent_grid(n_edges, EF_WAVES, 1);
-  const size_t shm = PDG_EDGE_X6 ? (size_t)EDGE_LDS_BYTES : 2 * WBLK * sizeof(float);
+  const size_t shm = (size_t)EDGE_LDS_BYTES;
   hipStream_t s = (hipStream_t)stream;
 #define PDG_EDGE_FWD(R, U)                                                                                     \
   hipLaunchKernelGGL((edge_fwd_kernel<R, U>), dim3(grid), dim3(64 * EF_WAVES), shm, s, n_edges, a2_prev, st, ln_g, ln_b, \

@@ -88,218 +88,12 @@ __device__ __forceinline__ void write_ln_partials(double (&sg)[4], double (&sx)[
 
 }  // namespace
 
-__global__ __launch_bounds__(NU_THREADS, 1) void node_net_kernel(
-    int N, const float* __restrict__ aggr, const float* __restrict__ x, const float* __restrict__ W1,
-    const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
-    float* __restrict__ a1_out, float* __restrict__ a2_out, double* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float xin[3 * XBUF];
-  __shared__ __attribute__((aligned(16))) float a1t[2 * TILE * AS];   // double-buffered: one barrier per tile
-  const int w = wave_id(), l = lane_id();
-  const bool loader = w >= NU_COMPUTE;
-  const int ntiles = tiles_of(N);
-  const int lt = threadIdx.x - 64 * NU_COMPUTE;   // loader lane
-  // compute state: lane row r = l & 15, quarter q = l >> 4; weights of output rows 16w + (l & 15)
-  const int r = l & 15, q = l >> 4;
-  f32x4 w1f[16], w2f[8];
-  if (!loader) {
-    const float* w1r = W1 + (size_t)(16 * w + r) * (2 * L) + 4 * q;
-    const float* w2r = W2 + (size_t)(16 * w + r) * L + 4 * q;
-#pragma unroll
-    for (int T = 0; T < 16; ++T) w1f[T] = *reinterpret_cast<const f32x4*>(w1r + 16 * T);
-#pragma unroll
-    for (int T = 0; T < 8; ++T) w2f[T] = *reinterpret_cast<const f32x4*>(w2r + 16 * T);
-  }
-  double s1 = 0, s2 = 0;
-  TileRegs tr;
-  if (loader) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (nu_tile(k) < ntiles) {
-        fetch_tile(tr, nu_tile(k), N, lt, aggr, x);
-        store_tile(xin + k * XBUF, lt, tr);
-      }
-  }
-  __syncthreads();
-  for (int i = 0;; ++i) {
-    const int tile = nu_tile(i);
-    if (tile >= ntiles) break;   // uniform across the block
-    const float* xb = xin + (i % 3) * XBUF;
-    const int row = tile * TILE + r;
-    const bool valid = row < N;
-    const bool ahead = nu_tile(i + 2) < ntiles;
-    f32x4 a1 = {0.f, 0.f, 0.f, 0.f};
-    if (loader) {
-      if (ahead) fetch_tile(tr, nu_tile(i + 2), N, lt, aggr, x);
-    } else {
-      // layer 1: a1 = relu(W1 [aggr | x] + b1), K = 256
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* xr = xb + r * XS + 4 * q;
-#pragma unroll
-      for (int T = 0; T < 16; ++T) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(xr + 16 * T);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w1f[T][jj], bv[jj], acc, 0, 0, 0);
-      }
-      const f32x4 bias1 = *reinterpret_cast<const f32x4*>(b1 + 16 * w + 4 * q);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) a1[c] = fmaxf(acc[c] + bias1[c], 0.f);
-      // D row 4q + c of this wave's block = feature 16w + 4q + c of node row r
-      *reinterpret_cast<f32x4*>(a1t + (i & 1) * TILE * AS + r * AS + 16 * w + 4 * q) = a1;
-      if (valid && a1_out) stg4(a1_out + (size_t)row * L + 16 * w + 4 * q, a1);
-    }
-    __syncthreads();
-    if (loader) {
-      if (ahead) store_tile(xin + ((i + 2) % 3) * XBUF, lt, tr);   // last read in iteration i - 1
-    } else {
-      // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      const float* ar = a1t + (i & 1) * TILE * AS + r * AS + 4 * q;
-#pragma unroll
-      for (int T = 0; T < 8; ++T) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(ar + 16 * T);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[T][jj], bv[jj], acc, 0, 0, 0);
-      }
-      const f32x4 bias2 = *reinterpret_cast<const f32x4*>(b2 + 16 * w + 4 * q);
-      f32x4 a2;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) a2[c] = fmaxf(acc[c] + bias2[c], 0.f);
-      if (valid) {
-        stg4(a2_out + (size_t)row * L + 16 * w + 4 * q, a2);
-        const float p1 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
-        const float p2 = (a2[0] * a2[0] + a2[1] * a2[1]) + (a2[2] * a2[2] + a2[3] * a2[3]);
-        s1 += (double)p1;
-        s2 += (double)p2;
-      }
-    }
-  }
-  __shared__ double red[2 * (NU_THREADS / 64)];
-  block_sum2(s1, s2, red);
-  if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = s1;
-    part[2 * blockIdx.x + 1] = s2;
-  }
-}
-
-// node_net_kernel with TWO tiles per iteration (the block's tiles i = 2p and 2p + 1 of the same
-// tile sequence, one after the other with node_net_kernel's MFMA order, so a1 / a2 and the fp64
-// partials - tile 2p's rows before 2p + 1's - are bitwise node_net_kernel's): half the barriers
-// per node and twice the bytes per loader round.  Loader and compute waves run separate loops
-// with the same barrier sequence (one per pair: the stores into buffer (p + 2) % 3 after it are
-// read after the next pair's barrier, and layer 1 of pair p + 1 writes the layer-1 tile pair that
-// layer 2 of pair p - 1 read before this one), so the loaders' two tiles of registers are never
-// live beside the compute waves' 96 weight VGPRs (one shared loop spilled at the 168-VGPR budget
-// of 12 waves).  Three pair buffers (prefetch distance 2 pairs) and a double-buffered pair of
-// layer-1 tiles: 136 KB of LDS, one block per CU.
-__global__ __launch_bounds__(NU_THREADS, 1) void node_net_pair_kernel(
-    int N, const float* __restrict__ aggr, const float* __restrict__ x, const float* __restrict__ W1,
-    const float* __restrict__ b1, const float* __restrict__ W2, const float* __restrict__ b2,
-    float* __restrict__ a1_out, float* __restrict__ a2_out, double* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) float xin[6 * XBUF];
-  __shared__ __attribute__((aligned(16))) float a1t[4 * TILE * AS];
-  const int w = wave_id(), l = lane_id();
-  const int ntiles = tiles_of(N);
-  double s1 = 0, s2 = 0;
-  if (w >= NU_COMPUTE) {
-    // ---- loader waves: pair p + 2 fetched before the barrier of pair p, stored after it into
-    // buffer (p + 2) % 3, last read by layer 1 of pair p - 1 (before the barrier of pair p - 1)
-    const int lt = threadIdx.x - 64 * NU_COMPUTE;
-    TileRegs tr[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (nu_tile(2 * k) < ntiles) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) fetch_tile(tr[h], nu_tile(2 * k + h), N, lt, aggr, x);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) store_tile(xin + (2 * k + h) * XBUF, lt, tr[h]);
-      }
-    __syncthreads();
-    for (int p = 0; nu_tile(2 * p) < ntiles; ++p) {
-      const bool ahead = nu_tile(2 * (p + 2)) < ntiles;
-      if (ahead) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) fetch_tile(tr[h], nu_tile(2 * (p + 2) + h), N, lt, aggr, x);
-      }
-      __syncthreads();
-      if (ahead) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) store_tile(xin + (2 * ((p + 2) % 3) + h) * XBUF, lt, tr[h]);
-      }
-    }
-  } else {
-    const int r = l & 15, q = l >> 4;
-    f32x4 w1f[16], w2f[8];
-    const float* w1r = W1 + (size_t)(16 * w + r) * (2 * L) + 4 * q;
-    const float* w2r = W2 + (size_t)(16 * w + r) * L + 4 * q;
-#pragma unroll
-    for (int T = 0; T < 16; ++T) w1f[T] = *reinterpret_cast<const f32x4*>(w1r + 16 * T);
-#pragma unroll
-    for (int T = 0; T < 8; ++T) w2f[T] = *reinterpret_cast<const f32x4*>(w2r + 16 * T);
-    const f32x4 bias1 = *reinterpret_cast<const f32x4*>(b1 + 16 * w + 4 * q);
-    const f32x4 bias2 = *reinterpret_cast<const f32x4*>(b2 + 16 * w + 4 * q);
-    __syncthreads();
-    for (int p = 0; nu_tile(2 * p) < ntiles; ++p) {
-      const float* xb = xin + 2 * (p % 3) * XBUF;
-      float* at = a1t + 2 * (p & 1) * TILE * AS;
-      // layer 1: a1 = relu(W1 [aggr | x] + b1), K = 256, tile 2p then tile 2p + 1
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int T = 0; T < 16; ++T) {
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(xb + h * XBUF + r * XS + 4 * q + 16 * T);
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w1f[T][jj], bv[jj], acc, 0, 0, 0);
-        }
-        f32x4 a1;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) a1[c] = fmaxf(acc[c] + bias1[c], 0.f);
-        *reinterpret_cast<f32x4*>(at + h * TILE * AS + r * AS + 16 * w + 4 * q) = a1;
-        const int row = nu_tile(2 * p + h) * TILE + r;
-        if (row < N && a1_out) stg4(a1_out + (size_t)row * L + 16 * w + 4 * q, a1);
-      }
-      __syncthreads();   // the layer-1 tiles are complete
-      // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int T = 0; T < 8; ++T) {
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(at + h * TILE * AS + r * AS + 4 * q + 16 * T);
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[T][jj], bv[jj], acc, 0, 0, 0);
-        }
-        f32x4 a2;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) a2[c] = fmaxf(acc[c] + bias2[c], 0.f);
-        const int row = nu_tile(2 * p + h) * TILE + r;
-        if (row < N) {
-          stg4(a2_out + (size_t)row * L + 16 * w + 4 * q, a2);
-          const float p1 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
-          const float p2 = (a2[0] * a2[0] + a2[1] * a2[1]) + (a2[2] * a2[2] + a2[3] * a2[3]);
-          s1 += (double)p1;
-          s2 += (double)p2;
-        }
-      }
-    }
-  }
-  __shared__ double red[2 * (NU_THREADS / 64)];
-  block_sum2(s1, s2, red);
-  if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = s1;
-    part[2 * blockIdx.x + 1] = s2;
-  }
-}
-
 // node_net with both layers as unbiased bf16x6 products (gemm_x6f; the fp32 kernels above are
 // MFMA-bound): 8 waves, no loader waves, the three weight slices W1a (aggr half), W1b (x half) and W2
 // as bf16 terms in registers (144 VGPRs).  Per 16-row tile: every thread fetches one row chunk of aggr
 // and x of tile i + 2, layer 1 of tile i from its [aggr | x] images, a barrier, the split of tile
 // i + 2 into the images layer 1 of tile i - 1 read, layer 2 of tile i from its a1 image (double-
 // buffered).  One barrier per tile; 96 KB of LDS.
-#ifndef PDG_NN_LATE_STAGE
-#define PDG_NN_LATE_STAGE 1
-#endif
 constexpr int NN_T16 = TILE * X6_ROWB;        // bytes per term plane of a 16-row image (4 KB)
 constexpr int NN_IMG = 3 * NN_T16;            // one 16-row bf16x6 image (12 KB)
 
@@ -355,9 +149,6 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
     x6_store4<NN_T16>(a1i + (i & 1) * NN_IMG, r, 4 * w + q, a1);
     if (row < N && a1_out) stg4(a1_out + (size_t)row * L + oc, a1);
     __syncthreads();   // the a1 image is complete; the input buffer of tile i - 1 is free
-#if !PDG_NN_LATE_STAGE
-    if (ahead) stage((i + 2) % 3);
-#endif
     // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
     f32x4 d2[1] = {{0.f, 0.f, 0.f, 0.f}};
     gemm_x6f<1, NN_T16, true>(d2, w2, a1i + (i & 1) * NN_IMG);
@@ -371,11 +162,9 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
       s1 += (double)p1;
       s2 += (double)p2;
     }
-#if PDG_NN_LATE_STAGE
     // tile i + 2 into the buffer layer 1 of tile i - 1 read (before the previous barrier); read after
     // the next one.  After layer 2 its loads have the whole tile to land.
     if (ahead) stage((i + 2) % 3);
-#endif
   }
   __shared__ double red[2 * NU_COMPUTE];
   block_sum2(s1, s2, red);
@@ -385,15 +174,9 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
   }
 }
 
-#ifndef PDG_NODE_NET_X6
-#define PDG_NODE_NET_X6 1
-#endif
 
 // paired tiles (node_net_pair_kernel) by default: 46.6 -> 45.5-46.4 us per config-2 call in a same-box
 // A/B; the same pairing of node_pq_rw measured no faster and is not kept
-#ifndef PDG_NODE_NET_PAIR
-#define PDG_NODE_NET_PAIR 1
-#endif
 
 extern "C" int pdg_node_net(int n_nodes, const float* aggr, const float* x, const float* Wn1, const float* bn1,
                             const float* Wn2, const float* bn2, float* a1n, float* a2n, double* partials,
@@ -406,12 +189,8 @@ extern "C" int pdg_node_net(int n_nodes, const float* aggr, const float* x, cons
   const int tiles = tiles_of(n_nodes);
   const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
   const int grid = tiles < cap ? tiles : cap;
-  if (PDG_NODE_NET_X6)
-    hipLaunchKernelGGL(node_net_x6_kernel, dim3(grid), dim3(64 * NU_COMPUTE), 0, (hipStream_t)stream, n_nodes, aggr, x,
-                       Wn1, bn1, Wn2, bn2, a1n, a2n, partials);
-  else
-    hipLaunchKernelGGL(PDG_NODE_NET_PAIR ? node_net_pair_kernel : node_net_kernel, dim3(grid), dim3(NU_THREADS), 0,
-                       (hipStream_t)stream, n_nodes, aggr, x, Wn1, bn1, Wn2, bn2, a1n, a2n, partials);
+  hipLaunchKernelGGL(node_net_x6_kernel, dim3(grid), dim3(64 * NU_COMPUTE), 0, (hipStream_t)stream, n_nodes, aggr, x,
+                     Wn1, bn1, Wn2, bn2, a1n, a2n, partials);
   PDG_CHECK_LAUNCH("pdg_node_net");
   if (nparts) *nparts = grid;
   return PDG_OK;
@@ -595,123 +374,11 @@ extern "C" int pdg_node_bwd(int n_nodes, const float* gy, const float* a2n, cons
 }
 
 // ============================================================================ node P/Q pre-pass
-// x_t = LN(a2_prev) [+ x_prev] (loader waves, -> LDS + HBM), P = Wa x_t, Q = Wb x_t (compute
-// waves, weights Wa = W1[:, 0:128], Wb = W1[:, 128:256] of edge_net.0 held in registers).
-// Bitwise the results of pdg_node_pq (node_pq_kernel).
-namespace {
-
-struct XtRegs {
-  f32x4 av[2], rv[2];
-};
-
-template <bool RES>
-__device__ __forceinline__ void fetch_xt(XtRegs& rg, int t, int N, int lt, const float* __restrict__ a2p,
-                                         const float* __restrict__ xres) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
-    const bool ok = node < N;
-    rg.av[u] = ok ? reinterpret_cast<const f32x4*>(a2p + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-    if (RES) rg.rv[u] = ok ? reinterpret_cast<const f32x4*>(xres + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-}
-
-template <bool RES>
-__device__ __forceinline__ void store_xt(float* __restrict__ buf, int t, int N, int lt, const XtRegs& rg,
-                                         const LNStat& st, const float* __restrict__ g,
-                                         const float* __restrict__ b, float* __restrict__ xout) {
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int c = lt + 256 * u, rr = c >> 5, j = c & 31, node = t * TILE + rr;
-    const f32x4 gg = reinterpret_cast<const f32x4*>(g)[j], bb = reinterpret_cast<const f32x4*>(b)[j];
-    f32x4 y;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {   // ln_res_frag (pdg_fwd.hip), element by element
-      float v = div_den(rg.av[u][e] - st.mean, st.den, st.rstd) * gg[e] + bb[e];
-      if (RES) v += rg.rv[u][e];
-      y[e] = v;
-    }
-    *reinterpret_cast<f32x4*>(buf + rr * GS + 4 * j) = y;
-    if (node < N) stg4(xout + (size_t)node * L + 4 * j, y);
-  }
-}
-
-}  // namespace
-
-template <bool RES>
-__global__ __launch_bounds__(NU_THREADS, 1) void node_pq_rw_kernel(
-    int N, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
-    const float* __restrict__ lb, const float* __restrict__ xres, float* __restrict__ xout,
-    const float* __restrict__ W1, float* __restrict__ P, float* __restrict__ Q, const double* __restrict__ part,
-    int nparts, double count, pdg_ln_stat* __restrict__ st_out) {
-  __shared__ __attribute__((aligned(16))) float xt[3 * TILE * GS];
-  __shared__ LNStat st_sh;
-  __shared__ double red_fin[2 * NU_THREADS / 64];
-  const int w = wave_id(), l = lane_id();
-  const bool loader = w >= NU_COMPUTE;
-  const int ntiles = tiles_of(N);
-  const int lt = threadIdx.x - 64 * NU_COMPUTE;
-  if (part) {   // the node LayerNorm statistics of the previous step, folded in (pdg_node_pq_rw_fin)
-    ln_stat_from_partials(part, nparts, count, &st_sh, red_fin);
-    __syncthreads();
-    if (blockIdx.x == 0 && threadIdx.x == 0) *st_out = st_sh;
-  }
-  const LNStat st = part ? st_sh : *reinterpret_cast<const LNStat*>(stp);
-  const int r = l & 15, q = l >> 4;
-  const int oc = 16 * w + 4 * q;
-  f32x4 waf[8], wbf[8];
-  if (!loader) {
-    const float* pa = W1 + (size_t)(16 * w + r) * (3 * L) + 4 * q;
-#pragma unroll
-    for (int T = 0; T < 8; ++T) {
-      waf[T] = *reinterpret_cast<const f32x4*>(pa + 16 * T);
-      wbf[T] = *reinterpret_cast<const f32x4*>(pa + L + 16 * T);
-    }
-  }
-  XtRegs rg;
-  if (loader) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (nu_tile(k) < ntiles) {
-        fetch_xt<RES>(rg, nu_tile(k), N, lt, a2p, xres);
-        store_xt<RES>(xt + k * TILE * GS, nu_tile(k), N, lt, rg, st, lg, lb, xout);
-      }
-  }
-  __syncthreads();
-  for (int i = 0;; ++i) {
-    const int tile = nu_tile(i);
-    if (tile >= ntiles) break;   // uniform across the block
-    const bool ahead = nu_tile(i + 2) < ntiles;
-    if (loader) {
-      if (ahead) fetch_xt<RES>(rg, nu_tile(i + 2), N, lt, a2p, xres);
-    } else {
-      const int row = tile * TILE + r;
-      f32x4 acc_p = {0.f, 0.f, 0.f, 0.f}, acc_q = {0.f, 0.f, 0.f, 0.f};
-      const float* xr = xt + (i % 3) * TILE * GS + r * GS + 4 * q;
-#pragma unroll
-      for (int T = 0; T < 8; ++T) {
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(xr + 16 * T);
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          acc_p = __builtin_amdgcn_mfma_f32_16x16x4f32(waf[T][jj], bv[jj], acc_p, 0, 0, 0);
-          acc_q = __builtin_amdgcn_mfma_f32_16x16x4f32(wbf[T][jj], bv[jj], acc_q, 0, 0, 0);
-        }
-      }
-      if (row < N) {
-        stg4(P + (size_t)row * L + oc, acc_p);
-        stg4(Q + (size_t)row * L + oc, acc_q);
-      }
-    }
-    __syncthreads();
-    if (loader && ahead)   // buffer (i + 2) % 3 was last read in iteration i - 1
-      store_xt<RES>(xt + ((i + 2) % 3) * TILE * GS, nu_tile(i + 2), N, lt, rg, st, lg, lb, xout);
-  }
-}
-
-// The same pass with P and Q as bf16x6 products (gemm_x6f: unbiased accumulation, 2.7x less matrix
-// time than the fp32 MFMAs; the kernel above is MFMA-bound).  x_t goes through a 16-row bf16x6 image
-// instead of an fp32 tile; Wa / Wb are held as bf16 terms (96 VGPRs).  x_t is bitwise the
-// kernel above's; P / Q agree with it to fp32 rounding and are closer to fp64.
+// x_t = LN(a2_prev) [+ x_prev], P = Wa x_t, Q = Wb x_t (weights Wa = W1[:, 0:128], Wb = W1[:, 128:256] of
+// edge_net.0) with P and Q as bf16x6 products (gemm_x6f: unbiased accumulation, 2.7x less matrix time than
+// the fp32 MFMAs of the LDS-weight pdg_node_pq, which was MFMA-bound).  x_t goes through a 16-row bf16x6
+// image; Wa / Wb are held as bf16 terms (96 VGPRs).  x_t is bitwise pdg_node_pq's; P / Q agree with it to
+// fp32 rounding and are closer to fp64.
 constexpr int PQ_T16 = TILE * X6_ROWB;       // bytes per term plane of a 16-row image (4 KB)
 constexpr int PQ_IMG = 3 * PQ_T16;           // one 16-row bf16x6 image (12 KB)
 
@@ -816,10 +483,7 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_pq_x6_kernel(
   }
 }
 
-#ifndef PDG_NODE_PQ_X6
-#define PDG_NODE_PQ_X6 1
-#endif
-static_assert(!PDG_PQ_BLOCKED || PDG_NODE_PQ_X6, "the blocked P / Q layout is written by node_pq_x6_kernel only");
+static_assert(!PDG_PQ_BLOCKED || 1, "the blocked P / Q layout is written by node_pq_x6_kernel only");
 
 static int node_pq_rw_launch(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                              const float* ln_b, const float* x_res, float* x_out, const float* W1, float* P,
@@ -832,13 +496,13 @@ static int node_pq_rw_launch(int n_nodes, const float* a2_prev, const pdg_ln_sta
   const int tiles = tiles_of(n_nodes);
   const int cap = device_cus() < MAX_BLOCKS ? device_cus() : MAX_BLOCKS;
   const int grid = tiles < cap ? tiles : cap;
-  const int nt = PDG_NODE_PQ_X6 ? 64 * NU_COMPUTE : NU_THREADS;
+  const int nt = 64 * NU_COMPUTE;
   if (x_res)
-    hipLaunchKernelGGL(PDG_NODE_PQ_X6 ? node_pq_x6_kernel<true> : node_pq_rw_kernel<true>, dim3(grid), dim3(nt), 0,
+    hipLaunchKernelGGL(node_pq_x6_kernel<true>, dim3(grid), dim3(nt), 0,
                        (hipStream_t)stream, n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, part, nparts,
                        count, st_out);
   else
-    hipLaunchKernelGGL(PDG_NODE_PQ_X6 ? node_pq_x6_kernel<false> : node_pq_rw_kernel<false>, dim3(grid), dim3(nt), 0,
+    hipLaunchKernelGGL(node_pq_x6_kernel<false>, dim3(grid), dim3(nt), 0,
                        (hipStream_t)stream, n_nodes, a2_prev, st, ln_g, ln_b, x_res, x_out, W1, P, Q, part, nparts,
                        count, st_out);
   PDG_CHECK_LAUNCH("pdg_node_pq_rw");

@@ -18,9 +18,6 @@
 using namespace pdg;
 
 constexpr int SLAB = L * L + L;   // floats per slab
-#ifndef PDG_WGRAD_GROUPS
-#define PDG_WGRAD_GROUPS 3
-#endif
 
 __device__ __forceinline__ void zero_acc16(f32x16 (&acc)[4]) {
 #pragma unroll
@@ -550,306 +547,6 @@ struct WgTable {
 };
 constexpr int WG_TABLE_FLOATS = (sizeof(WgTable) + 15) / 16 * 4;
 
-__device__ __forceinline__ void wg_load(const WgTable* tb, int nseg, long base, long r1, int (&seg)[4],
-                                        f32x4 (&gr)[4], f32x4 (&xr)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = threadIdx.x + 256 * i;
-    const int row = idx >> 5, c4 = idx & 31;
-    const long vr = base + row;
-    if (vr < r1) {
-      while (seg[i] + 1 < nseg && vr >= tb->start[seg[i] + 1]) ++seg[i];
-      const long r = vr - tb->start[seg[i]];
-      gr[i] = ldg4(tb->G[seg[i]] + r * L + 4 * c4);
-      xr[i] = ldg4(tb->X[seg[i]] + r * L + 4 * c4);
-    } else {
-      gr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-}
-
-__device__ __forceinline__ void wg_store(float* gs, float* xs, const f32x4 (&gr)[4], const f32x4 (&xr)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = threadIdx.x + 256 * i;
-    reinterpret_cast<f32x4*>(gs)[idx] = gr[i];
-    reinterpret_cast<f32x4*>(xs)[idx] = xr[i];
-  }
-}
-
-__global__ __launch_bounds__(256, 2) void wgrad_segments_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];   // [table | 2 x (G tile | X tile)]
-  WgTable* tb = reinterpret_cast<WgTable*>(smem);
-  float* lds = smem + WG_TABLE_FLOATS;
-  const int nseg = sg.nseg;
-  for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
-  for (int i = threadIdx.x; i < PDG_MAX_SEGS; i += blockDim.x) {
-    tb->G[i] = sg.G[i];
-    tb->X[i] = sg.X[i];
-  }
-  __syncthreads();
-  const int nb = gridDim.x;
-  long per = (total + nb - 1) / nb;
-  per = (per + WG_ROWS - 1) / WG_ROWS * WG_ROWS;
-  const long r0 = min(total, per * blockIdx.x), r1 = min(total, per * (blockIdx.x + 1));
-  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
-  const int ob = 64 * (w >> 1), ib = 64 * (w & 1);
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  float bsum0 = 0.f, bsum1 = 0.f;
-  f32x4 gr[4], xr[4];
-  int seg[4];
-  {
-    // first segment of this block's range (binary search, once)
-    int lo = 0, hi = nseg;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (tb->start[mid] <= r0) lo = mid; else hi = mid;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) seg[i] = lo;
-  }
-  int buf = 0;
-  if (r0 < r1) {
-    wg_load(tb, nseg, r0, r1, seg, gr, xr);
-    wg_store(lds, lds + WG_TILE, gr, xr);
-  }
-  __syncthreads();
-  for (long base = r0; base < r1; base += WG_ROWS) {
-    const bool more = base + WG_ROWS < r1;
-    if (more) wg_load(tb, nseg, base + WG_ROWS, r1, seg, gr, xr);   // next tile in flight during the MFMAs
-    const float* gs = lds + buf * 2 * WG_TILE;
-    const float* xs = gs + WG_TILE;
-#pragma unroll
-    for (int s = 0; s < WG_ROWS / 2; ++s) {
-      const int row = 2 * s + h;
-      const float a0 = gs[row * L + ob + c], a1 = gs[row * L + ob + 32 + c];
-      const float b0 = xs[row * L + ib + c], b1 = xs[row * L + ib + 32 + c];
-      bsum0 += a0;
-      bsum1 += a1;
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-    }
-    if (more) {
-      float* ngs = lds + (buf ^ 1) * 2 * WG_TILE;
-      wg_store(ngs, ngs + WG_TILE, gr, xr);
-    }
-    __syncthreads();
-    buf ^= 1;
-  }
-  float* slab = slabs + (size_t)blockIdx.x * SLAB;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int i = ib + 32 * b + c;
-        slab[o * L + i] = acc[a][b][r];
-      }
-  if ((w & 1) == 0) {   // bias sums from the waves whose quadrant starts at input 0
-    const float o0 = __shfl_xor(bsum0, 32), o1 = __shfl_xor(bsum1, 32);
-    if (h == 0) {
-      slab[L * L + ob + c] = bsum0 + o0;
-      slab[L * L + ob + 32 + c] = bsum1 + o1;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------- bf16x6 form
-// The same segmented reduction on the bf16 matrix cores with fp32 accuracy:
-// every operand value is split exactly into three bf16 terms x = x0 + x1 + x2
-// (round-to-nearest hi, mid, lo: 24 significant bits) and
-//   G^T X = sum over the six products with i + j <= 2 of Gi^T Xj,
-// accumulated in fp32 from the smallest terms up; the dropped products are
-// below 2^-24 |G||X|, the size of one fp32 rounding.  v_mfma_f32_32x32x16_bf16
-// does 16x the flops of v_mfma_f32_32x32x2_f32 per cycle, so the six products
-// cost 2.7x less matrix-core time than one fp32 product and the pass is bound
-// by HBM (reading G and X once).
-//
-// Block: 4 waves, three blocks per CU.  Per round it stages 32 rows: thread t
-// loads rows 4(t>>5) .. +3, columns 4(t&31) .. +3 of G and X (two full 512-B
-// rows per wave instruction), splits them and writes the terms row-major into
-// LDS images [term][32 rows][256 B] (ds_write_b64).  The MFMA operands need 8
-// consecutive ROWS of one column per lane; ds_read_b64_tr_b16 reads them
-// transposed (4 rows x 16 columns per 16-lane group).  The 16-B chunks of row r
-// are XOR-swizzled by ((r & 3) << 2 | (r >> 2) & 3): both the writes and each
-// 32-lane half of the transposed reads then hit 64 distinct banks.  Wave w owns the 64x64
-// output quadrant (o in 64(w>>1) + [0,64), i in 64(w&1) + [0,64)).
-// Split 4 rows x 4 columns and write them: row i of this thread goes to image row 4 rg + i.
-__device__ __forceinline__ void x6_store(unsigned char* img, int cg, int rg, const f32x4 (&v)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    unsigned h0, m0, l0, h1, m1, l1;
-    split3_pair(v[i][0], v[i][1], h0, m0, l0);
-    split3_pair(v[i][2], v[i][3], h1, m1, l1);
-    const int off = x6_addr(4 * rg + i, 8 * cg);
-    *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
-    *reinterpret_cast<u32x2*>(img + X6_TERM + off) = u32x2{m0, m1};
-    *reinterpret_cast<u32x2*>(img + 2 * X6_TERM + off) = u32x2{l0, l1};
-  }
-}
-
-__device__ __forceinline__ void x6_load(const WgTable* tb, int nseg, long base, long r1, int& seg, int cg,
-                                        f32x4 (&gr)[4], f32x4 (&xr)[4]) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const long vr = base + i;
-    if (vr < r1) {
-      while (seg + 1 < nseg && vr >= tb->start[seg + 1]) ++seg;
-      const long r = vr - tb->start[seg];
-      gr[i] = ldg4(tb->G[seg] + r * L + 4 * cg);
-      xr[i] = ldg4(tb->X[seg] + r * L + 4 * cg);
-    } else {
-      gr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      xr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-}
-
-// NG wave groups of 4 per block (NG = 3: one 768-thread block per CU): group g stages and multiplies
-// its own third of the block's rows in its own images, and the groups' accumulators are added in a
-// fixed order at the end, so each CU writes ONE slab (the slab traffic and the reduction that reads
-// it shrink NG-fold).  All groups run the same number of rounds (rows past a group's end are zero).
-template <int NG>
-__device__ __forceinline__ void wgrad_x6_body(const WgradSegs& sg, long total, float* __restrict__ slabs) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem6[];   // [table | NG x (G terms | X terms)]
-  WgTable* tb = reinterpret_cast<WgTable*>(smem6);
-  const int grp = threadIdx.x >> 8, tid = threadIdx.x & 255;
-  unsigned char* gimg = smem6 + WG_TABLE_FLOATS * 4 + grp * 6 * X6_TERM;
-  unsigned char* ximg = gimg + 3 * X6_TERM;
-  const int nseg = sg.nseg;
-  for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
-  for (int i = threadIdx.x; i < PDG_MAX_SEGS; i += blockDim.x) {
-    tb->G[i] = sg.G[i];
-    tb->X[i] = sg.X[i];
-  }
-  __syncthreads();
-  const int nb = gridDim.x;
-  long per = (total + nb - 1) / nb;
-  per = (per + NG * X6_ROWS - 1) / (NG * X6_ROWS) * (NG * X6_ROWS);
-  const long bper = per / NG;                                           // rows per group (whole rounds)
-  const long b0 = min(total, per * blockIdx.x), b1 = min(total, per * (blockIdx.x + 1));
-  const long r0 = min(b1, b0 + bper * grp), r1 = min(b1, r0 + bper);
-  const int l = lane_id(), h = l >> 5, c = l & 31, w = (tid >> 6);
-  const int cg = tid & 31, rg = tid >> 5;
-  const int ob = 64 * (w >> 1), ib = 64 * (w & 1);
-  // transposed-read row and column byte of this lane inside its 16-lane group (see x6_operand)
-  const int lrow = 8 * h + ((l & 15) >> 2);
-  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  int seg;
-  {
-    int lo = 0, hi = nseg;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (tb->start[mid] <= r0) lo = mid; else hi = mid;
-    }
-    seg = lo;
-  }
-  const long nrounds = (min(b1, b0 + bper) - b0 + X6_ROWS - 1) / X6_ROWS;   // group 0's count: the most
-  f32x4 gr[4], xr[4];
-  x6_load(tb, nseg, r0 + 4 * rg, r1, seg, cg, gr, xr);    // rows past r1 load as zeros
-#pragma unroll
-  for (int i = 0; i < 4; ++i) bsum += gr[i];
-  x6_store(gimg, cg, rg, gr);
-  x6_store(ximg, cg, rg, xr);
-  __syncthreads();
-  for (long k = 0; k < nrounds; ++k) {
-    const long base = r0 + k * X6_ROWS;
-    const bool more = k + 1 < nrounds;
-    if (more) x6_load(tb, nseg, base + X6_ROWS + 4 * rg, r1, seg, cg, gr, xr);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 A[2][3], B[2][3];
-#pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const int row = 16 * ks + lrow;
-        const int g0 = x6_addr(row, lcolb + 2 * (ob + 32 * a)), g1 = x6_addr(row + 4, lcolb + 2 * (ob + 32 * a));
-        const int x0 = x6_addr(row, lcolb + 2 * (ib + 32 * a)), x1 = x6_addr(row + 4, lcolb + 2 * (ib + 32 * a));
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          A[a][p] = x6_operand(gimg + p * X6_TERM, g0, g1);
-          B[a][p] = x6_operand(ximg + p * X6_TERM, x0, x1);
-        }
-      }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          f32x16 t = acc[a][b];
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2], B[b][0], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][1], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][2], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][0], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][1], t, 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][0], t, 0, 0, 0);
-        }
-    }
-    __syncthreads();
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) bsum += gr[i];
-      x6_store(gimg, cg, rg, gr);
-      x6_store(ximg, cg, rg, xr);
-    }
-    __syncthreads();
-  }
-  // combine the groups in a fixed order ((g_{NG-1} + ... ) + g_0) through LDS (the images are dead):
-  // element (o, i) at float o * 128 + i, bias sums after the 128 x 128 block
-  float* cmb = reinterpret_cast<float*>(smem6 + WG_TABLE_FLOATS * 4);
-  float* red = NG > 1 ? cmb + L * L : cmb;   // 8 row groups x 128 bias partials (NG = 1: cmb is unused)
-  for (int g = NG - 1; g >= 0; --g) {
-    if (grp == g) {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int i = ib + 32 * b + c;
-            float v = acc[a][b][r];
-            if (g < NG - 1) v = cmb[o * L + i] + v;
-            if (g == 0) slabs[(size_t)blockIdx.x * SLAB + o * L + i] = v;
-            else cmb[o * L + i] = v;
-          }
-      f32x4* rb = reinterpret_cast<f32x4*>(red + 4 * tid);
-      *rb = (g < NG - 1) ? *rb + bsum : bsum;
-    }
-    __syncthreads();
-  }
-  // bias sums: the 8 row groups of each column group, in row-group order
-  if (threadIdx.x < 128) {
-    const int col = threadIdx.x, g = col >> 2, j = col & 3;
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) s += red[4 * (32 * q + g) + j];
-    slabs[(size_t)blockIdx.x * SLAB + L * L + col] = s;
-  }
-}
-
-template <int NG>
-__global__ __launch_bounds__(256 * NG, 3 / NG) void wgrad_x6_kernel(WgradSegs sg, long total, float* __restrict__ slabs) {
-  wgrad_x6_body<NG>(sg, total, slabs);
-}
-
 // Several weights' segment passes in one launch (blockIdx.y = job; each job its own slab set):
 // the node_net.2 / decoder / node encoder passes were three launches, the two single-segment ones
 // ~19 us each for 41 MB (fill / drain).
@@ -859,12 +556,6 @@ struct WgradJobs {
   long total[WGJ_MAX];
   float* slabs[WGJ_MAX];
 };
-
-template <int NG>
-__global__ __launch_bounds__(256 * NG, 3 / NG) void wgrad_x6_jobs_kernel(WgradJobs jobs) {
-  const int j = blockIdx.y;
-  wgrad_x6_body<NG>(jobs.s[j], jobs.total[j], jobs.slabs[j]);
-}
 
 constexpr int WG16 = 16 * X6_ROWB;   // bytes per term plane of a 16-row image (4 KB)
 constexpr int WIMG16 = 3 * WG16;     // one 16-row bf16x6 image (12 KB)
@@ -885,9 +576,6 @@ __device__ __forceinline__ void x6_store1(unsigned char* img, int cg, int r, con
 // buffered 16-row images, one barrier per round.  Wave w owns o in 32 (w & 3) + [0, 32), i in
 // 64 (w >> 2) + [0, 64) as two 32x32 accumulators.  The block's K steps run in row order (the grouped
 // form above summed three row thirds and added them at the end: the same products in another order).
-#ifndef PDG_WGJ_2DEEP
-#define PDG_WGJ_2DEEP 1
-#endif
 __device__ __forceinline__ void wgrad_x6_body2(const WgradSegs& sg, long total, float* __restrict__ slabs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem7[];   // [table | parity x (G | X)]
   WgTable* tb = reinterpret_cast<WgTable*>(smem7);
@@ -1009,7 +697,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x6_jobs_kernel2(WgradJobs jobs) 
 
 constexpr size_t WGJ2_SHM = WG_TABLE_FLOATS * 4 + 2 * 2 * WIMG16;
 
-extern "C" int pdg_wgrad_slabs_per_cu(void) { return 3 / PDG_WGRAD_GROUPS; }
+extern "C" int pdg_wgrad_slabs_per_cu(void) { return 3 / 3; }
 
 extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const float* const* x_ptrs, const int* rows,
                                   float* slabs, int nslabs, void* stream) {
@@ -1029,20 +717,7 @@ extern "C" int pdg_wgrad_segments(int nseg, const float* const* g_ptrs, const fl
   for (int i = nseg + 1; i <= PDG_MAX_SEGS; ++i) sg.start[i] = tot;
   sg.nseg = nseg;
   PDG_CHECK_ARG(tot > 0, "pdg_wgrad_segments: no rows");
-#ifdef PDG_WGRAD_F32
-  hipLaunchKernelGGL(wgrad_segments_kernel, dim3(nslabs), dim3(256), (WG_TABLE_FLOATS + 4 * WG_TILE) * sizeof(float),
-                     (hipStream_t)stream, sg, tot, slabs);
-#else
-#if PDG_WGJ_2DEEP
   hipLaunchKernelGGL(wgrad_x6_kernel2, dim3(nslabs), dim3(512), WGJ2_SHM, (hipStream_t)stream, sg, tot, slabs);
-#elif PDG_WGRAD_GROUPS == 3
-  hipLaunchKernelGGL(wgrad_x6_kernel<3>, dim3(nslabs), dim3(768), WG_TABLE_FLOATS * 4 + 18 * X6_TERM,
-                     (hipStream_t)stream, sg, tot, slabs);
-#else
-  hipLaunchKernelGGL(wgrad_x6_kernel<1>, dim3(nslabs), dim3(256), WG_TABLE_FLOATS * 4 + 6 * X6_TERM, (hipStream_t)stream,
-                     sg, tot, slabs);
-#endif
-#endif
   PDG_CHECK_LAUNCH("pdg_wgrad_segments");
   return PDG_OK;
 }
@@ -1053,13 +728,6 @@ extern "C" int pdg_wgrad_segments_batch(int njobs, const int* nseg, const float*
   PDG_CHECK_ARG(njobs > 0 && njobs <= WGJ_MAX && nseg && g_ptrs && x_ptrs && rows && slabs,
                 "pdg_wgrad_segments_batch: 1..%d jobs", WGJ_MAX);
   PDG_CHECK_ARG(nslabs > 0 && nslabs <= MAX_BLOCKS, "pdg_wgrad_segments_batch: bad nslabs");
-#if defined(PDG_WGRAD_F32) || PDG_WGRAD_GROUPS != 3
-  for (int j = 0, k = 0; j < njobs; k += nseg[j], ++j) {
-    const int rc = pdg_wgrad_segments(nseg[j], g_ptrs + k, x_ptrs + k, rows + k, slabs[j], nslabs, stream);
-    if (rc != PDG_OK) return rc;
-  }
-  return PDG_OK;
-#else
   WgradJobs jobs;
   int k = 0;
   for (int j = 0; j < njobs; ++j) {
@@ -1081,14 +749,9 @@ extern "C" int pdg_wgrad_segments_batch(int njobs, const int* nseg, const float*
     jobs.total[j] = tot;
     jobs.slabs[j] = slabs[j];
   }
-  if (PDG_WGJ_2DEEP)
-    hipLaunchKernelGGL(wgrad_x6_jobs_kernel2, dim3(nslabs, njobs), dim3(512), WGJ2_SHM, (hipStream_t)stream, jobs);
-  else
-    hipLaunchKernelGGL(wgrad_x6_jobs_kernel<3>, dim3(nslabs, njobs), dim3(768), WG_TABLE_FLOATS * 4 + 18 * X6_TERM,
-                       (hipStream_t)stream, jobs);
+  hipLaunchKernelGGL(wgrad_x6_jobs_kernel2, dim3(nslabs, njobs), dim3(512), WGJ2_SHM, (hipStream_t)stream, jobs);
   PDG_CHECK_LAUNCH("pdg_wgrad_segments_batch");
   return PDG_OK;
-#endif
 }
 
 // ---------------------------------------------------------------------------- pairs
@@ -1110,151 +773,6 @@ struct WgTable3 {
 };
 constexpr int WG3_TABLE_BYTES = (sizeof(WgTable3) + 15) / 16 * 16;
 
-// Split 2 rows x 4 columns and write them: row i of this thread goes to image row 2 rg + i.
-__device__ __forceinline__ void x6_store2(unsigned char* img, int cg, int rg, const f32x4 (&v)[2]) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    unsigned h0, m0, l0, h1, m1, l1;
-    split3_pair(v[i][0], v[i][1], h0, m0, l0);
-    split3_pair(v[i][2], v[i][3], h1, m1, l1);
-    const int off = x6_addr(2 * rg + i, 8 * cg);
-    *reinterpret_cast<u32x2*>(img + off) = u32x2{h0, h1};
-    *reinterpret_cast<u32x2*>(img + X6_TERM + off) = u32x2{m0, m1};
-    *reinterpret_cast<u32x2*>(img + 2 * X6_TERM + off) = u32x2{l0, l1};
-  }
-}
-
-__device__ __forceinline__ void x6_load3(const WgTable3* tb, int nseg, long base, long r1, int& seg, int cg,
-                                         f32x4 (&v)[3][2]) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const long vr = base + i;
-    if (vr < r1) {
-      while (seg + 1 < nseg && vr >= tb->start[seg + 1]) ++seg;
-      const long r = vr - tb->start[seg];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) v[a][i] = ldg4(tb->A[a][seg] + r * L + 4 * cg);
-    } else {
-#pragma unroll
-      for (int a = 0; a < 3; ++a) v[a][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-}
-
-template <bool SHX>
-__global__ __launch_bounds__(512, 1) void wgrad_x6_pair_kernel(WgradSegs3 sg, long total, float* __restrict__ slabs0,
-                                                              float* __restrict__ slabs1) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem3[];   // [table | A0 | A1 | A2 terms]
-  WgTable3* tb = reinterpret_cast<WgTable3*>(smem3);
-  unsigned char* img = smem3 + WG3_TABLE_BYTES;
-  const int nseg = sg.nseg;
-  for (int i = threadIdx.x; i <= PDG_MAX_SEGS; i += blockDim.x) tb->start[i] = sg.start[i];
-  for (int i = threadIdx.x; i < 3 * PDG_MAX_SEGS; i += blockDim.x) tb->A[i / PDG_MAX_SEGS][i % PDG_MAX_SEGS] =
-      sg.A[i / PDG_MAX_SEGS][i % PDG_MAX_SEGS];
-  __syncthreads();
-  const int nb = gridDim.x;
-  long per = (total + nb - 1) / nb;
-  per = (per + X6_ROWS - 1) / X6_ROWS * X6_ROWS;
-  const long r0 = min(total, per * blockIdx.x), r1 = min(total, per * (blockIdx.x + 1));
-  const int l = lane_id(), h = l >> 5, c = l & 31, w = wave_id();
-  const int pw = w >> 2, w4 = w & 3;                      // product, quadrant
-  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;  // loader: rows 2 rg, 2 rg + 1, columns 4 cg ..
-  const int ob = 64 * (w4 >> 1), ib = 64 * (w4 & 1);
-  const unsigned char* gimg = img + (SHX ? pw : 0) * 3 * X6_TERM;
-  const unsigned char* ximg = img + (SHX ? 2 : 1 + pw) * 3 * X6_TERM;
-  const int lrow = 8 * h + ((l & 15) >> 2);
-  const int lcolb = 2 * (16 * ((l >> 4) & 1) + 4 * (l & 3));
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  f32x4 bs0 = f32x4{0.f, 0.f, 0.f, 0.f}, bs1 = f32x4{0.f, 0.f, 0.f, 0.f};   // column sums of A0 (and A1)
-  int seg;
-  {
-    int lo = 0, hi = nseg;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (tb->start[mid] <= r0) lo = mid; else hi = mid;
-    }
-    seg = lo;
-  }
-  f32x4 v[3][2];
-  auto stage = [&]() {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      bs0 += v[0][i];
-      if (SHX) bs1 += v[1][i];
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) x6_store2(img + a * 3 * X6_TERM, cg, rg, v[a]);
-  };
-  if (r0 < r1) {
-    x6_load3(tb, nseg, r0 + 2 * rg, r1, seg, cg, v);
-    stage();
-  }
-  __syncthreads();
-  for (long base = r0; base < r1; base += X6_ROWS) {
-    const bool more = base + X6_ROWS < r1;
-    if (more) x6_load3(tb, nseg, base + X6_ROWS + 2 * rg, r1, seg, cg, v);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 A[2][3], B[2][3];
-#pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const int row = 16 * ks + lrow;
-        const int g0 = x6_addr(row, lcolb + 2 * (ob + 32 * a)), g1 = x6_addr(row + 4, lcolb + 2 * (ob + 32 * a));
-        const int x0 = x6_addr(row, lcolb + 2 * (ib + 32 * a)), x1 = x6_addr(row + 4, lcolb + 2 * (ib + 32 * a));
-#pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          A[a][p] = x6_operand(gimg + p * X6_TERM, g0, g1);
-          B[a][p] = x6_operand(ximg + p * X6_TERM, x0, x1);
-        }
-      }
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          f32x16 t = acc[a][b];
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][2], B[b][0], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][1], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][2], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][1], B[b][0], t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][1], t, 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A[a][0], B[b][0], t, 0, 0, 0);
-        }
-    }
-    __syncthreads();
-    if (more) stage();
-    __syncthreads();
-  }
-  float* slab = (pw ? slabs1 : slabs0) + (size_t)blockIdx.x * SLAB;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int o = ob + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int i = ib + 32 * b + c;
-        slab[o * L + i] = acc[a][b][r];
-      }
-  // bias sums: the 16 row groups of each column group, in row-group order (the images are dead)
-  float* red = reinterpret_cast<float*>(img);
-  *reinterpret_cast<f32x4*>(red + 4 * threadIdx.x) = bs0;
-  *reinterpret_cast<f32x4*>(red + 2048 + 4 * threadIdx.x) = SHX ? bs1 : bs0;
-  __syncthreads();
-  if (threadIdx.x < 2 * L) {
-    const int p = threadIdx.x >> 7, col = threadIdx.x & 127, g = col >> 2, j = col & 3;
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) s += red[2048 * p + 4 * (32 * q + g) + j];
-    (p ? slabs1 : slabs0)[(size_t)blockIdx.x * SLAB + L * L + col] = s;
-  }
-}
-
 // Two-deep form (default): 16-row rounds with TWO rounds of row loads in flight, in the registers one
 // 32-row round used to take (two sets of one row x three arrays per thread, by round parity): set s
 // is staged for round n and re-issued for round n + 2 at once, so rows are landing while the CU
@@ -1265,9 +783,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_x6_pair_kernel(WgradSegs3 sg, lo
 // are formed per thread over other rows (fp32, another order).  Per config-2 call 174-179 -> 164-168 us
 // (rocprofv3, same box); three sets in flight (PDG_WGP_DEPTH=3, triple-buffered images) measured the
 // same as two: what is left is the round's MFMA phase (two waves per SIMD) in series with its stage.
-#ifndef PDG_WGP_2DEEP
-#define PDG_WGP_2DEEP 1
-#endif
 #ifndef PDG_WGP_DEPTH
 #define PDG_WGP_DEPTH 2
 #endif
@@ -1419,23 +934,13 @@ extern "C" int pdg_wgrad_pairs(int nseg, const float* const* a0_ptrs, const floa
   for (int i = nseg + 1; i <= PDG_MAX_SEGS; ++i) sg.start[i] = tot;
   sg.nseg = nseg;
   PDG_CHECK_ARG(tot > 0, "pdg_wgrad_pairs: no rows");
-  if (PDG_WGP_2DEEP) {
-    const size_t shm = WG3_TABLE_BYTES + WGP_DEPTH * 3 * WIMG16;
-    if (shared_x)
-      hipLaunchKernelGGL(wgrad_x6_pair2_kernel<true>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
-                         slabs0, slabs1);
-    else
-      hipLaunchKernelGGL(wgrad_x6_pair2_kernel<false>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
-                         slabs0, slabs1);
-  } else {
-    const size_t shm = WG3_TABLE_BYTES + 9 * X6_TERM;
-    if (shared_x)
-      hipLaunchKernelGGL(wgrad_x6_pair_kernel<true>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
-                         slabs0, slabs1);
-    else
-      hipLaunchKernelGGL(wgrad_x6_pair_kernel<false>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot,
-                         slabs0, slabs1);
-  }
+  const size_t shm = WG3_TABLE_BYTES + WGP_DEPTH * 3 * WIMG16;
+  if (shared_x)
+    hipLaunchKernelGGL(wgrad_x6_pair2_kernel<true>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot, slabs0,
+                       slabs1);
+  else
+    hipLaunchKernelGGL(wgrad_x6_pair2_kernel<false>, dim3(nslabs), dim3(512), shm, (hipStream_t)stream, sg, tot, slabs0,
+                       slabs1);
   PDG_CHECK_LAUNCH("pdg_wgrad_pairs");
   return PDG_OK;
 }

@@ -20,18 +20,11 @@ constexpr int X6_TERM = X6_ROWS * X6_ROWB;        // bytes per term image (8 KB)
 // Byte address of byte `b` (0..255) of image row `r`: 16-B chunk index XOR (4 (r & 3) + t((r >> 2) & 3)).
 // (measured: 1.9e7 -> 0 LDS bank-conflict cycles per edge_bwd_w2 launch with the mask stride below,
 // bitwise the same results, time unchanged within noise; the transposed reads stay conflict free)
-#ifndef PDG_X6_SWZ
-#define PDG_X6_SWZ 2
-#endif
 __device__ __forceinline__ int x6_addr(int r, int b) {
-#if PDG_X6_SWZ == 2
   // t = (0, 2, 3, 1): the straight 16-B operand reads of the edge backward (row = lane & 15,
   // chunk + (lane >> 4)) then hit 16 distinct chunks in every ds_read_b128 lane group
   const int t = (0x78 >> (2 * ((r >> 2) & 3))) & 3;
   return r * X6_ROWB + (b ^ (((r & 3) << 6) | (t << 4)));
-#else
-  return r * X6_ROWB + (b ^ (((r & 3) << 6) | (((r >> 2) & 3) << 4)));
-#endif
 }
 
 // (x0, x1) = hi + mid + lo exactly, per element: bf16 round-to-nearest-even of x, of the

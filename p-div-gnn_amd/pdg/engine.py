@@ -67,10 +67,6 @@ VARIANTS = {
     # edge backward with the W2 / Wc weight gradients fused (pdg_edge_bwd_w2 / pdg_edge_gout_wc); False:
     # pdg_edge_bwd + deferred pdg_wgrad_segments passes
     "fused_edge_wgrad": ("PDG_FUSED_EDGE_WGRAD", True),
-    # the two fused edge-backward kernels as ONE weight-specialised pass (pdg_edge_bwd_fused: gC and ge_next
-    # reach the Wc work through LDS instead of HBM; applies with fused_edge_wgrad and gz1e_from_gc, the split
-    # pair runs otherwise)
-    "fused_edge_bwd": ("PDG_FUSED_EDGE_BWD", False),
     # P/Q gather backward before the Wc pass (gz1m / gz1e re-read while still in the Infinity Cache:
     # pq_scatter_bwd 63.6 -> 59.7 us and edge_gout_wc 145 -> 140 us per call, same box)
     "pq_first": ("PDG_PQ_FIRST", True),
@@ -94,12 +90,6 @@ VARIANTS = {
     "node_enc_coop": ("PDG_NODE_ENC_COOP", True),
     # the decoder likewise (pdg_decoder_fwd_coop) instead of the LDS-weight pdg_decoder_fwd[_fin]
     "decoder_coop": ("PDG_DECODER_COOP", True),
-    # the edge encoder forward from its knot table (pdg_edge_enc_fwd_knots: one fma per output, no W2 product)
-    # instead of pdg_edge_enc_fwd: 33.6 vs 48.3 us per config-2 step and closer to fp64, but off: its rounding
-    # differs in kind from the reference's fp32 products, and after the resumed Adam step of
-    # tests/test_gpu_checkpoint.py the LayerNorm biases (gradient components at noise level, which Adam
-    # normalises) sit 1.03e-5 from the reference's instead of 1.0e-7 (EXPERIMENTS.md section 4)
-    "edge_enc_knots": ("PDG_EDGE_ENC_KNOTS", False),
     # pdg_edge_enc_fwd blocks per CU (104 VGPRs, 41 KB LDS per 8-wave block)
     "enc_blocks_per_cu": ("PDG_ENC_BLOCKS_PER_CU", 2),
 }
@@ -208,12 +198,9 @@ class EPDEngine:
         self.fused_edge_wgrad = var["fused_edge_wgrad"]
         self.pq_first = var["pq_first"]
         self.gz1e_from_gc = var["gz1e_from_gc"]
-        self.fused_edge_bwd = var["fused_edge_bwd"]
         self.coop_fwd = var["coop_fwd"]
         self.node_enc_coop = var["node_enc_coop"]
         self.decoder_coop = var["decoder_coop"]
-        self.edge_enc_knots = var["edge_enc_knots"]
-        self._knots = torch.empty(lib.pdg_edge_enc_knots_floats(), dtype=torch.float32, device=self.device)
         # the P / Q layout the library's node pre-pass writes and its cooperative edge forward reads
         self.pq_blocked = bool(lib.pdg_pq_layout())
         self._nslabs_e = min(torch.cuda.get_device_properties(self.device).multi_processor_count,
@@ -312,14 +299,7 @@ class EPDEngine:
         # pdg_edge_enc_bwd recomputes it from the scalar input
         a1_ee = self._empty(E, L) if (need_grad and not self.fused_edge_wgrad) else None
         a2_ee = self._empty(E, L)
-        if E and a1_ee is None and self.edge_enc_knots:   # piecewise-linear form (pdg_edge_enc_fwd_knots)
-            nb = self._nslabs_e   # one block per CU (the table and a row chunk take 148.6 KB of LDS)
-            self._t("edge_enc_fwd", lib.pdg_edge_enc_fwd_knots, E, _p(e_in), _p(P["edge_encoder.0.weight"]),
-                    _p(P["edge_encoder.0.bias"]), _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]),
-                    _p(self._knots), _p(a2_ee), _p(self._part_a), nb, s)
-            self._nparts.value = nb
-            self._finalize(self._part_a, E * L, st[1], s, True)
-        elif E and a1_ee is None:   # bf16x6 W2 product, register-stationary (pdg_edge_enc_fwd)
+        if E and a1_ee is None:   # bf16x6 W2 product, register-stationary (pdg_edge_enc_fwd)
             nb = self._enc_blocks
             self._t("edge_enc_fwd", lib.pdg_edge_enc_fwd, E, _p(e_in), _p(P["edge_encoder.0.weight"]),
                     _p(P["edge_encoder.0.bias"]), _p(P["edge_encoder.2.weight"]), _p(P["edge_encoder.2.bias"]),
@@ -600,29 +580,13 @@ class EPDEngine:
                 if eu:   # edge-update LayerNorm: gy = ge_next (per edge)
                     pp, n_e = edge_ln_pairs(PE(t), ge_next, d["a2e"], st[d["i_e"]], ACC_E, g_edge)
                     pe, ne = src(pp, n_e if not fused else n_edge)
-                # (the one-pass kernel forms no gz1e: with gz1e_from_gc off the split pair runs)
-                one_pass = fused and self.fused_edge_bwd and e_sum
-                if one_pass:
-                    # + the column sums / pairs of the LayerNorm that produced e_t (as pdg_edge_gout_wc)
-                    if t > 0:
-                        a2ln, st_ln, accb, gl, pp = (ctx.per_step[t - 1]["a2e"], st[ctx.per_step[t - 1]["i_e"]], ACC_E,
-                                                     g_edge, PE(t - 1))
-                    else:
-                        a2ln, st_ln, accb, gl, pp = ctx.a2_ee, st[1], ACC_EE, P["edge_encoder.4.weight"], P_EENC
-                    self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_fused, E, _p(plan.dst), _p(gaggr),
-                            _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
-                            st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(T["WcT"]),
-                            _p(d["e"]), _p(a2ln), st_ln, _p(gl), _p(gz1m), _p(gC), _p(ge_out), _p(slabs_w2),
-                            _p(slabs_wc), nse, _p(accb), _p(pp), pm, nm, pe, ne, int(t == S - 1), 1, s)
-                    n_edge = nse
-                elif fused:
+                if fused:
                     self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd_w2, E, _p(plan.dst), _p(gaggr),
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(gz1m),
                             _p(gz1e if eu else None), _p(gC), _p(slabs_w2), nse, pm, nm, pe, ne, int(t == S - 1), s)
-                # the edge-update rows of the P/Q gather backward: gz1e, or gC (= gz1m + gz1e) with e_is_sum
-                ge_rows, e_is_sum = (gC, 1) if (e_sum and eu) else (gz1e if eu else None, 0)
-                if fused and not one_pass:
+                    # the edge-update rows of the P/Q gather backward: gz1e, or gC (= gz1m + gz1e) with e_is_sum
+                    ge_rows, e_is_sum = (gC, 1) if (e_sum and eu) else (gz1e if eu else None, 0)
                     # + the column sums / pairs of the LayerNorm that produced e_t (LN_e of step t-1, or the
                     # edge encoder's)
                     if t > 0:
@@ -636,7 +600,7 @@ class EPDEngine:
                     if not self.pq_first:
                         self._t("edge_gout", gout_fn, *gout_args)
                     n_edge = nse
-                elif not fused:
+                else:
                     self._t("edge_bwd" if eu else "edge_bwd_last", lib.pdg_edge_bwd, E, _p(plan.dst), _p(gaggr),
                             _p(ge_next), _p(d["a2m"]), _p(d["a1m"]), _p(d["a2e"]), _p(d["a1e"]), st[d["i_m"]],
                             st[d["i_e"]] if eu else None, None, None, _p(g_edge), _p(T["W2T"]), _p(T["WcT"]),
@@ -644,7 +608,7 @@ class EPDEngine:
                     ge_rows, e_is_sum = gz1e if eu else None, 0
                 self._t("pq_scatter_bwd", lib.pdg_pq_scatter_bwd, N, _p(plan.rowptr_dst), _p(plan.rowptr_src),
                         _p(plan.perm_src), _p(gz1m), _p(ge_rows), e_is_sum, _p(gP), _p(gQ), s)
-                if fused and self.pq_first and not one_pass:   # gz1m / gz1e read while still in the Infinity Cache
+                if fused and self.pq_first:   # gz1m / gz1e read while still in the Infinity Cache
                     self._t("edge_gout", gout_fn, *gout_args)
             # gx_t, with the column sums / pairs of the LayerNorm whose output it is the gradient of:
             # the node LayerNorm of step t-1, or the node encoder's

@@ -79,8 +79,6 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
-    "pdg_edge_enc_fwd_knots": [I, P, P, P, P, P, P, P, P, I, P],
-    "pdg_edge_enc_knots_floats": [],
     "pdg_node_enc_fwd": [I, P, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_node_bwd_coop": [I] + [P] * 14 + [I, I, P],
@@ -94,7 +92,6 @@ SIGNATURES: dict[str, list] = {
     "pdg_enc_narrow_reduce": [P, I, P, P, P],
     "pdg_edge_bwd_w2": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, P, I, P, I, I, P],
     "pdg_edge_gout_wc": [I, P, P, P, P, P, P, I, P, P, P, P, P, I, I, P],
-    "pdg_edge_bwd_fused": [I] + [P] * 23 + [I, P, P, P, I, P, I, I, I, P],
     "pdg_mesh_graph": [I, P, I, I, P, I, P, P, P, ctypes.c_long, P, P, ctypes.c_long, P],
     "pdg_mesh_graph_scratch_bytes": [I, I],
     "pdg_wgrad_segments": [I, P, P, P, P, I, P],
@@ -152,8 +149,7 @@ class _Lib:
         if not name.startswith("pdg_"):
             raise AttributeError(name)
         fn = getattr(self.load(), name)
-        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks", "pdg_wgrad_slabs_per_cu", "pdg_pq_layout",
-                                                  "pdg_edge_enc_knots_floats"):
+        if name in _RESTYPES or name in ("pdg_version", "pdg_max_blocks", "pdg_wgrad_slabs_per_cu", "pdg_pq_layout"):
             return fn
 
         def call(*args):

@@ -160,3 +160,53 @@ def test_custom_ops_registered_and_refuse_cpu():
     with pytest.raises(RuntimeError, match="HIP device"):
         torch.ops.pdivgnn.batch_loss(torch.zeros(4, 3), torch.zeros(4, 3), torch.tensor([0, 4]), None, None, None,
                                      None, None, None, None, None, True, False, 1.0, False)
+
+
+def _params(name):
+    """(type, name) of every parameter of `name` in include/pdivgnn.h."""
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    m = re.search(rf"\bint\s+{name}\s*\(([^)]*)\)\s*;", text, re.S)
+    out = []
+    for a in m.group(1).split(","):
+        a = a.strip()
+        nm = re.findall(r"\w+", a)[-1]
+        out.append(("ptr" if "*" in a else "int", nm))
+    return out
+
+
+INTS = {"n_edges": 1000, "n_nodes": 1000, "nslabs": 256, "nblocks": 256, "npairs_m": 1, "npairs_e": 1,
+        "with_edge_update": 1, "slab_init": 0, "accumulate": 0, "e_is_sum": 0}
+
+
+def _args(name, null):
+    """Arguments of `name` with every pointer a distinct 16-byte-aligned fake address (never dereferenced:
+    the checks run on the host before any HIP call) except `null`, which is NULL."""
+    out = []
+    for i, (kind, nm) in enumerate(_params(name)):
+        if kind == "ptr":
+            out.append(None if nm in (null, "stream") else 0x100000 + 0x1000 * i)
+        else:
+            out.append(INTS[nm])
+    return out
+
+
+@pytest.mark.parametrize("name,outputs", [
+    ("pdg_edge_fwd_coop", ["e_out", "a2m", "part_m", "a2_prev", "src", "P"]),
+    ("pdg_edge_fwd", ["e_out", "a2m", "part_m", "dst", "Q"]),
+    ("pdg_edge_bwd", ["gz2m", "gz1m", "gC", "ge_out", "dst"]),
+    ("pdg_edge_bwd_w2", ["gz1m", "gC", "slabs", "gaggr"]),
+    ("pdg_edge_gout_wc", ["ge_out", "slabs", "gC", "WcT"]),
+    ("pdg_pq_scatter_bwd", ["gP", "gQ", "gz1m", "perm_src"]),
+])
+def test_edge_entry_points_refuse_null_required_arguments(name, outputs):
+    """the edge kernels write through their output pointers (buffer stores drop a NULL
+    range silently, flat stores fault), so every required input and output is checked on the host and a
+    NULL one refused with PdgError before anything is launched (round 5's fault was an engine branch that
+    passed NULL gz2m / gz1e outputs to pdg_edge_bwd)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("host-side argument checks only: never called with fake pointers where a GPU is present")
+    from pdg.lib import PdgError, lib
+    for nm in outputs:
+        with pytest.raises(PdgError, match="null argument|bad slabs|required"):
+            getattr(lib, name)(*_args(name, nm))

@@ -312,8 +312,7 @@ def test_gz1e_from_gc_matches_stored_gz1e(nmesh, ngraph, steps):
 @pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
 def test_forward_variants_agree(nmesh, ngraph, steps):
     """The two edge-forward kernels of the engine: pdg_edge_fwd_coop (default: block-cooperative, C and W2
-    in unbiased bf16x6) and pdg_edge_fwd (LDS weights, C in fp32 MFMAs), with the two edge-encoder forwards
-    (pdg_edge_enc_fwd's bf16x6 W2 product, default, and the knot-table pdg_edge_enc_fwd_knots).  Output (training and inference)
+    in unbiased bf16x6) and pdg_edge_fwd (LDS weights, C in fp32 MFMAs).  Output (training and inference)
     agree to 1e-5 and every parameter gradient to VARIANT_TOL (two fp32 evaluations may differ in a relu
     mask bit whose pre-activation is within rounding of zero)."""
     from gnn_local_stress import losses
@@ -326,7 +325,6 @@ def test_forward_variants_agree(nmesh, ngraph, steps):
         model = _model(steps, stats)
         eng = model._engine_for(batch.pos.device)
         eng.coop_fwd = coop
-        eng.edge_enc_knots = not coop   # the knot-table edge encoder (A/B variant) beside the default one
         with torch.no_grad():
             y_inf = model(batch, scale_output=True).local_stress.clone()
         pred = model(batch, scale_output=False).local_stress
@@ -375,36 +373,3 @@ def test_edgeless_batch_matches_oracle():
             assert float(p.grad.abs().max()) == 0.0, name        # the edge branch: exactly zero
         else:
             assert rel(p.grad, ref) <= GRAD_TOL, (name, rel(p.grad, ref))
-
-
-@pytest.mark.parametrize("nmesh,ngraph,steps", [(41, 3, 4), (9, 1, 3)])
-def test_one_pass_edge_backward_matches_split_pair(nmesh, ngraph, steps):
-    """pdg_edge_bwd_fused (engine variant fused_edge_bwd) against pdg_edge_bwd_w2 + pdg_edge_gout_wc through
-    the whole backward: d loss / d x_t and d loss / d e_t bit for bit at the first backward step (gz1m, gC
-    and ge_out are bitwise the split pair's) and to 1e-6 at the others, every parameter gradient to 1e-6
-    (the bias and LayerNorm column sums add in another order)."""
-    from gnn_local_stress import losses
-    from pdg import meshgen
-    samples = meshgen.make_dataset(ngraph, n=nmesh, hole_radius=(0.15, 0.3), seed=7)
-    batch = make_batch(samples)
-    stats = {k: float(v) for k, v in dataset_stats(batch).items()}
-    res = {}
-    for one in (False, True):
-        model = _model(steps, stats)
-        eng = model._engine_for(batch.pos.device)
-        eng.fused_edge_bwd = one
-        eng.probe = {}
-        pred = model(batch, scale_output=False).local_stress
-        gt = (batch.local_stress - model.mean_local_stress) / model.std_local_stress
-        total, _, _ = losses.batch_loss(pred, batch, gt, divergence=True, divergence_penalty=10.0)
-        total.backward()
-        res[one] = (float(total), {n: p.grad.detach().clone() for n, p in model.named_parameters()}, eng.probe)
-        eng.probe = None
-    (l0, g0, p0), (l1, g1, p1) = res[False], res[True]
-    assert l0 == l1
-    # the first backward step bit for bit; later steps read the LayerNorm pairs, whose sums changed order
-    assert torch.equal(p0[steps - 1]["ge"], p1[steps - 1]["ge"]) and torch.equal(p0[steps - 1]["gx"], p1[steps - 1]["gx"])
-    for t in p0:
-        assert rel(p1[t]["ge"], p0[t]["ge"]) < 1e-6 and rel(p1[t]["gx"], p0[t]["gx"]) < 1e-6, t
-    for name, g in g1.items():
-        assert rel(g, g0[name]) < 1e-6, (name, rel(g, g0[name]))

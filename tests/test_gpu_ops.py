@@ -919,12 +919,11 @@ def test_wgrad_reduce_batch_matches_single(env):
             assert rel(outs["batch"][1][i].double().cpu() - gb0[i].double().cpu(), ref[L * L:]) < 1e-5
 
 
-@pytest.mark.parametrize("kind", ["knots", "x6"])
 @pytest.mark.parametrize("E,nb", [(77, 37), (4099, 37), (20000, 512)])
-def test_edge_enc_fwd_vs_fp64(env, E, nb, kind):
-    """pdg_edge_enc_fwd (default: W2 product in bf16x6, register-stationary) and pdg_edge_enc_fwd_knots
-    (A/B variant: piecewise-linear form, knot table) against an fp64 restatement: a2 to fp32 rounding, the LayerNorm partials'
-    (sum, sum of squares) to 1e-6.  Rows past the edges are not written (the NaN fill survives nowhere)."""
+def test_edge_enc_fwd_vs_fp64(env, E, nb):
+    """pdg_edge_enc_fwd (W2 product in bf16x6, register-stationary) against an fp64 restatement: a2 to fp32
+    rounding, the LayerNorm partials' (sum, sum of squares) to 1e-6.  Rows past the edges are not written (the
+    NaN fill survives nowhere)."""
     lib, sh, _ = env
     s = sh()
     e_in = rnd(E)
@@ -932,13 +931,8 @@ def test_edge_enc_fwd_vs_fp64(env, E, nb, kind):
     W2, b2 = lin(L, L)
     a2 = torch.full((E + 5, L), float("nan"), device="cuda")
     part = torch.zeros(2 * nb, dtype=torch.float64, device="cuda")
-    if kind == "knots":
-        tab = torch.empty(lib.pdg_edge_enc_knots_floats(), device="cuda")
-        lib.pdg_edge_enc_fwd_knots(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
-                                   tab.data_ptr(), a2.data_ptr(), part.data_ptr(), nb, s)
-    else:
-        lib.pdg_edge_enc_fwd(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
-                             a2.data_ptr(), part.data_ptr(), nb, s)
+    lib.pdg_edge_enc_fwd(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
+                         a2.data_ptr(), part.data_ptr(), nb, s)
     assert bool(a2[E:].isnan().all())
     a2 = a2[:E]
     a1 = torch.relu(e_in.double()[:, None] * w0.double()[:, 0][None, :] + b0.double())
@@ -947,39 +941,6 @@ def test_edge_enc_fwd_vs_fp64(env, E, nb, kind):
     p = part.view(nb, 2).sum(0).cpu()
     assert abs(float(p[0]) - float(ref.sum())) <= 1e-6 * float(ref.abs().sum())
     assert abs(float(p[1]) - float((ref * ref).sum())) <= 1e-6 * float((ref * ref).sum())
-
-
-def test_edge_enc_fwd_knots_edge_cases(env):
-    """pdg_edge_enc_fwd_knots on the cases the knot table must get right: zero first-layer weights (a feature
-    active everywhere or nowhere, no knot), repeated knots (two features with the same w0, b0), inputs exactly
-    at knots and beyond every knot on both sides, and one edge: a2 within fp32 rounding of fp64."""
-    lib, sh, _ = env
-    s = sh()
-    w0, b0 = lin(L, 1)
-    W2, b2 = lin(L, L)
-    w0[:8] = 0.0
-    b0[:4] = 0.3
-    b0[4:8] = -0.2
-    w0[20], b0[20] = w0[21], b0[21]
-    w0[30], b0[30] = w0[31], b0[31]
-    knots = (-b0[8:] / w0[8:, 0]).float()
-    e_in = torch.cat([knots, knots * (1 + 1e-7), torch.tensor([-1e30, 1e30, 0.0, -0.0], device="cuda"),
-                      rnd(500, scale=5.0)]).contiguous()
-    tab = torch.empty(lib.pdg_edge_enc_knots_floats(), device="cuda")
-    for E in (1, e_in.numel()):
-        a2 = torch.full((E, L), float("nan"), device="cuda")
-        part = torch.zeros(2 * 37, dtype=torch.float64, device="cuda")
-        lib.pdg_edge_enc_fwd_knots(E, e_in.data_ptr(), w0.data_ptr(), b0.data_ptr(), W2.data_ptr(), b2.data_ptr(),
-                                   tab.data_ptr(), a2.data_ptr(), part.data_ptr(), 37, s)
-        a1 = torch.relu(e_in[:E].double()[:, None] * w0.double()[:, 0][None, :] + b0.double())
-        ref = torch.relu(a1 @ W2.double().T + b2.double())
-        mid = ref.abs().amax(1) < 1e20   # the +-1e30 rows: compare relative to their own scale
-        assert rel(a2[mid], ref[mid]) < TOL, rel(a2[mid], ref[mid])
-        if (~mid).any():
-            assert rel(a2[~mid], ref[~mid]) < TOL
-        p = part.view(37, 2).sum(0).cpu()
-        if E == 1:
-            assert abs(float(p[0]) - float(ref.sum())) <= 1e-6 * float(ref.abs().sum())
 
 
 @pytest.mark.parametrize("N,nb", [(7, 37), (1031, 37), (40328, 256), (100489, 256)])
@@ -1325,69 +1286,3 @@ def test_nmse_fwd_bwd_equals_fwd_then_bwd(env, sizes, accumulate):
         t, p = gt64[lo:hi], pr64[lo:hi]
         ref = (((t - p) ** 2).sum(0) / ((t - t.mean(0)) ** 2).sum(0)).mean()
         assert abs(float(l1[b]) - float(ref)) <= 1e-5 * abs(float(ref)), (b, float(l1[b]), float(ref))
-
-
-@pytest.mark.parametrize("E,eu", [(77, 1), (4099, 1), (4099, 0), (30011, 1)])
-def test_edge_bwd_fused_matches_split_pair(env, E, eu):
-    """pdg_edge_bwd_fused (one weight-specialised pass) against pdg_edge_bwd_w2 + pdg_edge_gout_wc on the
-    same inputs, twice (the first call initialises the slabs and LayerNorm partials, the second adds):
-    gz1m, gC, ge_out and the dW2 / dWc slab sums bitwise (the same MFMA sequence per element); the db2 / db1
-    slab sums, the LayerNorm column-sum rows and pairs to fp32 summation order.  E = 77: fewer rows than
-    blocks x 16 (empty and ragged blocks); eu = 0: the message branch only (gC is gz1m)."""
-    lib, sh, _ = env
-    s = sh()
-    N, ns = max(E // 6, 7), 37
-    g = torch.Generator().manual_seed(E + eu)
-    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values.int().cuda()
-    gaggr = rnd(N, L)
-    ge_next = rnd(E, L) if eu else None
-    a2m, a1m, a2e, a1e, a2ln = (torch.relu(rnd(E, L)) for _ in range(5))
-    e = rnd(E, L)
-    W2T, WcT = rnd(L, L) * 0.1, rnd(L, L) * 0.1
-    lg, lge = rnd(L) * 0.3 + 1.0, rnd(L) * 0.3 + 1.0
-
-    def stat(a):
-        part = torch.tensor([float(a.double().sum()), float((a.double() ** 2).sum())], dtype=torch.float64,
-                            device="cuda")
-        return finalize(lib, s, part, 1, a.numel())
-    st_m, st_e, st_ln = stat(a2m), stat(a2e), stat(a2ln)
-    pm, pe = rnd(5, 2).double() * 0.01, rnd(7, 2).double() * 0.01
-    P = lambda t: None if t is None else t.data_ptr()  # noqa: E731
-    res = {}
-    for arm in ("split", "fused"):
-        o = {k: torch.full((E, L), float("nan"), device="cuda") for k in ("gz1m", "gC", "ge_out")}
-        if not eu:
-            o["gC"] = o["gz1m"]
-        sw2, swc = (torch.full((ns, L * L + L), float("nan"), device="cuda") for _ in range(2))
-        lnp = torch.full((ns + 1, 2 * L), float("nan"), dtype=torch.float64, device="cuda")
-        prs = torch.full((ns, 2), float("nan"), dtype=torch.float64, device="cuda")
-        for call in (0, 1):
-            init, accum = int(call == 0), int(call == 1)
-            if arm == "split":
-                lib.pdg_edge_bwd_w2(E, dst.data_ptr(), gaggr.data_ptr(), P(ge_next), a2m.data_ptr(), a1m.data_ptr(),
-                                    a2e.data_ptr(), a1e.data_ptr(), st_m.data_ptr(), st_e.data_ptr(), None, None,
-                                    lg.data_ptr(), W2T.data_ptr(), o["gz1m"].data_ptr(), None, o["gC"].data_ptr(),
-                                    sw2.data_ptr(), ns, pm.data_ptr(), 5, pe.data_ptr(), 7, init, s)
-                lib.pdg_edge_gout_wc(E, o["gC"].data_ptr(), e.data_ptr(), P(ge_next), WcT.data_ptr(),
-                                     o["ge_out"].data_ptr(), swc.data_ptr(), ns, a2ln.data_ptr(), st_ln.data_ptr(),
-                                     lnp.data_ptr(), lge.data_ptr(), prs.data_ptr(), accum, init, s)
-            else:
-                lib.pdg_edge_bwd_fused(E, dst.data_ptr(), gaggr.data_ptr(), P(ge_next), a2m.data_ptr(), a1m.data_ptr(),
-                                       a2e.data_ptr(), a1e.data_ptr(), st_m.data_ptr(), st_e.data_ptr(), None, None,
-                                       lg.data_ptr(), W2T.data_ptr(), WcT.data_ptr(), e.data_ptr(), a2ln.data_ptr(),
-                                       st_ln.data_ptr(), lge.data_ptr(), o["gz1m"].data_ptr(), o["gC"].data_ptr(),
-                                       o["ge_out"].data_ptr(), sw2.data_ptr(), swc.data_ptr(), ns, lnp.data_ptr(),
-                                       prs.data_ptr(), pm.data_ptr(), 5, pe.data_ptr(), 7, init, accum, s)
-        torch.cuda.synchronize()
-        res[arm] = (o, sw2, swc, lnp[:ns], prs)
-    (o0, w0, c0, l0, p0), (o1, w1, c1, l1, p1) = res["split"], res["fused"]
-    for k in ("gz1m", "gC", "ge_out"):
-        assert torch.equal(o0[k], o1[k]), k
-    assert torch.equal(w0[:, : L * L], w1[:, : L * L]) and torch.equal(c0[:, : L * L], c1[:, : L * L])
-    for a, b in ((w0[:, L * L:], w1[:, L * L:]), (c0[:, L * L:], c1[:, L * L:]), (l0, l1), (p0, p1)):
-        assert torch.isfinite(b).all() and rel(b, a) < 1e-6
-    # the fp64 restatement of the outputs the split pair is checked against elsewhere: ge_out = [ge_next +] gC Wc
-    ref = o0["gC"].double() @ WcT.double().T
-    if eu:
-        ref = ref + ge_next.double()
-    assert rel(o1["ge_out"], ref) < TOL
