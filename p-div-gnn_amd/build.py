@@ -50,10 +50,18 @@ def hipcc() -> str:
 
 def _compile(src: Path, report: bool) -> Path:
     obj = BUILD / (src.stem + ".o")
-    deps = [src] + list(CSRC.glob("*.hpp")) + [CSRC.parent.parent / "include" / "pdivgnn.h"]
+    deps = [src] + sorted(CSRC.glob("*.hpp")) + [CSRC.parent.parent / "include" / "pdivgnn.h"]
     info = src.stem == INFO
-    if obj.exists() and all(obj.stat().st_mtime >= d.stat().st_mtime for d in deps) and not report and not info:
+    # an object is reused only when the CONTENT of its sources and the flags match the stamp written
+    # beside it (modification times let a source restored with an older mtime link a stale object)
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for d in deps:
+        h.update(d.name.encode())
+        h.update(d.read_bytes())
+    stamp = obj.with_suffix(".stamp")
+    if obj.exists() and stamp.exists() and stamp.read_text() == h.hexdigest() and not report and not info:
         return obj
+    stamp.unlink(missing_ok=True)
     cmd = [hipcc(), *FLAGS, "-c", str(src), "-o", str(obj)]
     if info:
         cmd.append(f'-DPDG_SRC_HASH="{source_hash()}"')
@@ -64,6 +72,7 @@ def _compile(src: Path, report: bool) -> Path:
         raise RuntimeError(f"hipcc failed on {src.name}:\n{r.stderr}")
     if report:
         (BUILD / (src.stem + ".res")).write_text(r.stderr)
+    stamp.write_text(h.hexdigest())
     return obj
 
 
