@@ -397,20 +397,29 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_bwd_w2_kernel(
 }
 
 // ============================================================================ Wc path
-template <bool RES>
+// ge_out = [ge_next +] Wc^T gC, dWc += gC^T e (+ b1 sums) and the column sums of the LayerNorm that
+// produced e, in pdg_edge_bwd_w2's layout: 16-row rounds, two rounds of row loads in flight
+// (register sets by round parity, each re-issued for the round after next as soon as its stage has
+// consumed it), double-buffered images, ONE barrier per round.  The products of round k go to an fp32 row
+// tile (parity k & 1) and its whole-row epilogue (ge_out = ge_next + Wc^T gC, the LayerNorm column sums)
+// runs after the NEXT round's barrier, so no second barrier waits for the tile.  The round's residual and
+// xhat rows are held from its stage to that epilogue.  Bitwise the outputs of the round-5 form (32-row
+// rounds, the next round's loads issued after the first of two barriers; removed): the same product chain
+// per element, dWc / b1 sums and the fp32 / fp64 column-sum steps in the same order (a 32-row unit's two
+// epilogues add into one fp32 sum before it is folded into the fp64 one); 125.7 -> 122.0 us per config-2
+// call (same box, EXPERIMENTS §5).
+constexpr int GO_TILE = R16 * OT_STRIDE;   // floats per 16-row output tile
+template <bool RES, bool LN>
 __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
-    const float* __restrict__ gC, const float* __restrict__ e,
-    const float* __restrict__ ge_next,
+    const float* __restrict__ gC, const float* __restrict__ e, const float* __restrict__ ge_next,
     const float* __restrict__ WcT, float* __restrict__ ge_out, float* __restrict__ slabs,
     const float* __restrict__ a2ln, const pdg_ln_stat* __restrict__ stln_p, double* __restrict__ part, int E,
     const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate, int slab_init) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  unsigned char* img_c = sm;                                         // gC
-  unsigned char* img_e = sm + EBW_IMG;                               // e
-  float* t_o = reinterpret_cast<float*>(sm + 2 * EBW_IMG);           // Wc^T gC rows
-  const bool ln = a2ln != nullptr;
+  unsigned char* img = sm;                                           // [parity][gC, e] 16-row images
+  float* tile = reinterpret_cast<float*>(sm + 4 * IMG16);            // [parity] Wc^T gC rows
   LNStat stln;
-  if (ln) stln = *reinterpret_cast<const LNStat*>(stln_p);
+  if (LN) stln = *reinterpret_cast<const LNStat*>(stln_p);
   const int l = lane_id(), w = wave_id();
   const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int oc = 16 * w + 4 * (l >> 4);
@@ -423,80 +432,90 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.f;
   f32x4 bsum = f32x4{0.f, 0.f, 0.f, 0.f};
-  // LayerNorm column sums of this thread's columns 4cg .. 4cg+3 (ln_colsum_kernel, pdg_bwd.hip)
+  const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
   double cs_g[4] = {0, 0, 0, 0}, cs_x[4] = {0, 0, 0, 0};
-  // prefetched rows of the next round, all whole-row (a second slot measured no faster)
-  f32x4 pc[2], pe[2], pres[2], pa2[2];
-  auto issue = [&](int base) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
-      pc[u] = *reinterpret_cast<const f32x4*>(gC + rc);
-      pe[u] = *reinterpret_cast<const f32x4*>(e + rc);
-      if (RES) pres[u] = *reinterpret_cast<const f32x4*>(ge_next + rc);
-      if (ln) pa2[u] = *reinterpret_cast<const f32x4*>(a2ln + rc);   // LayerNorm input of e
-    }
+  f32x4 sg = zero, sx = zero;   // the current 32-row unit's column sums (fp32, as edge_gout_wc_kernel's)
+  const __amdgpu_buffer_rsrc_t rs_out = rows_rsrc(ge_out, r0, r1);
+  f32x4 pc[2], pe[2], pres[2], pa2[2];   // rows in flight, by round parity
+  f32x4 hres[2], hx[2];                  // a staged round's residual and xhat, held to its epilogue
+  auto issue = [&](int s, int base) {
+    const size_t rc = (size_t)clamp_row(base + rg, r1) * L + 4 * cg;
+    pc[s] = *reinterpret_cast<const f32x4*>(gC + rc);
+    pe[s] = *reinterpret_cast<const f32x4*>(e + rc);
+    if (RES) pres[s] = *reinterpret_cast<const f32x4*>(ge_next + rc);
+    if (LN) pa2[s] = *reinterpret_cast<const f32x4*>(a2ln + rc);
   };
-  if (first < r1) issue(first);
-  load_wslice(ws, WcT, w);   // after the first round's row loads: both round trips in flight together
-  for (int base = first; base < r1; base += stride) {
-    f32x4 res[2], a2[2];
+  auto stage = [&](const int s, const int base) {
+    const bool ok = base + rg < r1;
+    const f32x4 c = ok ? pc[s] : zero;
+    bsum += c;
+    img_store4<T16>(img + (2 * s) * IMG16, rg, cg, c);
+    img_store4<T16>(img + (2 * s + 1) * IMG16, rg, cg, ok ? pe[s] : zero);
+    hres[s] = RES ? pres[s] : zero;
+    if (LN) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int r = rg + 16 * u;
-      const bool ok = base + r < r1;
-      const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-      const f32x4 c = ok ? pc[u] : zero;
-      bsum += c;
-      img_store4(img_c, r, cg, c);
-      img_store4(img_e, r, cg, ok ? pe[u] : zero);
-      res[u] = RES ? pres[u] : zero;
-      a2[u] = ln ? pa2[u] : zero;
+      for (int j = 0; j < 4; ++j) hx[s][j] = div_den(pa2[s][j] - stln.mean, stln.den, stln.rstd);
     }
-    __syncthreads();
-    if (base + stride < r1) issue(base + stride);
-    // ---- dWc += gC^T e
-    wgrad_round(acc, img_c, img_e);
-    // ---- Wc^T gC in the product's output layout -> row tile
-    f32x4 d[1][2];
-    const unsigned char* imgs[1] = {img_c};
-    gemm_round<1>(d, ws, imgs);
+    issue(s, base + stride);
+  };
+  auto compute = [&](const int s) {
+    wgrad_round<1, T16>(acc, img + (2 * s) * IMG16, img + (2 * s + 1) * IMG16);
+    f32x4 d[1][1];
+    const unsigned char* imgs[1] = {img + (2 * s) * IMG16};
+    gemm_round<1, 1, T16>(d, ws, imgs);
+    *reinterpret_cast<f32x4*>(tile + s * GO_TILE + (l & 15) * OT_STRIDE + oc) = d[0][0];
+  };
+  auto epilogue = [&](const int s, const int base) {   // round `base` (parity s), staged and computed before
+    const int row = base + rg;
+    const f32x4 dv = *reinterpret_cast<const f32x4*>(tile + s * GO_TILE + rg * OT_STRIDE + 4 * cg);
+    const f32x4 go = RES ? hres[s] + dv : dv;
+    rows_store4(rs_out, row - r0, 4 * cg, go);   // rows outside [r0, r1) dropped by the range
+    if (LN && row >= r0 && row < r1) {
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
-      *reinterpret_cast<f32x4*>(t_o + (16 * nb + (l & 15)) * OT_STRIDE + oc) = d[0][nb];
-    __syncthreads();   // tile complete; the images are free for the next round
-    // ---- ge_out = ge_next + Wc^T gC, whole rows; column sums of the LayerNorm that produced e
-    f32x4 sg = f32x4{0.f, 0.f, 0.f, 0.f}, sx = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int r = rg + 16 * u;
-      const int row = base + r;
-      if (row < r1) {
-        const f32x4 dv = *reinterpret_cast<const f32x4*>(t_o + r * OT_STRIDE + 4 * cg);
-        const f32x4 go = RES ? res[u] + dv : dv;
-        stg4(ge_out + (size_t)row * L + 4 * cg, go);
-        if (ln) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            sg[j] += go[j];
-            sx[j] += go[j] * div_den(a2[u][j] - stln.mean, stln.den, stln.rstd);
-          }
-        }
+      for (int j = 0; j < 4; ++j) {
+        sg[j] += go[j];
+        sx[j] += go[j] * hx[s][j];
       }
     }
-    if (ln) {
+  };
+  auto fold = [&]() {   // a unit's two epilogues done
+    if (LN) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         cs_g[j] += (double)sg[j];
         cs_x[j] += (double)sx[j];
       }
+      sg = zero;
+      sx = zero;
     }
+  };
+  // each set's loads strictly before the next set's, in the loop's re-issue order
+  issue(0, first);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(1, first + R16);
+  __builtin_amdgcn_sched_barrier(0);
+  load_wslice(ws, WcT, w);   // after the first rounds' row loads: the round trips overlap
+  int last = first - stride;   // the last unit's base (none: its rows lie below r0, every store dropped)
+  for (int base = first; base < r1; base += stride) {
+    stage(0, base);
+    __syncthreads();   // round base's images; the previous unit's second tile
+    compute(0);
+    epilogue(1, base - stride + R16);
+    fold();
+    stage(1, base + R16);
+    __syncthreads();
+    compute(1);
+    epilogue(0, base);
+    last = base;
   }
-  __syncthreads();   // the last round's tile reads precede the LDS reuse below
+  __syncthreads();   // the last round's tile
+  epilogue(1, last + R16);
+  fold();
+  __syncthreads();   // the last tile reads precede the LDS reuse below
   slab_accumulate(slabs + (size_t)blockIdx.x * WSLAB, acc, bsum, reinterpret_cast<float*>(sm), slab_init);
-  if (ln) {
-    // block partial = the 16 row groups' column sums, reduced in order through LDS
-    double* red = reinterpret_cast<double*>(sm + 2 * EBW_IMG);
+  if (LN) {
+    // block partial = the 16 row groups' column sums, reduced in order through LDS (after slab_accumulate's 8 KB)
+    double* red = reinterpret_cast<double*>(sm + 16384);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -504,7 +523,7 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_gout_wc_kernel(
       red[rg * 2 * L + L + 4 * cg + j] = cs_x[j];
     }
     __syncthreads();
-    double* row = red + EBW_THREADS / 32 * 2 * L;      // after the row groups' sums
+    double* row = red + EBW_THREADS / 32 * 2 * L;
     for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) {
       double v = 0;
       for (int g = 0; g < EBW_THREADS / 32; ++g) v += red[g * 2 * L + i];
@@ -1693,16 +1712,21 @@ extern "C" int pdg_edge_gout_wc(int n_edges, const float* gC, const float* e, co
   PDG_CHECK_ARG(ge_out != ge_next, "pdg_edge_gout_wc: ge_out must not alias ge_next");
   PDG_CHECK_ARG(!a2ln || (PDG_ALIGNED(a2ln) && st_ln && ln_partials), "pdg_edge_gout_wc: LayerNorm column-sum arguments");
   PDG_CHECK_ARG(!pairs || (a2ln && ln_g), "pdg_edge_gout_wc: pairs need a2ln and ln_g");
-  // LDS: the two images, then (LayerNorm column sums) the row groups' sums + one row + its scratch
-  const size_t shm = 2 * EBW_IMG + ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
-  if (ge_next)
-    hipLaunchKernelGGL(edge_gout_wc_kernel<true>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate,
-                       slab_init);
-  else
-    hipLaunchKernelGGL(edge_gout_wc_kernel<false>, dim3(nslabs), dim3(EBW_THREADS), shm, (hipStream_t)stream, gC, e,
-                       ge_next, WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate,
-                       slab_init);
+  // LDS: two rounds' images (gC, e) + two output tiles; afterwards the slab reduction (8 KB) and the
+  // LayerNorm column sums (row groups + one row + its scratch) from 16 KB on
+  const size_t shm_pipe = 4 * IMG16 + 2 * GO_TILE * sizeof(float);
+  const size_t shm_ln = 16384 + ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
+  const size_t shm = shm_pipe > shm_ln ? shm_pipe : shm_ln;
+  hipStream_t s = (hipStream_t)stream;
+#define PDG_GO2(R, LNF)                                                                                       \
+  hipLaunchKernelGGL((edge_gout_wc_kernel<R, LNF>), dim3(nslabs), dim3(EBW_THREADS), shm, s, gC, e, ge_next,   \
+                     WcT, ge_out, slabs, a2ln, st_ln, ln_partials, n_edges, ln_g, pairs, accumulate, slab_init)
+  if (ge_next) {
+    if (a2ln) PDG_GO2(true, true); else PDG_GO2(true, false);
+  } else {
+    if (a2ln) PDG_GO2(false, true); else PDG_GO2(false, false);
+  }
+#undef PDG_GO2
   PDG_CHECK_LAUNCH("pdg_edge_gout_wc");
   return PDG_OK;
 }

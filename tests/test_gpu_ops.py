@@ -1286,3 +1286,63 @@ def test_nmse_fwd_bwd_equals_fwd_then_bwd(env, sizes, accumulate):
         t, p = gt64[lo:hi], pr64[lo:hi]
         ref = (((t - p) ** 2).sum(0) / ((t - t.mean(0)) ** 2).sum(0)).mean()
         assert abs(float(l1[b]) - float(ref)) <= 1e-5 * abs(float(ref)), (b, float(l1[b]), float(ref))
+
+
+@pytest.mark.parametrize("E,nb", [(77, 37), (4099, 37), (30011, 256), (100000, 256)])
+@pytest.mark.parametrize("res,ln,acc", [(1, 1, 0), (0, 1, 1), (1, 0, 0), (0, 0, 0)])
+def test_edge_gout_wc_vs_fp64(env, E, nb, res, ln, acc):
+    """pdg_edge_gout_wc (16-row rounds, two rounds of loads in flight, one barrier per round, a round's
+    output rows stored after the next round's barrier) against fp64: ge_out = [ge_next +] gC Wc, the dWc
+    slabs (sum over blocks = gC^T e, b1 sums = column sums of gC; written by the first call, accumulated by
+    the second), the LayerNorm column partials (sum of ge_out and of ge_out * xhat per column, written or
+    accumulated) and the pairs; no row written past E (the NaN fill survives); grids of 37 blocks (ragged
+    tails, empty blocks) and 256.  (Round 6 replaced the 32-row two-barrier kernel; the two were bitwise
+    equal on these cases, EXPERIMENTS §5.)"""
+    lib, sh, _ = env
+    s = sh()
+    g = torch.Generator().manual_seed(E + 5 * res + 3 * ln)
+    gC, e, gen = (torch.randn(E, L, generator=g).cuda() for _ in range(3))
+    a2 = torch.relu(torch.randn(E, L, generator=g)).cuda()
+    WcT = (torch.randn(L, L, generator=g) * 0.08).cuda()
+    lg = (torch.randn(L, generator=g) * 0.3 + 1.0).cuda()
+    part = torch.empty(4096, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    tmp = torch.empty(E, L, device="cuda")
+    W2, b2 = lin(L, L)
+    lib.pdg_mlp2_fwd(E, a2.data_ptr(), W2.data_ptr(), b2.data_ptr(), tmp.data_ptr(), part.data_ptr(),
+                     ctypes.byref(n), s)
+    st = finalize(lib, s, part, n.value, E * L)
+    slabs = torch.randn(nb, L * L + L, generator=g).cuda()
+    lnp0 = torch.randn(nb + 1, 256, generator=g).double().cuda()
+    lnp = lnp0.clone()
+    pairs = torch.zeros(2 * nb, dtype=torch.float64, device="cuda")
+    go = torch.full((E + 3, L), float("nan"), device="cuda")
+    for init in (1, 0):   # the first call writes the slabs, the second accumulates
+        assert lib.pdg_edge_gout_wc(E, gC.data_ptr(), e.data_ptr(), gen.data_ptr() if res else None, WcT.data_ptr(),
+                                    go.data_ptr(), slabs.data_ptr(), nb, a2.data_ptr() if ln else None,
+                                    st.data_ptr() if ln else None, lnp.data_ptr() if ln else None,
+                                    lg.data_ptr() if ln else None, pairs.data_ptr() if ln else None, acc, init, s) == 0
+    torch.cuda.synchronize()
+    G, X = gC.double(), e.double()
+    ref = G @ WcT.double().T + (gen.double() if res else 0)
+    assert rel(go[:E].double(), ref) < 1e-6, rel(go[:E].double(), ref)
+    assert bool(go[E:].isnan().all())
+    tot = slabs.double().sum(0)
+    assert rel(tot[:L * L].view(L, L), 2 * G.T @ X) < 1e-6
+    assert rel(tot[L * L:], 2 * G.sum(0)) < 1e-6
+    if ln:
+        sd = stat_from(st)
+        mean, den = sd["mean"], sd["den"]
+        xhat = (a2.double() - mean) / den
+        cols = torch.cat([ref.sum(0), (ref * xhat).sum(0)])
+        got = lnp[:nb].sum(0) - (lnp0[:nb].sum(0) if acc else 0)
+        assert rel(got, (2 if acc else 1) * cols) < 1e-5, rel(got, (2 if acc else 1) * cols)
+        # the pairs are the last call's (of its own block rows, accumulated or not): against the written rows
+        # to rounding, and against fp64 at 5e-5 (the g-weighted column sums cancel: the products' accumulated
+        # rounding over 1e5 rows is ~1e-5 of the pair at E = 100,000)
+        pr = pairs.view(nb, 2).sum(0)
+        w = lg.double()
+        if not acc:
+            rows = lnp[:nb]
+            assert rel(pr, torch.stack([(rows[:, :L] * w).sum(), (rows[:, L:] * w).sum()])) < 1e-12
+        assert rel(pr, torch.stack([(cols[:L] * w).sum(), (cols[L:] * w).sum()])) < 5e-5
