@@ -108,17 +108,24 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
   const int r = l & 15, q = l >> 4;
   const int oc = 16 * w + 4 * q;
   const int j = threadIdx.x & 31, rr = threadIdx.x >> 5;   // the thread's staged row chunk
+  // no memory operation of the loop is conditional (rows past N are clamped on load and zeroed when
+  // staged, stores past N dropped by the buffer range), so its waits count loads: a load or store on a
+  // branch made the compiler wait for every outstanding load AND store (vmcnt(0)) once per tile
   f32x4 va, vx;
+  bool vok;
   auto fetch = [&](int t) {
     const int node = t * TILE + rr;
-    const bool ok = node < N;
-    va = ok ? reinterpret_cast<const f32x4*>(aggr + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
-    vx = ok ? reinterpret_cast<const f32x4*>(x + (size_t)node * L)[j] : f32x4{0.f, 0.f, 0.f, 0.f};
+    vok = node < N;
+    const size_t o = (size_t)clamp_row(node, N) * L;
+    va = reinterpret_cast<const f32x4*>(aggr + o)[j];
+    vx = reinterpret_cast<const f32x4*>(x + o)[j];
   };
   auto stage = [&](int buf) {
-    x6_store4<NN_T16>(xin + (2 * buf) * NN_IMG, rr, j, va);
-    x6_store4<NN_T16>(xin + (2 * buf + 1) * NN_IMG, rr, j, vx);
+    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
+    x6_store4<NN_T16>(xin + (2 * buf) * NN_IMG, rr, j, vok ? va : zero);
+    x6_store4<NN_T16>(xin + (2 * buf + 1) * NN_IMG, rr, j, vok ? vx : zero);
   };
+  const __amdgpu_buffer_rsrc_t rs_a1 = rows_rsrc(a1_out, 0, N), rs_a2 = rows_rsrc(a2_out, 0, N);
 #pragma unroll
   for (int k = 0; k < 2; ++k)
     if (nu_tile(k) < ntiles) {
@@ -136,8 +143,7 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
   for (int i = 0;; ++i) {
     const int tile = nu_tile(i);
     if (tile >= ntiles) break;   // uniform across the block
-    const bool ahead = nu_tile(i + 2) < ntiles;
-    if (ahead) fetch(nu_tile(i + 2));
+    fetch(nu_tile(i + 2));   // past the last tile: clamped rows, staged into a buffer no tile reads
     const int row = tile * TILE + r;
     // layer 1: a1 = relu(W1a aggr + W1b x + b1), the aggr chunks first
     f32x4 d1[1] = {{0.f, 0.f, 0.f, 0.f}};
@@ -147,7 +153,7 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
 #pragma unroll
     for (int c = 0; c < 4; ++c) a1[c] = fmaxf(d1[0][c] + bias1[c], 0.f);
     x6_store4<NN_T16>(a1i + (i & 1) * NN_IMG, r, 4 * w + q, a1);
-    if (row < N && a1_out) stg4(a1_out + (size_t)row * L + oc, a1);
+    rows_store4(rs_a1, row, oc, a1);   // a1_out NULL (inference): an empty range
     __syncthreads();   // the a1 image is complete; the input buffer of tile i - 1 is free
     // layer 2: a2 = relu(W2 a1 + b2) + LayerNorm partials
     f32x4 d2[1] = {{0.f, 0.f, 0.f, 0.f}};
@@ -155,8 +161,8 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
     f32x4 a2;
 #pragma unroll
     for (int c = 0; c < 4; ++c) a2[c] = fmaxf(d2[0][c] + bias2[c], 0.f);
+    rows_store4(rs_a2, row, oc, a2);
     if (row < N) {
-      stg4(a2_out + (size_t)row * L + oc, a2);
       const float p1 = (a2[0] + a2[1]) + (a2[2] + a2[3]);
       const float p2 = (a2[0] * a2[0] + a2[1] * a2[1]) + (a2[2] * a2[2] + a2[3] * a2[3]);
       s1 += (double)p1;
@@ -164,7 +170,7 @@ __global__ __launch_bounds__(64 * NU_COMPUTE, 1) void node_net_x6_kernel(
     }
     // tile i + 2 into the buffer layer 1 of tile i - 1 read (before the previous barrier); read after
     // the next one.  After layer 2 its loads have the whole tile to land.
-    if (ahead) stage((i + 2) % 3);
+    stage((i + 2) % 3);
   }
   __shared__ double red[2 * NU_COMPUTE];
   block_sum2(s1, s2, red);
@@ -182,6 +188,8 @@ extern "C" int pdg_node_net(int n_nodes, const float* aggr, const float* x, cons
                             const float* Wn2, const float* bn2, float* a1n, float* a2n, double* partials,
                             int* nparts, void* stream) {
   PDG_CHECK_ARG(n_nodes > 0, "pdg_node_net: n_nodes must be > 0");
+  // the output buffer ranges span all rows: byte sizes below 2^31
+  PDG_CHECK_ARG(n_nodes < (1 << 22), "pdg_node_net: at most 4,194,303 nodes per call");
   PDG_CHECK_ARG(aggr && x && a2n, "pdg_node_net: aggr, x and a2n are required");
   PDG_CHECK_ARG(PDG_ALIGNED(aggr) && PDG_ALIGNED(x) && PDG_ALIGNED(Wn1) && PDG_ALIGNED(Wn2) && PDG_ALIGNED(a2n) &&
                     PDG_ALIGNED(a1n) && PDG_ALIGNED(bn1) && PDG_ALIGNED(bn2),
