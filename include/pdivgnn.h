@@ -319,6 +319,16 @@ int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, 
                       const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
                       const float* b2, float* a1m, float* a2m, float* a1e, float* a2e, double* part_m,
                       double* part_e, int with_edge_update, int nblocks, void* stream);
+/* Inference edge forward (no layer-1 outputs: nothing reads them without a backward): pdg_edge_fwd_coop's
+ * e_out, a2m, a2e (bitwise) and LayerNorm partials (the rows added in another order) from 16-row rounds with
+ * one barrier per round -- the C product of round k beside the two W2 products of round k - 1, the gathers
+ * one round ahead, two register sets of row loads (pdg_ebw.hip).  Arguments as pdg_edge_fwd_coop's without
+ * a1m / a1e. */
+int pdg_edge_fwd_infer(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                       const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
+                       const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
+                       const float* b2, float* a2m, float* a2e, double* part_m, double* part_e,
+                       int with_edge_update, int nblocks, void* stream);
 int pdg_edge_bwd(int n_edges, const int* dst, const float* gaggr, const float* ge_next,
                  const float* a2m, const float* a1m, const float* a2e, const float* a1e,
                  const pdg_ln_stat* st_m, const pdg_ln_stat* st_e, const pdg_ln_bwd* lb_m,

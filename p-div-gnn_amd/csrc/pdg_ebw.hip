@@ -814,6 +814,208 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_coop_kernel(
   }
 }
 
+// ============================================================================ edge forward, inference
+// pdg_edge_fwd_coop's work without the layer-1 outputs (inference: nothing reads them) in 16-row rounds
+// with ONE barrier per round, the rounds' two product phases
+// overlapped (the layout of pdg_edge_bwd_w2: two register sets of row loads by round parity, double-
+// buffered images).  After the barrier that completes round k's e image and round k-1's a1 images, a wave
+// runs, for its 16 features:
+//   C_k = Wc e_k (unbiased bf16x6, gemm_x6f) and the two W2 products of round k-1 (gemm_round): three
+//   independent MFMA chains in one phase, where pdg_edge_fwd_coop runs them in two phases with a
+//   barrier between; then a2_{k-1} (+ LayerNorm partials) into its row tiles; a1_k = relu(C_k + b1 +
+//   gathered P / Q rows) into round k's a1 images (the gathers were issued one round earlier, so the
+//   products of the whole phase cover their latency); round k+1's gathers; the stage of round k+1 (its
+//   rows loaded two rounds earlier: LayerNorm + residual, e_{k+1} stored and imaged, the set re-issued for
+//   round k+3); the stores of a2_{k-2} from its tiles (written before the barrier).
+// Per output element the MFMA chains are those of pdg_edge_fwd_coop (bitwise the same e_t, a2); the
+// LayerNorm partial sums visit the rows in another order.  LDS: e images 2 x 12 KB, a1 images 4 x 12 KB,
+// a2 tiles 4 x 8.25 KB, Wc lo terms 16 KB = 121 KB.  Inference edge forward 494 -> 446 us (edge update)
+// and 344 -> 312 us (message only) per 614k-edge call; in training (the a1 rows stored through tiles as
+// well) it measured no faster than pdg_edge_fwd_coop (EXPERIMENTS §5), which stays the training kernel.
+constexpr int EP_TILE = R16 * OT_STRIDE;          // floats per 16-row fp32 tile
+template <bool RES, bool EU, bool X>
+__global__ __launch_bounds__(EBW_THREADS, 1) void edge_fwd_infer_kernel(
+    int E, const float* __restrict__ a2p, const pdg_ln_stat* __restrict__ stp, const float* __restrict__ lg,
+    const float* __restrict__ lb, const float* __restrict__ eres, float* __restrict__ eout,
+    const int* __restrict__ src, const int* __restrict__ dst, const float* __restrict__ P,
+    const float* __restrict__ Q, const float* __restrict__ W1, const float* __restrict__ b1,
+    const float* __restrict__ W2, const float* __restrict__ b2, float* __restrict__ a2m, float* __restrict__ a2e,
+    double* __restrict__ part_m, double* __restrict__ part_e) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  unsigned char* img_e = sm;                                    // [2] e images (round parity)
+  unsigned char* img_a = sm + 2 * IMG16;                        // [2][2] a1 images: [parity][m, e]
+  float* t_a2 = reinterpret_cast<float*>(sm + 6 * IMG16);       // [2][2] a2 tiles: [parity][m, e]
+  unsigned char* wlo = reinterpret_cast<unsigned char*>(t_a2 + 4 * EP_TILE);
+  const int l = lane_id(), w = wave_id();
+  const int cg = threadIdx.x & 31, rg = threadIdx.x >> 5;      // the thread's staged row rg (0..15)
+  const int oc = 16 * w + 4 * (l >> 4), pr = l & 15;            // this lane's product features and row
+  int r0, r1, first, stride;   // 32-row units (rounds base and base + 16), the next unit `stride` rows on
+  row_schedule(X, E, r0, r1, first, stride);
+  const int units = first < r1 ? (r1 - 1 - first) / stride + 1 : 0;
+  const int K = 2 * units;                                       // rounds of this block
+  auto rbase = [&](int k) { return first + (k >> 1) * stride + R16 * (k & 1); };
+  WSlice wsc, ws2;
+  const LNStat st = *reinterpret_cast<const LNStat*>(stp);
+  const f32x4 g4 = *reinterpret_cast<const f32x4*>(lg + 4 * cg), bb4 = *reinterpret_cast<const f32x4*>(lb + 4 * cg);
+  const f32x4 b1o = *reinterpret_cast<const f32x4*>(b1 + oc), b2o = *reinterpret_cast<const f32x4*>(b2 + oc);
+  double sm1 = 0, sm2 = 0, se1 = 0, se2 = 0;
+  // row outputs through range-checked buffer stores (no conditional memory operation in the loop)
+  const __amdgpu_buffer_rsrc_t rs_e = rows_rsrc(eout, r0, r1);
+  const __amdgpu_buffer_rsrc_t rs_a2m = rows_rsrc(a2m, r0, r1);
+  const __amdgpu_buffer_rsrc_t rs_a2e = rows_rsrc(EU ? a2e : nullptr, r0, r1);
+  // two register sets of prefetched rows (round parity): the staged row's a2_prev / e_prev chunk and the
+  // product row's dst / src
+  f32x4 xa[2], xr[2];
+  int dq[2], sq[2];
+  auto issue = [&](int s, int k) {
+    const int base = rbase(k);
+    const size_t rc = (size_t)clamp_row(base + rg, r1) * L + 4 * cg;
+    xa[s] = *reinterpret_cast<const f32x4*>(a2p + rc);
+    if (RES) xr[s] = *reinterpret_cast<const f32x4*>(eres + rc);
+    const int q = clamp_row(base + pr, r1);
+    dq[s] = dst[q];
+    sq[s] = src[q];
+  };
+  f32x4 gpd, gqs, gps, gqd;   // the next round's gathered P / Q rows at this lane's features
+  auto gather = [&](int s) {
+    gpd = *reinterpret_cast<const f32x4*>(P + (size_t)dq[s] * PQ_LD + pq_col(oc));
+    gqs = *reinterpret_cast<const f32x4*>(Q + (size_t)sq[s] * PQ_LD + pq_col(oc));
+    if (EU) {
+      gps = *reinterpret_cast<const f32x4*>(P + (size_t)sq[s] * PQ_LD + pq_col(oc));
+      gqd = *reinterpret_cast<const f32x4*>(Q + (size_t)dq[s] * PQ_LD + pq_col(oc));
+    }
+  };
+  auto stage = [&](int s, int k) {   // round k's e rows from set s into e image s; the set re-issued for k + 2
+    const int base = rbase(k);
+    const bool ok = base + rg < r1;
+    f32x4 e;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {   // ln_apply (pdg_fwd.hip), element by element
+      float y = div_den(xa[s][j] - st.mean, st.den, st.rstd) * g4[j] + bb4[j];
+      if (RES) y += xr[s][j];
+      e[j] = y;
+    }
+    rows_store4_nt(rs_e, base + rg - r0, 4 * cg, e);
+    img_store4<T16>(img_e + s * IMG16, rg, cg, ok ? e : f32x4{0.f, 0.f, 0.f, 0.f});
+    issue(s, k + 2);
+  };
+  // the a1 images of "round -1" (read by the first phase's W2 products, whose rows are all dropped) zeroed
+  for (int i = threadIdx.x; i < 4 * IMG16 / 16; i += EBW_THREADS)
+    reinterpret_cast<f32x4*>(img_a)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  issue(0, 0);
+  __builtin_amdgcn_sched_barrier(0);
+  issue(1, 1);
+  __builtin_amdgcn_sched_barrier(0);
+  load_wslice(wsc, W1 + 2 * L, w, 3 * L);
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) *reinterpret_cast<bf16x8*>(wlo + ((2 * w + ks) * 64 + l) * 16) = wsc.a[ks][2];
+  load_wslice(ws2, W2, w);
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      if (p < 2 || ks >= 2) pin_vgpr(wsc.a[ks][p]);
+      pin_vgpr(ws2.a[ks][p]);
+    }
+  pin_vgpr(b1o);
+  pin_vgpr(b2o);
+  gather(0);
+  __builtin_amdgcn_sched_barrier(0);
+  stage(0, 0);
+  // one round; its parity S is a compile-time constant (the loop runs rounds in pairs): register sets indexed
+  // by a run-time parity became selects that waited for both sets' loads (vmcnt(0)) every round
+  auto round = [&](auto S, const int k) {
+    constexpr int s = decltype(S)::value, sp = s ^ 1;   // round k's buffers / set, round k +- 1's
+    const int basep = rbase(k - 1);
+    __syncthreads();   // e image k, a1 images k - 1, the a2 / a1 tiles of rounds k - 2 / k - 1 complete
+    // ---- C_k = Wc e_k and W2 a1_{k-1} for both evaluations: three independent MFMA chains
+    f32x4 dc[1] = {{0.f, 0.f, 0.f, 0.f}};
+    {
+      WSlice wc = wsc;   // the lo terms of K chunks 0-1 from LDS
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) wc.a[ks][2] = *reinterpret_cast<const bf16x8*>(wlo + ((2 * w + ks) * 64 + l) * 16);
+      gemm_x6f<1, T16, true>(dc, wc, img_e + s * IMG16);
+    }
+    constexpr int NI = EU ? 2 : 1;
+    f32x4 d2[NI][1];
+    const unsigned char* ia[NI];
+    ia[0] = img_a + (2 * sp) * IMG16;
+    if (EU) ia[NI - 1] = img_a + (2 * sp + 1) * IMG16;
+    gemm_round<NI, 1, T16>(d2, ws2, ia);
+    // ---- a2_{k-1} into its tiles (parity sp) and the LayerNorm partials of its valid rows
+    {
+      const bool ok = k > 0 && basep + pr < r1;
+#pragma unroll
+      for (int u = 0; u < NI; ++u) {
+        f32x4 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = fmaxf(d2[u][0][j] + b2o[j], 0.f);
+        *reinterpret_cast<f32x4*>(t_a2 + (2 * sp + u) * EP_TILE + pr * OT_STRIDE + oc) = a;
+        if (ok) {
+          const double p1 = (double)((a[0] + a[1]) + (a[2] + a[3]));
+          const double p2 = (double)((a[0] * a[0] + a[1] * a[1]) + (a[2] * a[2] + a[3] * a[3]));
+          if (u) { se1 += p1; se2 += p2; } else { sm1 += p1; sm2 += p2; }
+        }
+      }
+    }
+    // ---- a1_k = relu(C_k + b1 + gathered rows) into round k's a1 images
+    {
+      f32x4 am, ae;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float c = dc[0][j] + b1o[j];
+        am[j] = fmaxf((c + gpd[j]) + gqs[j], 0.f);
+        if (EU) ae[j] = fmaxf((c + gps[j]) + gqd[j], 0.f);
+      }
+      img_store4<T16>(img_a + (2 * s) * IMG16, pr, 4 * w + (l >> 4), am);
+      if (EU) img_store4<T16>(img_a + (2 * s + 1) * IMG16, pr, 4 * w + (l >> 4), ae);
+    }
+    // ---- round k + 1: its gathers (indices in set sp, before the stage re-issues the set), its stage
+    __builtin_amdgcn_sched_barrier(0);
+    gather(sp);
+    __builtin_amdgcn_sched_barrier(0);
+    stage(sp, k + 1);
+    // ---- the stores of a2_{k-2} (tiles of parity s), every tile read first
+    {
+      const int base2 = rbase(k - 2);
+      f32x4 v[2];
+      v[0] = *reinterpret_cast<const f32x4*>(t_a2 + (2 * s) * EP_TILE + rg * OT_STRIDE + 4 * cg);
+      if (EU) v[1] = *reinterpret_cast<const f32x4*>(t_a2 + (2 * s + 1) * EP_TILE + rg * OT_STRIDE + 4 * cg);
+      // rounds before the first (k < 2) lie below r0: their stores are dropped
+      rows_store4_nt(rs_a2m, (k >= 2 ? base2 : r0 - R16) + rg - r0, 4 * cg, v[0]);
+      if (EU) rows_store4_nt(rs_a2e, (k >= 2 ? base2 : r0 - R16) + rg - r0, 4 * cg, v[1]);
+    }
+  };
+  for (int k = 0; k < K; k += 2) {   // K = 2 x units is even
+    round(std::integral_constant<int, 0>{}, k);
+    round(std::integral_constant<int, 1>{}, k + 1);
+  }
+  round(std::integral_constant<int, 0>{}, K);   // the last round's products, stores of the last two rounds
+  {   // the last round's a2 rows (round K - 1, tiles of parity (K - 1) & 1)
+    __syncthreads();
+    constexpr int sl = 1;   // round K - 1 (K even)
+    f32x4 v0 = *reinterpret_cast<const f32x4*>(t_a2 + (2 * sl) * EP_TILE + rg * OT_STRIDE + 4 * cg), v1;
+    if (EU) v1 = *reinterpret_cast<const f32x4*>(t_a2 + (2 * sl + 1) * EP_TILE + rg * OT_STRIDE + 4 * cg);
+    const int bl = K > 0 ? rbase(K - 1) : r0 - R16;
+    rows_store4_nt(rs_a2m, bl + rg - r0, 4 * cg, v0);
+    if (EU) rows_store4_nt(rs_a2e, bl + rg - r0, 4 * cg, v1);
+  }
+  double* red = reinterpret_cast<double*>(sm);
+  __syncthreads();
+  block_sum2(sm1, sm2, red);
+  if (threadIdx.x == 0) {
+    part_m[2 * blockIdx.x] = sm1;
+    part_m[2 * blockIdx.x + 1] = sm2;
+  }
+  if (EU) {
+    block_sum2(se1, se2, red + 32);
+    if (threadIdx.x == 0) {
+      part_e[2 * blockIdx.x] = se1;
+      part_e[2 * blockIdx.x + 1] = se2;
+    }
+  }
+}
+
 // ============================================================================ edge encoder forward
 // The edge encoder (models.py:264-275, input 1 -> 128 -> 128 + the LayerNorm partials of the
 // output) in the cooperative layout: a1 = relu(w0 e + b0) formed per element (encoder_kernel's
@@ -1981,6 +2183,46 @@ extern "C" int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln
   return PDG_OK;
 }
 
+extern "C" int pdg_edge_fwd_infer(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
+                                  const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
+                                  const float* P, const float* Q, const float* W1, const float* b1, const float* W2,
+                                  const float* b2, float* a2m, float* a2e, double* part_m, double* part_e,
+                                  int with_edge_update, int nblocks, void* stream) {
+  PDG_CHECK_ARG(n_edges > 0, "pdg_edge_fwd_infer: n_edges must be > 0");
+  PDG_CHECK_ARG(nblocks > 0 && nblocks <= MAX_BLOCKS, "pdg_edge_fwd_infer: bad nblocks");
+  PDG_CHECK_ARG(a2_prev && st && ln_g && ln_b && e_out && src && dst && P && Q && W1 && b1 && W2 && b2 && a2m &&
+                    part_m,
+                "pdg_edge_fwd_infer: null argument");
+  PDG_CHECK_ARG(PDG_ALIGNED(a2_prev) && PDG_ALIGNED(e_out) && PDG_ALIGNED(P) && PDG_ALIGNED(Q) &&
+                    PDG_ALIGNED(a2m) && PDG_ALIGNED(W1) && PDG_ALIGNED(W2) && PDG_ALIGNED(b1) && PDG_ALIGNED(b2) &&
+                    PDG_ALIGNED(ln_g) && PDG_ALIGNED(ln_b) && (!e_res || PDG_ALIGNED(e_res)),
+                "pdg_edge_fwd_infer: misaligned pointer");
+  PDG_CHECK_ARG(!with_edge_update || (a2e && part_e && PDG_ALIGNED(a2e)),
+                "pdg_edge_fwd_infer: edge-update outputs missing or misaligned");
+  const bool xcd = nblocks == XCD_GRID;
+  const size_t shm = 6 * IMG16 + 4 * EP_TILE * sizeof(float) + 2 * EBW_WAVES * 64 * 16;
+  hipStream_t s = (hipStream_t)stream;
+#define PDG_EI_X(R, U, X)                                                                                     \
+  hipLaunchKernelGGL((edge_fwd_infer_kernel<R, U, X>), dim3(nblocks), dim3(EBW_THREADS), shm, s, n_edges, a2_prev, \
+                     st, ln_g, ln_b, e_res, e_out, src, dst, P, Q, W1, b1, W2, b2, a2m, a2e, part_m, part_e)
+#define PDG_EI(R, U)             \
+  do {                           \
+    if (xcd) {                   \
+      PDG_EI_X(R, U, true);      \
+    } else {                     \
+      PDG_EI_X(R, U, false);     \
+    }                            \
+  } while (0)
+  if (e_res) {
+    if (with_edge_update) PDG_EI(true, true); else PDG_EI(true, false);
+  } else {
+    if (with_edge_update) PDG_EI(false, true); else PDG_EI(false, false);
+  }
+#undef PDG_EI
+#undef PDG_EI_X
+  PDG_CHECK_LAUNCH("pdg_edge_fwd_infer");
+  return PDG_OK;
+}
 
 extern "C" int pdg_node_enc_fwd(int n_nodes, const float* x_in, const float* w0, const float* b0, const float* W2,
                                 const float* b2, float* a1, float* a2, double* partials, int nblocks, void* stream) {

@@ -76,6 +76,9 @@ VARIANTS = {
     # edge forward in the block-cooperative layout (pdg_edge_fwd_coop; 240 -> 230 us per call at config 2)
     # instead of pdg_edge_fwd
     "coop_fwd": ("PDG_EDGE_FWD_COOP", True),
+    # inference (no backward): the edge forward of at least INFER_PIPE_MIN_EDGES edges in 16-row rounds with one
+    # barrier per round (pdg_edge_fwd_infer; bitwise the same rows): 494 -> 446 us per 614k-edge call
+    "fwd_infer_pipe": ("PDG_EDGE_FWD_INFER", True),
     # the backward's input gradient of x (gP, gQ -> gx) in bf16x6 (pdg_gemm_sum2_coop) instead of the fp32-MFMA
     # pdg_gemm_sum2_rw
     "gsum2_coop": ("PDG_GSUM2_COOP", True),
@@ -93,6 +96,11 @@ VARIANTS = {
     # pdg_edge_enc_fwd blocks per CU (104 VGPRs, 41 KB LDS per 8-wave block)
     "enc_blocks_per_cu": ("PDG_ENC_BLOCKS_PER_CU", 2),
 }
+
+
+# pdg_edge_fwd_infer from this many edges on (alone, 256 blocks: +1.5 us against pdg_edge_fwd_coop at 2.5k - 11k
+# edges, equal at 27k, -3 us at 59k, -10 % from 150k edges on; tools/diag/efwd_sweep.py)
+INFER_PIPE_MIN_EDGES = 32768
 
 
 def _parse_variant(name: str, raw: str):
@@ -199,6 +207,7 @@ class EPDEngine:
         self.pq_first = var["pq_first"]
         self.gz1e_from_gc = var["gz1e_from_gc"]
         self.coop_fwd = var["coop_fwd"]
+        self.fwd_infer_pipe = var["fwd_infer_pipe"]
         self.node_enc_coop = var["node_enc_coop"]
         self.decoder_coop = var["decoder_coop"]
         # the P / Q layout the library's node pre-pass writes and its cooperative edge forward reads
@@ -348,7 +357,13 @@ class EPDEngine:
             a1m = self._empty(E, L) if need_grad else None   # layer-1 outputs: backward only
             a2e = self._empty(E, L) if eu else None
             a1e = self._empty(E, L) if (eu and need_grad) else None
-            if E and self.coop_fwd:
+            if E and self.coop_fwd and not need_grad and self.fwd_infer_pipe and E >= INFER_PIPE_MIN_EDGES:
+                self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_infer, E, _p(a2e_prev), ste_prev,
+                        _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm),
+                        _p(W1), _p(b1), _p(W2), _p(b2), _p(a2m), _p(a2e), _p(self._part_a), _p(self._part_b), int(eu),
+                        self._nslabs_e, s)
+                self._nparts.value = self._nslabs_e
+            elif E and self.coop_fwd:
                 self._t("edge_fwd" if eu else "edge_fwd_last", lib.pdg_edge_fwd_coop, E, _p(a2e_prev), ste_prev,
                         _p(ge_prev), _p(be_prev), _p(e_prev), _p(e_t), _p(plan.src), _p(plan.dst), _p(Pm), _p(Qm),
                         _p(W1), _p(b1), _p(W2), _p(b2), _p(a1m), _p(a2m), _p(a1e), _p(a2e), _p(self._part_a),

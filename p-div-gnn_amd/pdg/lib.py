@@ -78,6 +78,7 @@ SIGNATURES: dict[str, list] = {
     "pdg_wgrad_reduce_batch": [I, P, P, P, P, P, P, P],
     "pdg_wgrad_segments_batch": [I, P, P, P, P, P, I, P],
     "pdg_edge_fwd_coop": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
+    "pdg_edge_fwd_infer": [I, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, P],
     "pdg_edge_enc_fwd": [I, P, P, P, P, P, P, P, I, P],
     "pdg_node_enc_fwd": [I, P, P, P, P, P, P, P, P, I, P],
     "pdg_gemm_sum2_coop": [I, P, P, P, P, P, P, P, P, P, P, P, I, I, P],

@@ -1346,3 +1346,56 @@ def test_edge_gout_wc_vs_fp64(env, E, nb, res, ln, acc):
             rows = lnp[:nb]
             assert rel(pr, torch.stack([(rows[:, :L] * w).sum(), (rows[:, L:] * w).sum()])) < 1e-12
         assert rel(pr, torch.stack([(cols[:L] * w).sum(), (cols[L:] * w).sum()])) < 5e-5
+
+
+
+
+@pytest.mark.parametrize("E,nb", [(77, 37), (4099, 37), (30011, 256), (100000, 256)])
+@pytest.mark.parametrize("eu,res", [(1, 1), (0, 1), (1, 0), (0, 0)])
+def test_edge_fwd_infer_matches_coop(env, E, nb, eu, res):
+    """pdg_edge_fwd_infer (inference: 16-row rounds, one barrier per round, the C product of round k beside the
+    W2 products of round k - 1) against pdg_edge_fwd_coop without layer-1 outputs on the same inputs: e_t, a2m /
+    a2e bitwise (the same MFMA chain per element), no row written past E (the NaN fill survives), the
+    LayerNorm partials' totals to 1e-12 (the same fp64 terms in another order); grids of 37 blocks (contiguous
+    ranges, ragged tails, empty blocks) and 256 (XCD-interleaved units)."""
+    lib, sh, _ = env
+    s = sh()
+    N = max(E // 6, 40)
+    g = torch.Generator().manual_seed(E + 7 * eu + 3 * res)
+    src = torch.randint(0, N, (E,), generator=g).int().cuda()
+    dst = torch.sort(torch.randint(0, N, (E,), generator=g)).values.int().cuda()
+    a2p, eres = torch.relu(rnd(E, L)), rnd(E, L)
+    Pn, Qn = rnd(N, L), rnd(N, L)
+    W1, b1 = lin(L, 3 * L)
+    W2, b2 = lin(L, L)
+    lg, lbv = rnd(L) * 0.3 + 1.0, rnd(L) * 0.1
+    part = torch.empty(4096, dtype=torch.float64, device="cuda")
+    n = ctypes.c_int(0)
+    tmp = torch.empty(E, L, device="cuda")
+    lib.pdg_mlp2_fwd(E, a2p.data_ptr(), W2.data_ptr(), b2.data_ptr(), tmp.data_ptr(), part.data_ptr(),
+                     ctypes.byref(n), s)
+    st = finalize(lib, s, part, n.value, E * L)
+    pq = PQ.of(lib, Pn, Qn)
+    outs = {}
+    for infer in (False, True):
+        o = {k: torch.full((E + 3, L), float("nan"), device="cuda") for k in ("e", "a2m", "a2e")}
+        pm = torch.zeros(2 * nb, dtype=torch.float64, device="cuda")
+        pe = torch.zeros(2 * nb, dtype=torch.float64, device="cuda")
+        head = (E, a2p.data_ptr(), st.data_ptr(), lg.data_ptr(), lbv.data_ptr(), eres.data_ptr() if res else None,
+                o["e"].data_ptr(), src.data_ptr(), dst.data_ptr(), pq.p, pq.q, W1.data_ptr(), b1.data_ptr(),
+                W2.data_ptr(), b2.data_ptr())
+        tail = (pm.data_ptr(), pe.data_ptr() if eu else None, eu, nb, s)
+        a2e = o["a2e"].data_ptr() if eu else None
+        if infer:
+            assert lib.pdg_edge_fwd_infer(*head, o["a2m"].data_ptr(), a2e, *tail) == 0
+        else:
+            assert lib.pdg_edge_fwd_coop(*head, None, o["a2m"].data_ptr(), None, a2e, *tail) == 0
+        torch.cuda.synchronize()
+        outs[infer] = (o, pm.view(nb, 2).sum(0), pe.view(nb, 2).sum(0))
+    (o0, pm0, pe0), (o1, pm1, pe1) = outs[False], outs[True]
+    for k in ["e", "a2m"] + (["a2e"] if eu else []):
+        assert torch.equal(o0[k][:E], o1[k][:E]), (k, rel(o1[k][:E], o0[k][:E]))
+        assert bool(o1[k][E:].isnan().all()), k
+    assert float((pm1 - pm0).abs().max()) <= 1e-12 * float(pm0.abs().max())
+    if eu:
+        assert float((pe1 - pe0).abs().max()) <= 1e-12 * float(pe0.abs().max())
