@@ -60,7 +60,10 @@ def _cfg_glob(glob: str, config: int) -> str:
     return glob if config == 2 else glob.replace(".json", f"_c{config}.json")
 TREE_GLOBS = ("p-div-gnn_amd/pdg/libpdivgnn_hip.so", "p-div-gnn_amd/csrc/*.hip", "p-div-gnn_amd/csrc/*.hpp", "include/*.h", "p-div-gnn_amd/pdg/*.py",
               "p-div-gnn_amd/gnn_local_stress/*.py", "bench.py")
-PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_kernel<true, true>"),
+# the edge forward's training kernel, its inference kernel (calls of >= 32k edges without a backward) and the
+# LDS-weight reference
+PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd_infer_kernel<true, true",
+                          "void edge_fwd_kernel<true, true>"),
              "edge_bwd": "void edge_bwd_kernel<true>",
              "segment_sum": ("segment_sum_kernel",), "node_net": ("node_net_x6_kernel", "node_net_pair_kernel", "node_net_kernel"),
              # the edge-update steps' instantiation (gz1e formed as gC - gz1m); the last step's is <false>
@@ -68,7 +71,7 @@ PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd
              "wgrad_W2": "wgrad_x6_kernel",
              # the edge-update instantiations
              "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
-             "edge_gout": "void edge_gout_wc_kernel<true>",
+             "edge_gout": ("void edge_gout_wc_kernel<true, true>", "void edge_gout_wc_kernel<true>"),
              "node_bwd": "node_bwd_coop_kernel", "node_pq": "void node_pq_x6_kernel<true>",
              "gemm_sum2": "void gemm_sum2_coop_kernel<true>", "wgrad_pairs": "void wgrad_x6_pair2_kernel"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md

@@ -126,3 +126,17 @@ def test_counter_files_are_per_config(tmp_path, monkeypatch):
     path, reason = bench.pmc_file("aaaa", config=3)
     assert path is None and "_c3" in reason
     assert bench.load_pmc(True, c5)["edge_fwd"] == 3_000_000_000
+
+
+def test_pmc_names_cover_the_shipped_instantiations(tmp_path):
+    """The counter lookup finds the kernels the engine launches: the inference edge forward (config 5 runs no
+    cooperative edge forward) and the Wc pass's <RES, LN> instantiation."""
+    p = tmp_path / "pmc.json"
+    p.write_text(json.dumps({
+        "_meta": {"tree": "aaaa"},
+        "void edge_fwd_infer_kernel<true, true, true>(int, ...)": {"total": 1.75e9},
+        "void edge_gout_wc_kernel<true, true>(float const*, ...)": {"total": 6.5e8},
+        "void edge_gout_wc_kernel<false, true>(float const*, ...)": {"total": 1.0}}))
+    pmc = bench.load_pmc(True, p)
+    assert pmc["edge_fwd"] == 1_750_000_000
+    assert pmc["edge_gout"] == 650_000_000
