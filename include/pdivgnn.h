@@ -172,7 +172,7 @@ int pdg_decoder_fwd_fin(int n_nodes, const float* a2_prev, const double* partial
                         pdg_ln_stat* st_out, const float* ln_g, const float* ln_b, const float* x_res,
                         float* x_out, const float* Wd1, const float* bd1, float* a1d, const float* Wd2,
                         const float* bd2, const float* stats8, int scale_output, float* y, void* stream);
-/* The decoder in the cooperative layout (pdg_ebw.hip): x_out bitwise pdg_decoder_fwd's, Wd1 x_S as an
+/* The decoder in the cooperative layout (pdg_efwd.hip): x_out bitwise pdg_decoder_fwd's, Wd1 x_S as an
  * unbiased bf16x6 product from registers, a1d and y to fp32 rounding; partials != NULL: the statistics
  * reduced in-kernel as pdg_decoder_fwd_fin does (st unused), else st.  nblocks blocks of 512 threads. */
 int pdg_decoder_fwd_coop(int n_nodes, const float* a2_prev, const pdg_ln_stat* st, const double* partials,
@@ -309,7 +309,7 @@ int pdg_node_bwd_coop(int n_nodes, const float* gy, const float* a2n, const floa
                       const pdg_ln_bwd* lb, const float* ln_g, const float* Wn2T, const float* Wn1aT,
                       const float* Wn1bT, float* gz2, float* gz1, float* gaggr, float* gx_part,
                       const double* lb_pairs, int lb_npairs, int nblocks, void* stream);
-/* pdg_edge_fwd in the block-cooperative layout (pdg_ebw.hip): nblocks blocks of 512 threads, one
+/* pdg_edge_fwd in the block-cooperative layout (pdg_efwd.hip): nblocks blocks of 512 threads, one
  * contiguous row range each, Wc and W2 stationary in registers as bf16 terms, whole-row HBM access.
  * Same outputs to fp32 rounding (e_t bitwise; C = Wc e and the W2 products as unbiased bf16x6
  * products); part_m / part_e get nblocks partials.  P and Q in the pdg_pq_layout() layout (what
@@ -322,7 +322,7 @@ int pdg_edge_fwd_coop(int n_edges, const float* a2_prev, const pdg_ln_stat* st, 
 /* Inference edge forward (no layer-1 outputs: nothing reads them without a backward): pdg_edge_fwd_coop's
  * e_out, a2m, a2e (bitwise) and LayerNorm partials (the rows added in another order) from 16-row rounds with
  * one barrier per round -- the C product of round k beside the two W2 products of round k - 1, the gathers
- * one round ahead, two register sets of row loads (pdg_ebw.hip).  Arguments as pdg_edge_fwd_coop's without
+ * one round ahead, two register sets of row loads (pdg_efwd.hip).  Arguments as pdg_edge_fwd_coop's without
  * a1m / a1e. */
 int pdg_edge_fwd_infer(int n_edges, const float* a2_prev, const pdg_ln_stat* st, const float* ln_g,
                        const float* ln_b, const float* e_res, float* e_out, const int* src, const int* dst,
