@@ -192,6 +192,7 @@ def _args(name, null):
 
 @pytest.mark.parametrize("name,outputs", [
     ("pdg_edge_fwd_coop", ["e_out", "a2m", "part_m", "a2_prev", "src", "P"]),
+    ("pdg_edge_fwd_infer", ["e_out", "a2m", "part_m", "a2_prev", "src", "Q"]),
     ("pdg_edge_fwd", ["e_out", "a2m", "part_m", "dst", "Q"]),
     ("pdg_edge_bwd", ["gz2m", "gz1m", "gC", "ge_out", "dst"]),
     ("pdg_edge_bwd_w2", ["gz1m", "gC", "slabs", "gaggr"]),
