@@ -54,12 +54,13 @@ def _compile(src: Path, report: bool) -> Path:
     info = src.stem == INFO
     # an object is reused only when the CONTENT of its sources and the flags match the stamp written
     # beside it (modification times let a source restored with an older mtime link a stale object)
-    h = hashlib.sha256(" ".join(FLAGS).encode())
+    # (a --report compile embeds its extra flag in the object: its objects are never reused by a normal build)
+    h = hashlib.sha256(" ".join(FLAGS + (["--report"] if report else [])).encode())
     for d in deps:
         h.update(d.name.encode())
         h.update(d.read_bytes())
     stamp = obj.with_suffix(".stamp")
-    if obj.exists() and stamp.exists() and stamp.read_text() == h.hexdigest() and not report and not info:
+    if obj.exists() and stamp.exists() and stamp.read_text() == h.hexdigest() and not info:
         return obj
     stamp.unlink(missing_ok=True)
     cmd = [hipcc(), *FLAGS, "-c", str(src), "-o", str(obj)]
