@@ -73,7 +73,7 @@ PMC_NAMES = {"edge_fwd": ("void edge_fwd_coop_kernel<true, true", "void edge_fwd
              "edge_bwd_w2": "void edge_bwd_w2_kernel<true>",
              "edge_gout": ("void edge_gout_wc_kernel<true, true>", "void edge_gout_wc_kernel<true>"),
              "node_bwd": "node_bwd_coop_kernel", "node_pq": "void node_pq_x6_kernel<true>",
-             "gemm_sum2": "void gemm_sum2_coop_kernel<true>", "wgrad_pairs": "void wgrad_x6_pair2_kernel"}
+             "gemm_sum2": ("void gemm_sum2_coop_kernel<true, true>", "void gemm_sum2_coop_kernel<true>"), "wgrad_pairs": "void wgrad_x6_pair2_kernel"}
 PEAK_FP32_MFMA = 157.3e12   # MI355X dense fp32 MFMA, /opt/skills/guides/MI355X_MICROARCH.md
 PEAK_BF16_MFMA = 16 * PEAK_FP32_MFMA   # dense bf16 MFMA (2.5 PF; the fp32 rate is 1/16 of it, same guide)
 X6 = 6                      # bf16x6: six bf16 products per fp32-accurate product

@@ -365,21 +365,22 @@ __global__ __launch_bounds__(512) void enc_narrow_reduce_kernel(const double* __
 // the backward of the LayerNorm LN(ln_a2) whose upstream gradient is `out` (as gemm_sum2_rw).  The
 // fp32-MFMA kernel was bound by its matrix time (about half the fp32 MFMA rate at 12 waves / 168
 // VGPRs); this one does 2.7x less matrix work.
-__device__ __forceinline__ void gemm_sum2_round(f32x4 (&d)[2], const WSlice& ws0, const unsigned char* img0,
+template <int NB = 2, int TERM = X6_TERM>
+__device__ __forceinline__ void gemm_sum2_round(f32x4 (&d)[NB], const WSlice& ws0, const unsigned char* img0,
                                                 const WSlice& ws1, const unsigned char* img1) {
   const int l = lane_id(), n = l & 15, kg = l >> 4;
 #pragma unroll
-  for (int nb = 0; nb < 2; ++nb) d[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int nb = 0; nb < NB; ++nb) d[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
+    for (int nb = 0; nb < NB; ++nb) {
       const int off = x6_addr(16 * nb + n, 64 * ks + 16 * kg);
       bf16x8 B[3], C[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        B[p] = *reinterpret_cast<const bf16x8*>(img0 + p * X6_TERM + off);
-        C[p] = *reinterpret_cast<const bf16x8*>(img1 + p * X6_TERM + off);
+        B[p] = *reinterpret_cast<const bf16x8*>(img0 + p * TERM + off);
+        C[p] = *reinterpret_cast<const bf16x8*>(img1 + p * TERM + off);
       }
       f32x4 t = d[nb];
       t = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws0.a[ks][2], B[0], t, 0, 0, 0);
@@ -397,16 +398,20 @@ __device__ __forceinline__ void gemm_sum2_round(f32x4 (&d)[2], const WSlice& ws0
     }
 }
 
-template <bool COLS>
+// In 16-row rounds with two rounds of row loads in flight and one barrier per round, each round's output rows
+// stored from an fp32 tile after the next round's barrier (pdg_edge_gout_wc's structure, round 6): bitwise the
+// outputs, column partials and pairs of the 32-row two-barrier form it replaced (the same fp32 / fp64 summation
+// steps per 32-row unit), 31.0 -> 30.0 us per config-2 call (EXPERIMENTS §5).
+template <bool COLS, bool RES>
 __global__ __launch_bounds__(EBW_THREADS, 1) void gemm_sum2_coop_kernel(
     int N, const float* __restrict__ in0, const float* __restrict__ in1, const float* __restrict__ W0T,
     const float* __restrict__ W1T, const float* __restrict__ res, float* __restrict__ out,
     const float* __restrict__ ln_a2, const pdg_ln_stat* __restrict__ ln_st, double* __restrict__ part,
     const float* __restrict__ ln_g, double* __restrict__ pairs, int accumulate) {
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
-  unsigned char* img0 = sm;
-  unsigned char* img1 = sm + EBW_IMG;
-  float* t_o = reinterpret_cast<float*>(sm + 2 * EBW_IMG);
+  unsigned char* img = sm;                                        // [parity][in0, in1] 16-row images
+  float* tile = reinterpret_cast<float*>(sm + 4 * IMG16);         // [parity] output rows
+  constexpr int TL = R16 * OT_STRIDE;
   LNStat stln;
   if (COLS) stln = *reinterpret_cast<const LNStat*>(ln_st);
   const int l = lane_id(), w = wave_id();
@@ -415,67 +420,80 @@ __global__ __launch_bounds__(EBW_THREADS, 1) void gemm_sum2_coop_kernel(
   int r0, r1;
   block_rows(N, r0, r1);
   WSlice ws0, ws1;
+  const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
   double cs_g[4] = {0, 0, 0, 0}, cs_x[4] = {0, 0, 0, 0};
-  f32x4 p0[2], p1[2], pres[2], pa2[2];
-  auto issue = [&](int base) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const size_t rc = (size_t)clamp_row(base + rg + 16 * u, r1) * L + 4 * cg;
-      p0[u] = *reinterpret_cast<const f32x4*>(in0 + rc);
-      p1[u] = *reinterpret_cast<const f32x4*>(in1 + rc);
-      if (res) pres[u] = *reinterpret_cast<const f32x4*>(res + rc);
-      if (COLS) pa2[u] = *reinterpret_cast<const f32x4*>(ln_a2 + rc);
-    }
+  f32x4 sg = zero, sx = zero;
+  const __amdgpu_buffer_rsrc_t rs_out = rows_rsrc(out, r0, r1);
+  f32x4 p0[2], p1[2], pres[2], pa2[2], hres[2], hx[2];
+  auto issue = [&](int s, int base) {
+    const size_t rc = (size_t)clamp_row(base + rg, r1) * L + 4 * cg;
+    p0[s] = *reinterpret_cast<const f32x4*>(in0 + rc);
+    p1[s] = *reinterpret_cast<const f32x4*>(in1 + rc);
+    if (RES) pres[s] = *reinterpret_cast<const f32x4*>(res + rc);
+    if (COLS) pa2[s] = *reinterpret_cast<const f32x4*>(ln_a2 + rc);
   };
-  if (r0 < r1) issue(r0);
-  load_wslice(ws0, W0T, w);   // after the first round's row loads: both round trips in flight together
-  load_wslice(ws1, W1T, w);
-  for (int base = r0; base < r1; base += X6_ROWS) {
-    const f32x4 zero = f32x4{0.f, 0.f, 0.f, 0.f};
-    f32x4 rv[2], av[2];
+  auto stage = [&](const int s, const int base) {
+    const bool ok = base + rg < r1;
+    img_store4<T16>(img + (2 * s) * IMG16, rg, cg, ok ? p0[s] : zero);
+    img_store4<T16>(img + (2 * s + 1) * IMG16, rg, cg, ok ? p1[s] : zero);
+    hres[s] = RES ? pres[s] : zero;
+    if (COLS) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int r = rg + 16 * u;
-      const bool ok = base + r < r1;
-      img_store4(img0, r, cg, ok ? p0[u] : zero);
-      img_store4(img1, r, cg, ok ? p1[u] : zero);
-      rv[u] = res ? pres[u] : zero;
-      av[u] = COLS ? pa2[u] : zero;
+      for (int j = 0; j < 4; ++j) hx[s][j] = div_den(pa2[s][j] - stln.mean, stln.den, stln.rstd);
     }
-    __syncthreads();   // images complete
-    if (base + X6_ROWS < r1) issue(base + X6_ROWS);
-    f32x4 d[2];
-    gemm_sum2_round(d, ws0, img0, ws1, img1);
+    issue(s, base + X6_ROWS);
+  };
+  auto compute = [&](const int s) {
+    f32x4 d[1];
+    gemm_sum2_round<1, T16>(d, ws0, img + (2 * s) * IMG16, ws1, img + (2 * s + 1) * IMG16);
+    *reinterpret_cast<f32x4*>(tile + s * TL + (l & 15) * OT_STRIDE + oc) = d[0];
+  };
+  auto epilogue = [&](const int s, const int base) {
+    const int row = base + rg;
+    const f32x4 o = *reinterpret_cast<const f32x4*>(tile + s * TL + rg * OT_STRIDE + 4 * cg) + hres[s];
+    rows_store4(rs_out, row - r0, 4 * cg, o);
+    if (COLS && row >= r0 && row < r1) {
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) *reinterpret_cast<f32x4*>(t_o + (16 * nb + (l & 15)) * OT_STRIDE + oc) = d[nb];
-    __syncthreads();   // tile complete; the images are free for the next round
-    f32x4 sg = zero, sx = zero;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int r = rg + 16 * u;
-      const int row = base + r;
-      if (row < r1) {
-        const f32x4 o = *reinterpret_cast<const f32x4*>(t_o + r * OT_STRIDE + 4 * cg) + rv[u];
-        stg4(out + (size_t)row * L + 4 * cg, o);
-        if (COLS) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {   // the pdg_ln_colsum formulas
-            sg[j] += o[j];
-            sx[j] += o[j] * div_den(av[u][j] - stln.mean, stln.den, stln.rstd);
-          }
-        }
+      for (int j = 0; j < 4; ++j) {
+        sg[j] += o[j];
+        sx[j] += o[j] * hx[s][j];
       }
     }
+  };
+  auto fold = [&]() {
     if (COLS) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         cs_g[j] += (double)sg[j];
         cs_x[j] += (double)sx[j];
       }
+      sg = zero;
+      sx = zero;
     }
+  };
+  issue(0, r0);   // N > 0: an empty block (r0 = r1 = N) reads row N - 1
+  __builtin_amdgcn_sched_barrier(0);
+  issue(1, r0 + R16);
+  __builtin_amdgcn_sched_barrier(0);
+  load_wslice(ws0, W0T, w);
+  load_wslice(ws1, W1T, w);
+  int last = r0 - X6_ROWS;
+  for (int base = r0; base < r1; base += X6_ROWS) {
+    stage(0, base);
+    __syncthreads();
+    compute(0);
+    epilogue(1, base - R16);
+    fold();
+    stage(1, base + R16);
+    __syncthreads();
+    compute(1);
+    epilogue(0, base);
+    last = base;
   }
+  __syncthreads();
+  epilogue(1, last + R16);
+  fold();
   if (COLS) {
-    // block partial = the 16 row groups' column sums, reduced in order through LDS
     double* red = reinterpret_cast<double*>(sm);
     __syncthreads();
 #pragma unroll
@@ -1149,20 +1167,21 @@ extern "C" int pdg_gemm_sum2_coop(int rows, const float* in0, const float* in1, 
   PDG_CHECK_ARG(PDG_ALIGNED(in0) && PDG_ALIGNED(in1) && PDG_ALIGNED(out) && PDG_ALIGNED(W0T) && PDG_ALIGNED(W1T) &&
                     PDG_ALIGNED(res),
                 "pdg_gemm_sum2_coop: misaligned pointer");
-  // LDS: the two images, then the row tile / (COLS) the row groups' sums + one row + its scratch
-  const size_t tile = (size_t)EFC_TILE * sizeof(float);
+  // LDS: two rounds' images + two output tiles; afterwards (COLS) the row groups' sums + one row + its scratch
+  const size_t pipe = 4 * IMG16 + (size_t)2 * R16 * OT_STRIDE * sizeof(float);
   const size_t cols = ((size_t)EBW_THREADS / 32 + 2) * 2 * L * sizeof(double);
+  hipStream_t s = (hipStream_t)stream;
+#define PDG_GS2(C, R)                                                                                          \
+  hipLaunchKernelGGL((gemm_sum2_coop_kernel<C, R>), dim3(nblocks), dim3(EBW_THREADS), C ? (pipe > cols ? pipe : cols) \
+                     : pipe, s, rows, in0, in1, W0T, W1T, res, out, ln_a2, ln_st, partials, ln_g, pairs, accumulate)
   if (partials) {
     PDG_CHECK_ARG(ln_a2 && ln_st && PDG_ALIGNED(ln_a2) && (!pairs || ln_g),
                   "pdg_gemm_sum2_coop: column partials need an aligned ln_a2, ln_st (and ln_g for pairs)");
-    const size_t shm = 2 * EBW_IMG + tile > cols ? 2 * EBW_IMG + tile : cols;
-    hipLaunchKernelGGL(gemm_sum2_coop_kernel<true>, dim3(nblocks), dim3(EBW_THREADS), shm, (hipStream_t)stream, rows,
-                       in0, in1, W0T, W1T, res, out, ln_a2, ln_st, partials, ln_g, pairs, accumulate);
+    if (res) PDG_GS2(true, true); else PDG_GS2(true, false);
   } else {
-    hipLaunchKernelGGL(gemm_sum2_coop_kernel<false>, dim3(nblocks), dim3(EBW_THREADS), 2 * EBW_IMG + tile,
-                       (hipStream_t)stream, rows, in0, in1, W0T, W1T, res, out, nullptr, nullptr, nullptr, nullptr,
-                       nullptr, 0);
+    if (res) PDG_GS2(false, true); else PDG_GS2(false, false);
   }
+#undef PDG_GS2
   PDG_CHECK_LAUNCH("pdg_gemm_sum2_coop");
   return PDG_OK;
 }

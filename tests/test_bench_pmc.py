@@ -136,7 +136,9 @@ def test_pmc_names_cover_the_shipped_instantiations(tmp_path):
         "_meta": {"tree": "aaaa"},
         "void edge_fwd_infer_kernel<true, true, true>(int, ...)": {"total": 1.75e9},
         "void edge_gout_wc_kernel<true, true>(float const*, ...)": {"total": 6.5e8},
-        "void edge_gout_wc_kernel<false, true>(float const*, ...)": {"total": 1.0}}))
+        "void edge_gout_wc_kernel<false, true>(float const*, ...)": {"total": 1.0},
+        "void gemm_sum2_coop_kernel<true, true>(int, ...)": {"total": 1.06e8}}))
     pmc = bench.load_pmc(True, p)
     assert pmc["edge_fwd"] == 1_750_000_000
     assert pmc["edge_gout"] == 650_000_000
+    assert pmc["gemm_sum2"] == 106_000_000

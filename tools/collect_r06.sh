@@ -38,7 +38,7 @@ w = json.load(open('profiles/r06_rocprof_window.json'))
 sq = {k['kernel']: k for k in s}; ks = w['kernels']
 for wn in ['edge_bwd_w2_kernel<true>', 'edge_fwd_coop_kernel<true, true, true>', 'edge_gout_wc_kernel<true, true>',
            'pq_scatter_bwd_kernel<true>', 'node_bwd_coop_kernel', 'segment_sum_kernel', 'node_net_x6_kernel',
-           'gemm_sum2_coop_kernel<true>', 'node_pq_x6_kernel<true>', 'ln_colsum_nodes_kernel']:
+           'gemm_sum2_coop_kernel<true, true>', 'node_pq_x6_kernel<true>', 'ln_colsum_nodes_kernel']:
     n = [k for k in ks if wn in k][0]; v = ks[n]; mb = p[n]['total'] / 1e6
     b = sq.get(n, {}).get('mfma_busy_at_2.4GHz')
     print(f"| `{n.split('(')[0].replace('void ', '')}` | {v['calls_per_step']:.0f} | {v['avg_us']:.1f} | "
